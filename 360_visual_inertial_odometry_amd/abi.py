@@ -1,0 +1,219 @@
+"""ctypes mirror of include/vio360.h (the C-ABI boundary).
+
+Only plain C types cross the boundary; the structures below must stay byte-identical to the
+header (checked by tests/test_abi.py against offsetof values compiled from the header).
+"""
+import ctypes as C
+
+import numpy as np
+
+VIO_BA_LOCAL, VIO_BA_FULL, VIO_BA_VI, VIO_PNP = 0, 1, 2, 3
+VIO_TERM_CONVERGENCE, VIO_TERM_NO_CONVERGENCE, VIO_TERM_FAILURE = 0, 1, 2
+
+_u8p = C.POINTER(C.c_uint8)
+_i32p = C.POINTER(C.c_int32)
+_f32p = C.POINTER(C.c_float)
+_f64p = C.POINTER(C.c_double)
+
+
+class VioPose(C.Structure):
+    _fields_ = [("R", C.c_double * 9), ("t", C.c_double * 3)]
+
+
+class VioPreint(C.Structure):
+    _fields_ = [
+        ("delta_R", C.c_float * 9), ("delta_V", C.c_float * 3), ("delta_P", C.c_float * 3),
+        ("J_Rg", C.c_float * 9), ("J_Vg", C.c_float * 9), ("J_Va", C.c_float * 9),
+        ("J_Pg", C.c_float * 9), ("J_Pa", C.c_float * 9),
+        ("cov9", C.c_float * 81), ("gyro_bias", C.c_float * 3), ("accel_bias", C.c_float * 3),
+        ("_pad", C.c_float * 2), ("dt_total", C.c_double),
+    ]
+
+
+class VioBaProblem(C.Structure):
+    _fields_ = [
+        ("variant", C.c_int32), ("num_kf", C.c_int32), ("num_lm", C.c_int32), ("num_obs", C.c_int32),
+        ("cols", C.c_double), ("rows", C.c_double), ("huber_delta", C.c_double),
+        ("info", C.c_double * 4), ("chi2_threshold", C.c_double),
+        ("T_cb", C.POINTER(VioPose)), ("T_wb_init", C.POINTER(VioPose)),
+        ("kf_const", _u8p), ("lm_const", _u8p), ("lm_marg", _u8p),
+        ("lm_xyz", _f64p), ("obs_kf", _i32p), ("obs_lm", _i32p), ("obs_uv", _f32p),
+        ("preint", C.POINTER(VioPreint)), ("preint_valid", _u8p), ("vel", _f64p),
+        ("bg", C.c_double * 3), ("ba", C.c_double * 3), ("gravity", C.c_double * 3),
+        ("max_iterations", C.c_int32), ("fixed_iterations", C.c_int32),
+        ("num_rounds", C.c_int32), ("_pad0", C.c_int32),
+    ]
+
+
+class VioBaSummary(C.Structure):
+    _fields_ = [
+        ("success", C.c_int32), ("termination", C.c_int32), ("iterations", C.c_int32),
+        ("num_successful_steps", C.c_int32), ("num_unsuccessful_steps", C.c_int32),
+        ("num_inliers", C.c_int32), ("num_outliers", C.c_int32), ("num_bad_lm", C.c_int32),
+        ("initial_cost", C.c_double), ("final_cost", C.c_double), ("fixed_cost", C.c_double),
+        ("_pad1", C.c_double),
+    ]
+
+
+class VioBaOutput(C.Structure):
+    _fields_ = [
+        ("T_wb", C.POINTER(VioPose)), ("lm_xyz", _f64p), ("obs_chi2", _f64p), ("obs_outlier", _u8p),
+        ("lm_bad", _u8p), ("vel", _f64p), ("bg", _f64p), ("ba", _f64p),
+        ("summary", C.POINTER(VioBaSummary)),
+    ]
+
+
+class ErpKltParams(C.Structure):
+    _fields_ = [("win", C.c_int32), ("max_level", C.c_int32), ("max_iters", C.c_int32),
+                ("epsilon", C.c_float), ("min_eig_threshold", C.c_float), ("_pad", C.c_int32)]
+
+
+class ErpTrackerParams(C.Structure):
+    _fields_ = [("n_pts", C.c_int32), ("ransac_iters", C.c_int32), ("ransac_thresh_rad", C.c_float),
+                ("max_corners", C.c_int32), ("quality", C.c_double), ("min_dist", C.c_double),
+                ("boundary_margin", C.c_int32), ("polar_ratio", C.c_float)]
+
+
+def default_klt_params():
+    """FeatureTracker's hard-coded LK settings (src/processing/FeatureTracker.cpp:33-35,240)."""
+    return ErpKltParams(21, 3, 30, 0.01, 0.01, 0)
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype)) if a is not None else None
+
+
+def poses_to_c(T):
+    """(K,4,4) or (K,3,4) float array -> ctypes array of VioPose (f64)."""
+    T = np.asarray(T, dtype=np.float64)
+    arr = (VioPose * len(T))()
+    for k in range(len(T)):
+        arr[k].R[:] = T[k, :3, :3].reshape(-1).tolist()
+        arr[k].t[:] = T[k, :3, 3].tolist()
+    return arr
+
+
+def poses_from_c(arr, K):
+    out = np.zeros((K, 4, 4))
+    for k in range(K):
+        out[k, :3, :3] = np.array(arr[k].R[:]).reshape(3, 3)
+        out[k, :3, 3] = arr[k].t[:]
+        out[k, 3, 3] = 1.0
+    return out
+
+
+def preints_to_c(preints):
+    """list (len K, entry 0 may be None) of dicts -> (VioPreint array, valid u8 array)."""
+    K = len(preints)
+    arr = (VioPreint * K)()
+    valid = np.zeros(K, np.uint8)
+    for k, p in enumerate(preints):
+        if p is None:
+            continue
+        valid[k] = 1
+        e = arr[k]
+        e.delta_R[:] = np.asarray(p["delta_R"], np.float32).reshape(-1).tolist()
+        e.delta_V[:] = np.asarray(p["delta_V"], np.float32).tolist()
+        e.delta_P[:] = np.asarray(p["delta_P"], np.float32).tolist()
+        for nm in ("J_Rg", "J_Vg", "J_Va", "J_Pg", "J_Pa"):
+            getattr(e, nm)[:] = np.asarray(p[nm], np.float32).reshape(-1).tolist()
+        e.cov9[:] = np.asarray(p["cov"], np.float32)[:9, :9].reshape(-1).tolist()
+        e.gyro_bias[:] = np.asarray(p["gyro_bias"], np.float32).tolist()
+        e.accel_bias[:] = np.asarray(p["accel_bias"], np.float32).tolist()
+        e.dt_total = float(p["dt_total"])
+    return arr, valid
+
+
+class BaProblem:
+    """Owns numpy buffers + the ctypes struct pointing at them (keeps everything alive)."""
+
+    def __init__(self, window, variant=VIO_BA_LOCAL, max_iterations=50, fixed_iterations=0,
+                 chi2_threshold=None, num_rounds=4, huber_delta=1.0):
+        w = window
+        self.K = int(len(w["T_wb_init"]))
+        self.L = int(len(w["lm_xyz"]))
+        self.N = int(len(w["obs_kf"]))
+        self.variant = variant
+        self.T_cb = poses_to_c(w["T_cb"] if np.ndim(w["T_cb"]) == 3 else np.repeat(np.asarray(w["T_cb"])[None], self.K, 0))
+        self.T_wb_init = poses_to_c(w["T_wb_init"])
+        self.kf_const = np.ascontiguousarray(w["kf_const"], np.uint8)
+        self.lm_const = np.ascontiguousarray(w["lm_const"], np.uint8)
+        self.lm_marg = np.ascontiguousarray(w.get("lm_marg", np.zeros(self.L, np.uint8)), np.uint8)
+        self.lm_xyz = np.ascontiguousarray(w["lm_xyz"], np.float64).reshape(-1)
+        self.obs_kf = np.ascontiguousarray(w["obs_kf"], np.int32)
+        self.obs_lm = np.ascontiguousarray(w["obs_lm"], np.int32)
+        self.obs_uv = np.ascontiguousarray(w["obs_uv"], np.float32).reshape(-1)
+        p = VioBaProblem()
+        p.variant = variant
+        p.num_kf, p.num_lm, p.num_obs = self.K, self.L, self.N
+        p.cols, p.rows = float(w["cols"]), float(w["rows"])
+        p.huber_delta = huber_delta
+        p.info[:] = [1.0, 0.0, 0.0, 1.0]
+        if chi2_threshold is None:
+            chi2_threshold = 5.99146 if variant == VIO_BA_LOCAL else 5.991
+        p.chi2_threshold = chi2_threshold
+        p.T_cb = C.cast(self.T_cb, C.POINTER(VioPose))
+        p.T_wb_init = C.cast(self.T_wb_init, C.POINTER(VioPose))
+        p.kf_const = _ptr(self.kf_const, C.c_uint8)
+        p.lm_const = _ptr(self.lm_const, C.c_uint8)
+        p.lm_marg = _ptr(self.lm_marg, C.c_uint8)
+        p.lm_xyz = _ptr(self.lm_xyz, C.c_double)
+        p.obs_kf = _ptr(self.obs_kf, C.c_int32)
+        p.obs_lm = _ptr(self.obs_lm, C.c_int32)
+        p.obs_uv = _ptr(self.obs_uv, C.c_float)
+        if variant == VIO_BA_VI:
+            self.preint, self.preint_valid = preints_to_c(w["preint"])
+            self.vel = np.ascontiguousarray(w["vel"], np.float64).reshape(-1)
+            p.preint = C.cast(self.preint, C.POINTER(VioPreint))
+            p.preint_valid = _ptr(self.preint_valid, C.c_uint8)
+            p.vel = _ptr(self.vel, C.c_double)
+            p.bg[:] = list(np.asarray(w.get("bg", np.zeros(3)), np.float64))
+            p.ba[:] = list(np.asarray(w.get("ba", np.zeros(3)), np.float64))
+            p.gravity[:] = list(np.asarray(w["gravity"], np.float64))
+        p.max_iterations = max_iterations
+        p.fixed_iterations = fixed_iterations
+        p.num_rounds = num_rounds
+        self.c = p
+
+
+class BaOutput:
+    def __init__(self, K, L, N):
+        self.K, self.L, self.N = K, L, N
+        self.T_wb = (VioPose * K)()
+        self.lm_xyz = np.zeros(3 * max(L, 1))
+        self.obs_chi2 = np.zeros(max(N, 1))
+        self.obs_outlier = np.zeros(max(N, 1), np.uint8)
+        self.lm_bad = np.zeros(max(L, 1), np.uint8)
+        self.vel = np.zeros(3 * K)
+        self.bg = np.zeros(3)
+        self.ba = np.zeros(3)
+        self.summary = VioBaSummary()
+        o = VioBaOutput()
+        o.T_wb = C.cast(self.T_wb, C.POINTER(VioPose))
+        o.lm_xyz = _ptr(self.lm_xyz, C.c_double)
+        o.obs_chi2 = _ptr(self.obs_chi2, C.c_double)
+        o.obs_outlier = _ptr(self.obs_outlier, C.c_uint8)
+        o.lm_bad = _ptr(self.lm_bad, C.c_uint8)
+        o.vel = _ptr(self.vel, C.c_double)
+        o.bg = _ptr(self.bg, C.c_double)
+        o.ba = _ptr(self.ba, C.c_double)
+        o.summary = C.pointer(self.summary)
+        self.c = o
+
+    def result(self):
+        s = self.summary
+        return {
+            "T_wb": poses_from_c(self.T_wb, self.K),
+            "lm_xyz": self.lm_xyz[: 3 * self.L].reshape(-1, 3).copy(),
+            "obs_chi2": self.obs_chi2[: self.N].copy(),
+            "obs_outlier": self.obs_outlier[: self.N].copy(),
+            "lm_bad": self.lm_bad[: self.L].copy(),
+            "vel": self.vel.reshape(-1, 3).copy(),
+            "bg": self.bg.copy(),
+            "ba": self.ba.copy(),
+            "success": s.success, "termination": s.termination, "iterations": s.iterations,
+            "num_successful_steps": s.num_successful_steps,
+            "num_unsuccessful_steps": s.num_unsuccessful_steps,
+            "num_inliers": s.num_inliers, "num_outliers": s.num_outliers, "num_bad_lm": s.num_bad_lm,
+            "initial_cost": s.initial_cost, "final_cost": s.final_cost, "fixed_cost": s.fixed_cost,
+        }

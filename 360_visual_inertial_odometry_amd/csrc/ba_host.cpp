@@ -1,0 +1,526 @@
+// ba_host.cpp — C-ABI entry points for bundle adjustment (vio_ba_*), host side.
+//
+// Packs vio_ba_problem windows into the pooled device layout of ba_types.h, uploads them, launches
+// one workgroup per window (ba_kernel.hip) and scatters the results back.  The packing applies
+// Ceres' problem reduction (program.cc:305-400): constant parameter blocks and residual blocks
+// whose parameters are all constant leave the optimisation, and the surviving blocks get their
+// offsets in the reduced (Schur) system.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ba_types.h"
+#include "ctx.h"
+
+namespace vio360 {
+
+hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream);
+size_t ba_ws_extra_doubles();
+
+void set_error(vio_ctx* ctx, const std::string& msg) {
+    if (ctx) ctx->last_error = msg;
+}
+int hip_fail(vio_ctx* ctx, hipError_t e, const char* what) {
+    set_error(ctx, std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? VIO_ENOMEM : VIO_EDEVICE;
+}
+void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes) {
+    if ((int)ctx->bufs.size() <= slot) {
+        ctx->bufs.resize(slot + 1, nullptr);
+        ctx->caps.resize(slot + 1, 0);
+    }
+    if (ctx->caps[slot] >= bytes && ctx->bufs[slot]) return ctx->bufs[slot];
+    if (ctx->bufs[slot]) hipFree(ctx->bufs[slot]);
+    ctx->bufs[slot] = nullptr;
+    ctx->caps[slot] = 0;
+    size_t cap = std::max<size_t>(bytes, 256);
+    if (hipMalloc(&ctx->bufs[slot], cap) != hipSuccess) return nullptr;
+    ctx->caps[slot] = cap;
+    return ctx->bufs[slot];
+}
+
+namespace {
+
+// host image of a packed batch
+struct Packed {
+    std::vector<BaWin> win;
+    std::vector<double> pose_raw, lm_xyz0, vel0;
+    std::vector<uint8_t> kf_const, lm_var, lm_marg, preint_valid;
+    std::vector<int32_t> lm_ptr, obs_kf, obs_lm, kf_ptr, kf_obs;
+    std::vector<float> obs_uv;
+    std::vector<vio_preint> preint;
+    std::vector<std::vector<int32_t>> perm;  // per window: sorted position -> original obs index
+    int64_t ws_total = 0, out_total = 0, N_total = 0, L_total = 0;
+};
+
+int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
+    const int K = p.num_kf, L = p.num_lm, N = p.num_obs;
+    if (K <= 0 || L < 0 || N < 0) { set_error(ctx, "invalid sizes"); return VIO_EINVAL; }
+    if (p.variant < VIO_BA_LOCAL || p.variant > VIO_PNP) { set_error(ctx, "unknown variant"); return VIO_EINVAL; }
+    if (K > BA_KMAX) { set_error(ctx, "num_kf > 16 is not supported on the windowed path"); return VIO_ENOSYS; }
+    const bool vi = p.variant == VIO_BA_VI, pnp = p.variant == VIO_PNP;
+    if (vi && K > 10) { set_error(ctx, "VIBA windows support num_kf <= 10"); return VIO_ENOSYS; }
+    if (!p.T_cb || !p.T_wb_init || !p.kf_const || (L > 0 && (!p.lm_const || !p.lm_xyz)) ||
+        (N > 0 && (!p.obs_kf || !p.obs_lm || !p.obs_uv))) {
+        set_error(ctx, "null input array");
+        return VIO_EINVAL;
+    }
+    if (vi && (!p.preint || !p.preint_valid || !p.vel)) { set_error(ctx, "VIBA needs preint/preint_valid/vel"); return VIO_EINVAL; }
+    if (p.max_iterations < 0) { set_error(ctx, "max_iterations < 0"); return VIO_EINVAL; }
+    for (int o = 0; o < N; ++o) {
+        if (p.obs_kf[o] < 0 || p.obs_kf[o] >= K || p.obs_lm[o] < 0 || p.obs_lm[o] >= L) {
+            set_error(ctx, "observation index out of range");
+            return VIO_EINVAL;
+        }
+    }
+    // one observation per (keyframe, landmark): MapPoint::AddObservation keeps one per frame
+    {
+        std::vector<int64_t> key(N);
+        for (int o = 0; o < N; ++o) key[o] = (int64_t)p.obs_lm[o] * K + p.obs_kf[o];
+        std::sort(key.begin(), key.end());
+        for (int o = 1; o < N; ++o)
+            if (key[o] == key[o - 1]) {
+                set_error(ctx, "duplicate (keyframe, landmark) observation");
+                return VIO_EINVAL;
+            }
+    }
+    BaWin w;
+    std::memset(&w, 0, sizeof w);
+    w.K = K; w.L = L; w.N = N; w.variant = p.variant;
+    w.is_vi = vi; w.is_pnp = pnp;
+    w.max_iter = p.max_iterations;
+    w.fixed_iter = p.fixed_iterations;
+    w.rounds = pnp ? (p.num_rounds > 0 ? p.num_rounds : 4) : 1;
+    w.cols = p.cols; w.rows = p.rows; w.huber = p.huber_delta; w.chi2_thr = p.chi2_threshold;
+    for (int i = 0; i < 4; ++i) w.info[i] = p.info[i];
+    {   // chol(info) lower (Eigen LLT of the 2x2), identity fallback
+        double a = p.info[0], b = p.info[2], d = p.info[3];
+        w.Lw[0] = 1; w.Lw[1] = 0; w.Lw[2] = 0; w.Lw[3] = 1;
+        if (a > 0) {
+            double l00 = std::sqrt(a), l10 = b / l00, t = d - l10 * l10;
+            if (t > 0) { w.Lw[0] = l00; w.Lw[2] = l10; w.Lw[3] = std::sqrt(t); }
+        }
+    }
+    if (vi) for (int i = 0; i < 3; ++i) { w.gravity[i] = p.gravity[i]; w.bg0[i] = p.bg[i]; w.ba0[i] = p.ba[i]; }
+    // reduced problem: which blocks are free and used
+    std::vector<uint8_t> pose_used(K, 0), lm_used(L, 0), vel_used(K, 0);
+    bool bias_used = false;
+    for (int o = 0; o < N; ++o) {
+        int k = p.obs_kf[o], l = p.obs_lm[o];
+        bool kvar = !p.kf_const[k], lvar = !pnp && !p.lm_const[l];
+        if (kvar) pose_used[k] = 1;
+        if (lvar) lm_used[l] = 1;
+    }
+    if (vi) {
+        for (int k = 1; k < K; ++k) {
+            if (!p.preint_valid[k]) continue;
+            vel_used[k - 1] = vel_used[k] = 1;
+            bias_used = true;
+            if (!p.kf_const[k - 1]) pose_used[k - 1] = 1;
+            if (!p.kf_const[k]) pose_used[k] = 1;
+        }
+    }
+    int off = 0, P = 0;
+    for (int k = 0; k < BA_KMAX; ++k) { w.pose_f[k] = -1; w.vel_f[k] = -1; }
+    for (int k = 0; k < K; ++k)
+        if (pose_used[k]) { w.pose_f[k] = off; off += 6; P++; }
+    w.np = off;
+    for (int k = 0; k < K; ++k)
+        if (vel_used[k]) { w.vel_f[k] = off; off += 3; }
+    w.bg_f = bias_used ? off : -1; if (bias_used) off += 3;
+    w.ba_f = bias_used ? off : -1; if (bias_used) off += 3;
+    w.nf = off;
+    w.ni = w.nf - w.np;
+    if (w.nf > BA_NF_MAX) { set_error(ctx, "reduced system larger than 96 parameters"); return VIO_ENOSYS; }
+    w.T = (w.np + 1 + 15) / 16;
+    if (w.T < 1) w.T = 1;
+    w.npad = 16 * w.T;
+    w.n_imu = 0;
+    if (vi) for (int k = 1; k < K; ++k) w.n_imu += p.preint_valid[k] ? 1 : 0;
+    // offsets
+    w.o_pose = (int64_t)pk.kf_const.size();
+    w.o_lm = (int64_t)pk.lm_var.size();
+    w.o_lmptr = (int64_t)pk.lm_ptr.size();
+    w.o_obs = (int64_t)pk.obs_kf.size();
+    w.o_kfptr = (int64_t)pk.kf_ptr.size();
+    w.o_ws = pk.ws_total;
+    w.o_out = pk.out_total;
+    BaWsLayout WL = ba_ws_layout(K, L, N);
+    pk.ws_total += WL.total + (int64_t)ba_ws_extra_doubles();
+    pk.ws_total = (pk.ws_total + 31) & ~(int64_t)31;
+    pk.out_total += ba_out_layout(K, L, N).total;
+    // poses
+    for (int k = 0; k < K; ++k) {
+        for (int i = 0; i < 9; ++i) pk.pose_raw.push_back(p.T_wb_init[k].R[i]);
+        for (int i = 0; i < 3; ++i) pk.pose_raw.push_back(p.T_wb_init[k].t[i]);
+        for (int i = 0; i < 9; ++i) pk.pose_raw.push_back(p.T_cb[k].R[i]);
+        for (int i = 0; i < 3; ++i) pk.pose_raw.push_back(p.T_cb[k].t[i]);
+        pk.kf_const.push_back(p.kf_const[k] ? 1 : 0);
+        if (vi) {
+            pk.preint.push_back(p.preint[k]);
+            pk.preint_valid.push_back(k >= 1 && p.preint_valid[k] ? 1 : 0);
+            for (int i = 0; i < 3; ++i) pk.vel0.push_back(p.vel[3 * k + i]);
+        } else {
+            vio_preint z;
+            std::memset(&z, 0, sizeof z);
+            pk.preint.push_back(z);
+            pk.preint_valid.push_back(0);
+            for (int i = 0; i < 3; ++i) pk.vel0.push_back(0.0);
+        }
+    }
+    // landmarks
+    const uint8_t* marg = pnp ? p.lm_const : p.lm_marg;
+    for (int l = 0; l < L; ++l) {
+        for (int i = 0; i < 3; ++i) pk.lm_xyz0.push_back(p.lm_xyz[3 * l + i]);
+        pk.lm_var.push_back(lm_used[l]);
+        pk.lm_marg.push_back(marg ? (marg[l] ? 1 : 0) : 0);
+    }
+    // observations sorted by landmark (stable)
+    std::vector<int32_t> perm(N);
+    for (int o = 0; o < N; ++o) perm[o] = o;
+    std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return p.obs_lm[a] < p.obs_lm[b]; });
+    std::vector<int32_t> lptr(L + 1, 0);
+    for (int o = 0; o < N; ++o) lptr[p.obs_lm[o] + 1]++;
+    for (int l = 0; l < L; ++l) lptr[l + 1] += lptr[l];
+    pk.lm_ptr.insert(pk.lm_ptr.end(), lptr.begin(), lptr.end());
+    for (int q = 0; q < N; ++q) {
+        int o = perm[q];
+        pk.obs_kf.push_back(p.obs_kf[o]);
+        pk.obs_lm.push_back(p.obs_lm[o]);
+        pk.obs_uv.push_back(p.obs_uv[2 * o]);
+        pk.obs_uv.push_back(p.obs_uv[2 * o + 1]);
+    }
+    std::vector<int32_t> kptr(K + 1, 0);
+    for (int q = 0; q < N; ++q) kptr[p.obs_kf[perm[q]] + 1]++;
+    for (int k = 0; k < K; ++k) kptr[k + 1] += kptr[k];
+    std::vector<int32_t> fill(K, 0), kobs(N);
+    for (int q = 0; q < N; ++q) {
+        int k = p.obs_kf[perm[q]];
+        kobs[kptr[k] + fill[k]++] = q;
+    }
+    pk.kf_ptr.insert(pk.kf_ptr.end(), kptr.begin(), kptr.end());
+    pk.kf_obs.insert(pk.kf_obs.end(), kobs.begin(), kobs.end());
+    pk.perm.push_back(std::move(perm));
+    pk.win.push_back(w);
+    pk.N_total += N;
+    pk.L_total += L;
+    return VIO_OK;
+}
+
+template <class T>
+size_t bytes_of(const std::vector<T>& v) { return v.size() * sizeof(T); }
+
+}  // namespace
+
+// device image of a batch
+struct BaDevice {
+    int n = 0;
+    Packed pk;
+    // device allocations (owned)
+    std::vector<void*> allocs;
+    BaPools P{};
+    void* prof_buf = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double ms_sum = 0.0;
+    int ms_count = 0;
+    bool timing_pending = false;
+};
+
+static int upload_batch(vio_ctx* ctx, BaDevice& d) {
+    Packed& pk = d.pk;
+    auto up = [&](const void* src, size_t bytes, void** dst) -> int {
+        size_t b = std::max<size_t>(bytes, 16);
+        void* p = nullptr;
+        VIO_HIP(ctx, hipMalloc(&p, b));
+        d.allocs.push_back(p);
+        if (bytes) VIO_HIP(ctx, hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+        *dst = p;
+        return VIO_OK;
+    };
+    void* ptr;
+    int rc;
+#define UP(vec, field, type)                                                  \
+    if ((rc = up(vec.data(), bytes_of(vec), &ptr)) != VIO_OK) return rc;      \
+    d.P.field = (type)ptr;
+    UP(pk.win, win, const BaWin*);
+    UP(pk.pose_raw, pose_raw, const double*);
+    UP(pk.kf_const, kf_const, const uint8_t*);
+    UP(pk.lm_xyz0, lm_xyz0, const double*);
+    UP(pk.lm_var, lm_var, const uint8_t*);
+    UP(pk.lm_marg, lm_marg, const uint8_t*);
+    UP(pk.lm_ptr, lm_ptr, const int32_t*);
+    UP(pk.obs_kf, obs_kf, const int32_t*);
+    UP(pk.obs_lm, obs_lm, const int32_t*);
+    UP(pk.obs_uv, obs_uv, const float*);
+    UP(pk.kf_ptr, kf_ptr, const int32_t*);
+    UP(pk.kf_obs, kf_obs, const int32_t*);
+    UP(pk.preint, preint, const vio_preint*);
+    UP(pk.preint_valid, preint_valid, const uint8_t*);
+    UP(pk.vel0, vel0, const double*);
+#undef UP
+    auto alloc = [&](size_t bytes, void** dst) -> int {
+        void* p = nullptr;
+        VIO_HIP(ctx, hipMalloc(&p, std::max<size_t>(bytes, 16)));
+        d.allocs.push_back(p);
+        *dst = p;
+        return VIO_OK;
+    };
+    if ((rc = alloc(sizeof(double) * pk.ws_total, &ptr)) != VIO_OK) return rc;
+    d.P.ws = (double*)ptr;
+    if ((rc = alloc(sizeof(double) * pk.out_total, &ptr)) != VIO_OK) return rc;
+    d.P.out = (double*)ptr;
+    if ((rc = alloc(pk.N_total, &ptr)) != VIO_OK) return rc;
+    d.P.out_u8 = (uint8_t*)ptr;
+    if ((rc = alloc(pk.L_total, &ptr)) != VIO_OK) return rc;
+    d.P.out_bad = (uint8_t*)ptr;
+    if ((rc = alloc(sizeof(int32_t) * SI_COUNT * d.n, &ptr)) != VIO_OK) return rc;
+    d.P.out_i32 = (int32_t*)ptr;
+    if ((rc = alloc(sizeof(double) * SD_COUNT * d.n, &ptr)) != VIO_OK) return rc;
+    d.P.out_sum = (double*)ptr;
+    VIO_HIP(ctx, hipEventCreate(&d.ev0));
+    VIO_HIP(ctx, hipEventCreate(&d.ev1));
+    return VIO_OK;
+}
+
+static void free_batch(BaDevice& d) {
+    for (void* p : d.allocs) hipFree(p);
+    d.allocs.clear();
+    if (d.prof_buf) hipFree(d.prof_buf);
+    d.prof_buf = nullptr;
+    if (d.ev0) hipEventDestroy(d.ev0);
+    if (d.ev1) hipEventDestroy(d.ev1);
+    d.ev0 = d.ev1 = nullptr;
+}
+
+static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
+    Packed& pk = d.pk;
+    std::vector<double> out(pk.out_total);
+    std::vector<uint8_t> u8(pk.N_total), bad(pk.L_total);
+    std::vector<int32_t> si(SI_COUNT * d.n);
+    std::vector<double> sd(SD_COUNT * d.n);
+    VIO_HIP(ctx, hipMemcpyAsync(out.data(), d.P.out, sizeof(double) * out.size(), hipMemcpyDeviceToHost, ctx->stream));
+    VIO_HIP(ctx, hipMemcpyAsync(u8.data(), d.P.out_u8, u8.size(), hipMemcpyDeviceToHost, ctx->stream));
+    VIO_HIP(ctx, hipMemcpyAsync(bad.data(), d.P.out_bad, bad.size(), hipMemcpyDeviceToHost, ctx->stream));
+    VIO_HIP(ctx, hipMemcpyAsync(si.data(), d.P.out_i32, sizeof(int32_t) * si.size(), hipMemcpyDeviceToHost, ctx->stream));
+    VIO_HIP(ctx, hipMemcpyAsync(sd.data(), d.P.out_sum, sizeof(double) * sd.size(), hipMemcpyDeviceToHost, ctx->stream));
+    VIO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < d.n; ++i) {
+        const BaWin& w = pk.win[i];
+        vio_ba_output& o = outs[i];
+        BaOutLayout OL = ba_out_layout(w.K, w.L, w.N);
+        const double* ob = out.data() + w.o_out;
+        if (o.T_wb)
+            for (int k = 0; k < w.K; ++k) {
+                std::memcpy(o.T_wb[k].R, ob + OL.T_wb + 12 * k, 9 * sizeof(double));
+                std::memcpy(o.T_wb[k].t, ob + OL.T_wb + 12 * k + 9, 3 * sizeof(double));
+            }
+        if (o.lm_xyz) std::memcpy(o.lm_xyz, ob + OL.lm, sizeof(double) * 3 * w.L);
+        const std::vector<int32_t>& perm = pk.perm[i];
+        for (int q = 0; q < w.N; ++q) {
+            if (o.obs_chi2) o.obs_chi2[perm[q]] = ob[OL.chi2 + q];
+            if (o.obs_outlier) o.obs_outlier[perm[q]] = u8[w.o_obs + q];
+        }
+        if (o.lm_bad) std::memcpy(o.lm_bad, bad.data() + w.o_lm, w.L);
+        if (w.is_vi) {
+            if (o.vel) std::memcpy(o.vel, ob + OL.vel, sizeof(double) * 3 * w.K);
+            if (o.bg) std::memcpy(o.bg, ob + OL.bias, sizeof(double) * 3);
+            if (o.ba) std::memcpy(o.ba, ob + OL.bias + 3, sizeof(double) * 3);
+        }
+        if (o.summary) {
+            vio_ba_summary& s = *o.summary;
+            std::memset(&s, 0, sizeof s);
+            const int32_t* a = si.data() + SI_COUNT * i;
+            const double* b = sd.data() + SD_COUNT * i;
+            s.success = a[SI_SUCCESS];
+            s.termination = a[SI_TERM];
+            s.iterations = a[SI_ITERS];
+            s.num_successful_steps = a[SI_NSUCC];
+            s.num_unsuccessful_steps = a[SI_NUNSUCC];
+            s.num_inliers = a[SI_NIN];
+            s.num_outliers = a[SI_NOUT];
+            s.num_bad_lm = a[SI_NBAD];
+            s.initial_cost = b[SD_INIT];
+            s.final_cost = b[SD_FINAL];
+            s.fixed_cost = b[SD_FIXED];
+        }
+    }
+    return VIO_OK;
+}
+
+static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
+    if (timed) VIO_HIP(ctx, hipEventRecord(d.ev0, ctx->stream));
+    hipError_t e = launch_ba_windows(d.P, d.n, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "ba_window_kernel launch");
+    if (timed) {
+        VIO_HIP(ctx, hipEventRecord(d.ev1, ctx->stream));
+        d.timing_pending = true;
+    }
+    return VIO_OK;
+}
+
+}  // namespace vio360
+
+using namespace vio360;
+
+struct vio_ba_batch {
+    vio_ctx* ctx;
+    BaDevice dev;
+};
+
+extern "C" {
+
+int vio_abi_version(void) { return VIO360_ABI_VERSION; }
+
+static std::string g_create_error;
+
+int vio_ctx_create(int device, vio_ctx** out) {
+    if (!out) return VIO_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) {
+        g_create_error = "no HIP device available";
+        return VIO_EDEVICE;
+    }
+    if (device < 0 || device >= n) {
+        g_create_error = "device index out of range";
+        return VIO_EINVAL;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        g_create_error = "hipSetDevice failed";
+        return VIO_EDEVICE;
+    }
+    vio_ctx* c = new vio_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        g_create_error = "hipStreamCreate failed";
+        return VIO_EDEVICE;
+    }
+    *out = c;
+    return VIO_OK;
+}
+
+void vio_ctx_destroy(vio_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    for (void* p : ctx->bufs)
+        if (p) hipFree(p);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* vio_ctx_last_error(const vio_ctx* ctx) {
+    return ctx ? ctx->last_error.c_str() : g_create_error.c_str();
+}
+
+int vio_ba_batch_create(vio_ctx* ctx, const vio_ba_problem* probs, int n, vio_ba_batch** out) {
+    if (!ctx || !probs || n <= 0 || !out) return VIO_EINVAL;
+    *out = nullptr;
+    hipSetDevice(ctx->device);
+    vio_ba_batch* b = new vio_ba_batch();
+    b->ctx = ctx;
+    b->dev.n = n;
+    for (int i = 0; i < n; ++i) {
+        int rc = pack_window(ctx, probs[i], b->dev.pk);
+        if (rc != VIO_OK) { delete b; return rc; }
+    }
+    int rc = upload_batch(ctx, b->dev);
+    if (rc != VIO_OK) { free_batch(b->dev); delete b; return rc; }
+    *out = b;
+    return VIO_OK;
+}
+
+int vio_ba_batch_run(vio_ba_batch* b) {
+    if (!b) return VIO_EINVAL;
+    vio_ctx* ctx = b->ctx;
+    if (b->dev.timing_pending) {  // fold the previous run's time in before re-recording
+        VIO_HIP(ctx, hipEventSynchronize(b->dev.ev1));
+        float ms = 0.f;
+        VIO_HIP(ctx, hipEventElapsedTime(&ms, b->dev.ev0, b->dev.ev1));
+        b->dev.ms_sum += ms;
+        b->dev.ms_count++;
+        b->dev.timing_pending = false;
+    }
+    return launch(ctx, b->dev, true);
+}
+
+int vio_ba_batch_sync(vio_ba_batch* b) {
+    if (!b) return VIO_EINVAL;
+    VIO_HIP(b->ctx, hipStreamSynchronize(b->ctx->stream));
+    return VIO_OK;
+}
+
+int vio_ba_batch_download(vio_ba_batch* b, vio_ba_output* outs) {
+    if (!b || !outs) return VIO_EINVAL;
+    return download_batch(b->ctx, b->dev, outs);
+}
+
+int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count) {
+    if (!b || !avg_ms || !count) return VIO_EINVAL;
+    if (b->dev.timing_pending) {
+        VIO_HIP(b->ctx, hipEventSynchronize(b->dev.ev1));
+        float ms = 0.f;
+        VIO_HIP(b->ctx, hipEventElapsedTime(&ms, b->dev.ev0, b->dev.ev1));
+        b->dev.ms_sum += ms;
+        b->dev.ms_count++;
+        b->dev.timing_pending = false;
+    }
+    *count = b->dev.ms_count;
+    *avg_ms = b->dev.ms_count ? b->dev.ms_sum / b->dev.ms_count : 0.0;
+    b->dev.ms_sum = 0.0;
+    b->dev.ms_count = 0;
+    return VIO_OK;
+}
+
+int vio_ba_batch_profile(vio_ba_batch* b, int enable) {
+    if (!b) return VIO_EINVAL;
+    if (enable && !b->dev.prof_buf) {
+        VIO_HIP(b->ctx, hipMalloc(&b->dev.prof_buf, sizeof(unsigned long long) * 16 * b->dev.n));
+        VIO_HIP(b->ctx, hipMemsetAsync(b->dev.prof_buf, 0, sizeof(unsigned long long) * 16 * b->dev.n, b->ctx->stream));
+    }
+    b->dev.P.prof = enable ? (unsigned long long*)b->dev.prof_buf : nullptr;
+    return VIO_OK;
+}
+
+int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out16) {
+    if (!b || !out16 || !b->dev.prof_buf) return VIO_EINVAL;
+    std::vector<unsigned long long> v(16 * b->dev.n);
+    VIO_HIP(b->ctx, hipMemcpyAsync(v.data(), b->dev.prof_buf, sizeof(unsigned long long) * v.size(),
+                                   hipMemcpyDeviceToHost, b->ctx->stream));
+    VIO_HIP(b->ctx, hipStreamSynchronize(b->ctx->stream));
+    for (int s = 0; s < 16; ++s) {
+        out16[s] = 0;
+        for (int i = 0; i < b->dev.n; ++i) out16[s] += v[16 * i + s];
+    }
+    return VIO_OK;
+}
+
+void vio_ba_batch_destroy(vio_ba_batch* b) {
+    if (!b) return;
+    hipSetDevice(b->ctx->device);
+    hipStreamSynchronize(b->ctx->stream);
+    free_batch(b->dev);
+    delete b;
+}
+
+int vio_ba_solve_batched(vio_ctx* ctx, const vio_ba_problem* probs, vio_ba_output* outs, int n) {
+    if (!ctx || !probs || !outs || n <= 0) return VIO_EINVAL;
+    vio_ba_batch* b = nullptr;
+    int rc = vio_ba_batch_create(ctx, probs, n, &b);
+    if (rc != VIO_OK) return rc;
+    rc = launch(ctx, b->dev, false);
+    if (rc == VIO_OK) rc = download_batch(ctx, b->dev, outs);
+    vio_ba_batch_destroy(b);
+    return rc;
+}
+
+int vio_ba_solve(vio_ctx* ctx, const vio_ba_problem* prob, vio_ba_output* out) {
+    return vio_ba_solve_batched(ctx, prob, out, 1);
+}
+
+}  // extern "C"

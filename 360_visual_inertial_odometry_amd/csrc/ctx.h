@@ -1,0 +1,32 @@
+// ctx.h — vio_ctx: device + stream + grow-only device scratch (host side of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "vio360.h"
+
+struct vio_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    // grow-only device buffers keyed by slot
+    std::vector<void*> bufs;
+    std::vector<size_t> caps;
+};
+
+namespace vio360 {
+
+void set_error(vio_ctx* ctx, const std::string& msg);
+int hip_fail(vio_ctx* ctx, hipError_t e, const char* what);
+// device buffer of at least `bytes` for slot `slot` (contents undefined); nullptr on failure
+void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes);
+
+#define VIO_HIP(ctx, expr)                                  \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return hip_fail(ctx, _e, #expr); \
+    } while (0)
+
+}  // namespace vio360

@@ -1,0 +1,238 @@
+/*
+ * vio360.h — C-ABI of the MI355X-native hot path of 93won/360_visual_inertial_odometry.
+ *
+ * Pure C, caller-owned host buffers, no Eigen/OpenCV/torch types.  Each entry point replaces
+ * one reference interface (cited file:line, paths relative to the reference repo root):
+ *
+ *   vio_ba_solve          Optimizer::RunLocalBA / RunBA / RunFullBA / RunVIBA / SolvePnP
+ *                         (src/optimization/Optimizer.h:107-177, Optimizer.cpp:83-966)
+ *                         = Ceres::Solve(SPARSE/DENSE_SCHUR, LM) over BAFactor/PnPFactor/
+ *                         InertialFactorFixedGravity (src/optimization/Factors.cpp:33-612,1299-1485)
+ *                         plus the chi^2 outlier tagging that follows each solve.
+ *   vio_ba_solve_batched  many independent windows in one launch (config 4 / §8e).
+ *   erp_klt_track         cv::calcOpticalFlowPyrLK call in FeatureTracker::TrackOpticalFlow
+ *                         (src/processing/FeatureTracker.cpp:228-251)
+ *   erp_gftt              cv::goodFeaturesToTrack call in FeatureTracker::DetectNewFeatures
+ *                         (src/processing/FeatureTracker.cpp:208-226)
+ *   erp_rot_ransac        FeatureTracker::RejectOutliersRotationRANSAC / EstimateRotation /
+ *                         ComputeRotationInliers (src/processing/FeatureTracker.cpp:253-379)
+ *
+ * The gather of a window from the Frame/MapPoint graph and the write-back rules are the host
+ * adapter's job; this ABI sees only flat arrays.
+ *
+ * Return convention: 0 on success, negative errno-style code on an API error (bad argument,
+ * HIP failure).  A numerical failure of the solver is NOT an API error: it is reported through
+ * vio_ba_summary.success = 0, exactly like Ceres Solver::Summary::IsSolutionUsable().
+ */
+#ifndef VIO360_H_
+#define VIO360_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VIO360_ABI_VERSION 1
+
+/* ----------------------------------------------------------------------------------------- */
+/* error codes                                                                                */
+#define VIO_OK 0
+#define VIO_EINVAL (-22)   /* bad argument / inconsistent sizes */
+#define VIO_ENOMEM (-12)   /* device allocation failed */
+#define VIO_EDEVICE (-5)   /* HIP runtime error */
+#define VIO_ENOSYS (-38)   /* variant not supported */
+
+/* ----------------------------------------------------------------------------------------- */
+/* context = device + stream + device scratch; one per host thread.                          */
+typedef struct vio_ctx vio_ctx;
+
+int vio_ctx_create(int device, vio_ctx** out);
+void vio_ctx_destroy(vio_ctx* ctx);
+/* last error message of this context (or of the last failed vio_ctx_create when ctx==NULL) */
+const char* vio_ctx_last_error(const vio_ctx* ctx);
+int vio_abi_version(void);
+
+/* ----------------------------------------------------------------------------------------- */
+/* Bundle adjustment / PnP                                                                    */
+
+/* rigid transform, row-major rotation, f64 (reference keeps f32 Eigen::Matrix4f and casts) */
+typedef struct {
+    double R[9];
+    double t[3];
+} vio_pose;
+
+/* IMUPreintegration (src/processing/IMUPreintegrator.h:40-69), f32 fields as in the reference */
+typedef struct {
+    float delta_R[9];   /* row-major */
+    float delta_V[3];
+    float delta_P[3];
+    float J_Rg[9], J_Vg[9], J_Va[9], J_Pg[9], J_Pa[9];
+    float cov9[81];     /* covariance.block<9,9>(0,0), row-major */
+    float gyro_bias[3];
+    float accel_bias[3];
+    float _pad[2];
+    double dt_total;
+} vio_preint;
+
+/* which Optimizer entry point the problem mirrors (selects constants and fixing rules) */
+enum {
+    VIO_BA_LOCAL = 0, /* RunLocalBA: pose 0 constant (if observed), marginalised MPs constant,
+                         chi2 threshold 5.99146 (Optimizer.cpp:726-966) */
+    VIO_BA_FULL = 1,  /* RunBA(fix_first, fix_last): chi2 threshold 5.991 (Optimizer.cpp:304-486) */
+    VIO_BA_VI = 2,    /* RunVIBA: + InertialFactorFixedGravity (Optimizer.cpp:493-724) */
+    VIO_PNP = 3       /* SolvePnP: pose-only, 4 rounds of outlier tagging (Optimizer.cpp:83-302) */
+};
+
+/* Ceres termination types (ceres/types.h), mirrored */
+enum { VIO_TERM_CONVERGENCE = 0, VIO_TERM_NO_CONVERGENCE = 1, VIO_TERM_FAILURE = 2 };
+
+/*
+ * One window = one Ceres problem.  Observation o links keyframe obs_kf[o] to landmark obs_lm[o]
+ * with pixel obs_uv[2o..2o+1] (the f32 Feature::GetPixelCoord()).  Every observation given here
+ * becomes one residual block (the adapter already dropped near-boundary features).
+ *
+ * Constant blocks: kf_const[k] != 0 → pose k is SetParameterBlockConstant; lm_const[l] != 0 →
+ * point l constant.  For VIO_PNP all points are constant and lm_const marks *marginalised*
+ * MapPoints (never tagged as outliers, Optimizer.cpp:219-220).  For every variant lm_marg[l]
+ * marks marginalised MapPoints (exempt from outlier counting / SetBad); may be NULL.
+ */
+typedef struct {
+    int32_t variant;          /* VIO_BA_* */
+    int32_t num_kf;           /* K */
+    int32_t num_lm;           /* L */
+    int32_t num_obs;          /* N */
+    double cols, rows;        /* ERP size (CameraParameters) */
+    double huber_delta;       /* HuberLoss(δ) — 1.0 in the reference (Optimizer.cpp:28) */
+    double info[4];           /* 2x2 information matrix, row-major (identity in the reference) */
+    double chi2_threshold;    /* 5.99146 (LocalBA) or 5.991 (BA/VIBA/PnP) */
+    const vio_pose* T_cb;     /* K entries: Frame::GetTCB() of each keyframe (raw f32->f64) */
+    const vio_pose* T_wb_init;/* K entries: Frame::GetTwb() (raw f32->f64) */
+    const uint8_t* kf_const;  /* K */
+    const uint8_t* lm_const;  /* L */
+    const uint8_t* lm_marg;   /* L, may be NULL */
+    const double* lm_xyz;     /* L*3 initial positions (f32 -> f64) */
+    const int32_t* obs_kf;    /* N */
+    const int32_t* obs_lm;    /* N */
+    const float* obs_uv;      /* 2N */
+    /* VIO_BA_VI only (else NULL) */
+    const vio_preint* preint; /* K entries; preint[k] links keyframe k-1 -> k (entry 0 unused) */
+    const uint8_t* preint_valid; /* K; 0 → factor k-1->k missing (RunVIBA skips it) */
+    const double* vel;        /* K*3 initial velocities */
+    double bg[3], ba[3];      /* initial shared biases */
+    double gravity[3];        /* fixed gravity in world */
+    /* solver controls */
+    int32_t max_iterations;   /* 50 in the reference (Optimizer.cpp:30) */
+    int32_t fixed_iterations; /* != 0 → benchmark mode: run exactly max_iterations LM iterations
+                                 with all convergence tests disabled */
+    int32_t num_rounds;       /* VIO_PNP: outlier rounds (4); ignored otherwise */
+    int32_t _pad0;
+} vio_ba_problem;
+
+typedef struct {
+    int32_t success;          /* Summary::IsSolutionUsable() (and PnP inlier gate) */
+    int32_t termination;      /* VIO_TERM_* of the (last) solve */
+    int32_t iterations;       /* summary.iterations.size() (PnP: sum over rounds) */
+    int32_t num_successful_steps;
+    int32_t num_unsuccessful_steps;
+    int32_t num_inliers;      /* chi2 <= threshold after the solve */
+    int32_t num_outliers;
+    int32_t num_bad_lm;       /* MapPoints to SetBad(): inliers==0 && outliers>=2 && !marg */
+    double initial_cost;      /* summary.initial_cost (includes fixed cost) */
+    double final_cost;        /* summary.final_cost  (PnP: mean inlier chi2 of last round) */
+    double fixed_cost;        /* cost of residual blocks whose parameters are all constant */
+    double _pad1;
+} vio_ba_summary;
+
+/* outputs, caller-owned; any pointer may be NULL if not wanted */
+typedef struct {
+    vio_pose* T_wb;           /* K: SE3(T_wb_init) * exp(delta) (constant poses: SE3(T_wb_init)) */
+    double* lm_xyz;           /* L*3 final point parameters */
+    double* obs_chi2;         /* N: compute_chi_square at the solution */
+    uint8_t* obs_outlier;     /* N: chi2 > threshold (PnP: also !marginalised) */
+    uint8_t* lm_bad;          /* L: SetBad decision */
+    double* vel;              /* K*3 (VI) */
+    double* bg;               /* 3 (VI) */
+    double* ba;               /* 3 (VI) */
+    vio_ba_summary* summary;  /* 1 */
+} vio_ba_output;
+
+int vio_ba_solve(vio_ctx* ctx, const vio_ba_problem* prob, vio_ba_output* out);
+
+/* n independent windows in ONE device launch (one workgroup per window) */
+int vio_ba_solve_batched(vio_ctx* ctx, const vio_ba_problem* probs, vio_ba_output* outs, int n);
+
+/*
+ * Device-resident batched interface for benchmarking and multi-GPU sharding: upload once,
+ * then vio_ba_batch_run() solves all windows from the resident copy with no host transfer.
+ */
+typedef struct vio_ba_batch vio_ba_batch;
+int vio_ba_batch_create(vio_ctx* ctx, const vio_ba_problem* probs, int n, vio_ba_batch** out);
+int vio_ba_batch_run(vio_ba_batch* b);          /* async on the context stream */
+int vio_ba_batch_sync(vio_ba_batch* b);
+int vio_ba_batch_download(vio_ba_batch* b, vio_ba_output* outs);
+/* average device time (ms) of the solver kernel over the runs since the last reset */
+int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count);
+void vio_ba_batch_destroy(vio_ba_batch* b);
+/* diagnostics: per-phase shader-clock accounting of the solver kernel (sum over windows of the
+   last run; 16 slots: setup, eval+J, linearise, step prep, Schur GEMM, Cholesky, back-subst,
+   candidate, eval cost, control, post) */
+int vio_ba_batch_profile(vio_ba_batch* b, int enable);
+int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out16);
+
+/* ----------------------------------------------------------------------------------------- */
+/* ERP feature tracking                                                                       */
+
+typedef struct {
+    int32_t win;              /* LK window (21, FeatureTracker.cpp:33) */
+    int32_t max_level;        /* 3 */
+    int32_t max_iters;        /* 30 */
+    float epsilon;            /* 0.01 (criteria.epsilon; squared internally) */
+    float min_eig_threshold;  /* 0.01 (the reference passes epsilon here, :240) */
+    int32_t _pad;
+} erp_klt_params;
+
+/* prev/curr: u8 W x H, row stride `stride` bytes, host memory.  Returns next/status/err. */
+int erp_klt_track(vio_ctx* ctx, const uint8_t* prev, const uint8_t* curr, int W, int H, int stride,
+                  const float* pts, int n, float* next, uint8_t* status, float* err,
+                  const erp_klt_params* params);
+
+/* goodFeaturesToTrack(img, max_corners, quality, min_dist, mask, blockSize 3, useHarris false).
+   mask may be NULL.  out_xy holds up to max_corners float2, *n_out the count. */
+int erp_gftt(vio_ctx* ctx, const uint8_t* img, const uint8_t* mask, int W, int H, int stride,
+             int max_corners, double quality, double min_dist, float* out_xy, int* n_out);
+
+/* rotation-only RANSAC on ERP bearings with an injected sample stream (iters*3 indices) */
+int erp_rot_ransac(vio_ctx* ctx, const float* p0, const float* p1, int n, int W, int H,
+                   const int32_t* samples, int iters, float thresh_rad, uint8_t* mask, int* n_in);
+
+/* whole FeatureTracker::TrackFeatures numeric path for one frame pair, device-resident:
+   pyramids of both frames + LK + RANSAC + GFTT re-detection (see erp_tracker_* below). */
+typedef struct erp_tracker erp_tracker;
+int erp_tracker_create(vio_ctx* ctx, int W, int H, int max_points, int max_corners, erp_tracker** out);
+/* upload a frame into slot 0 (prev) or 1 (curr) */
+int erp_tracker_upload(erp_tracker* t, int slot, const uint8_t* img, int stride);
+typedef struct {
+    int32_t n_pts;            /* tracked points (input) */
+    int32_t ransac_iters;     /* 1000 */
+    float ransac_thresh_rad;  /* 2 deg */
+    int32_t max_corners;      /* GFTT re-detection cap */
+    double quality;           /* 0.01 */
+    double min_dist;          /* 30 */
+    int32_t boundary_margin;  /* 20 */
+    float polar_ratio;        /* 0.15 */
+} erp_tracker_params;
+/* runs the device pipeline (async); pts/samples already uploaded by erp_tracker_set_points */
+int erp_tracker_set_points(erp_tracker* t, const float* pts, int n, const int32_t* samples, int iters);
+int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p);
+int erp_tracker_sync(erp_tracker* t);
+int erp_tracker_download(erp_tracker* t, float* next, uint8_t* status, uint8_t* inlier,
+                         float* corners, int* n_corners);
+int erp_tracker_kernel_ms(erp_tracker* t, double* pyr_ms, double* lk_ms, double* gftt_ms,
+                          double* ransac_ms);
+void erp_tracker_destroy(erp_tracker* t);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VIO360_H_ */

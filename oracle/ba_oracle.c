@@ -1,0 +1,1591 @@
+/*
+ * ba_oracle.c — TEST INFRASTRUCTURE ONLY (parity checker + timed CPU baseline, never shipped).
+ *
+ * CPU restatement, in plain C99, of the reference's sliding-window bundle-adjustment path:
+ *   - ERP reprojection factors  BAFactor / PnPFactor (src/optimization/Factors.cpp:33-612)
+ *   - InertialFactorFixedGravity (src/optimization/Factors.cpp:1299-1519)
+ *   - SE3d/SO3d maths incl. the SVD re-orthonormalisation (src/util/LieUtils.cpp:203-370)
+ *   - HuberLoss + Corrector (thirdparty/ceres-solver/internal/ceres/loss_function.cc:48-62,
+ *     corrector.cc:42-156, residual_block.cc:161-197)
+ *   - Ceres 2.0 TrustRegionMinimizer + LevenbergMarquardtStrategy with Jacobi scaling
+ *     (internal/ceres/trust_region_minimizer.cc:67-826, levenberg_marquardt_strategy.cc:66-160,
+ *      trust_region_step_evaluator.cc:52-63), fixed-block removal (program.cc:305-400) and
+ *     final-cost bookkeeping (solver_utils.h:46-55)
+ *   - Schur-complement linear solve with the points as e-blocks
+ *     (internal/ceres/schur_complement_solver.cc:118-356, schur_eliminator_impl.h:179-377)
+ *   - Optimizer::RunLocalBA / RunBA / RunVIBA / SolvePnP solve + chi^2 post-processing
+ *     (src/optimization/Optimizer.cpp:83-966)
+ *
+ * It consumes the same vio_ba_problem the HIP library consumes (include/vio360.h) so the two
+ * can be compared on identical inputs.  Parity status: the Ceres control flow is pinned by the
+ * restated Ceres known-answer tests (tests/test_oracle_kat.py); the first-party factor maths has
+ * no reference tests and is cross-checked against an independent numpy restatement
+ * (oracle/oracle_np.py) and finite differences — "parity unpinned" against the reference binary,
+ * which cannot be built here (no Eigen/OpenCV in the image).
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/vio360.h"
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+#define EPS_D 1e-10 /* kEpsilonD, src/util/LieUtils.h:24 */
+
+/* ========================================================================================= */
+/* 3x3 helpers (row-major)                                                                   */
+/* ========================================================================================= */
+static void m3_mul(const double* a, const double* b, double* c) {
+    double t[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) t[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+    memcpy(c, t, sizeof t);
+}
+static void m3_tr(const double* a, double* b) {
+    double t[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) t[3 * i + j] = a[3 * j + i];
+    memcpy(b, t, sizeof t);
+}
+static void m3_vec(const double* a, const double* v, double* o) {
+    double t[3];
+    for (int i = 0; i < 3; ++i) t[i] = a[3 * i] * v[0] + a[3 * i + 1] * v[1] + a[3 * i + 2] * v[2];
+    memcpy(o, t, sizeof t);
+}
+static void hat3(const double* v, double* S) {
+    S[0] = 0; S[1] = -v[2]; S[2] = v[1];
+    S[3] = v[2]; S[4] = 0; S[5] = -v[0];
+    S[6] = -v[1]; S[7] = v[0]; S[8] = 0;
+}
+static double det3(const double* a) {
+    return a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) + a[2] * (a[3] * a[7] - a[4] * a[6]);
+}
+static double norm3(const double* v) { return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+
+/* symmetric 3x3 eigen-decomposition by cyclic Jacobi: A = V diag(w) V^T */
+static void sym3_eig(const double* A_in, double* w, double* V) {
+    double A[9];
+    memcpy(A, A_in, sizeof A);
+    for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        double off = A[1] * A[1] + A[2] * A[2] + A[5] * A[5];
+        double dia = A[0] * A[0] + A[4] * A[4] + A[8] * A[8];
+        if (off <= 1e-36 * dia || off == 0.0) break;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                double apq = A[3 * p + q];
+                if (apq == 0.0) continue;
+                double app = A[3 * p + p], aqq = A[3 * q + q];
+                double theta = (aqq - app) / (2.0 * apq);
+                double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 3; ++k) { /* A = J^T A J */
+                    double akp = A[3 * k + p], akq = A[3 * k + q];
+                    A[3 * k + p] = c * akp - s * akq;
+                    A[3 * k + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    double apk = A[3 * p + k], aqk = A[3 * q + k];
+                    A[3 * p + k] = c * apk - s * aqk;
+                    A[3 * q + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    double vkp = V[3 * k + p], vkq = V[3 * k + q];
+                    V[3 * k + p] = c * vkp - s * vkq;
+                    V[3 * k + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    w[0] = A[0]; w[1] = A[4]; w[2] = A[8];
+}
+
+/*
+ * Nearest proper rotation of a 3x3 matrix: R = U diag(1,1,d) V^T with d = sign(det(U V^T)).
+ * This is exactly what SO3d(const Matrix3d&) (LieUtils.cpp:275-288, U col 2 flipped when
+ * det<0) and EstimateRotation (FeatureTracker.cpp:341-352, V col 2 flipped) compute; the result
+ * is unique whenever the two largest singular values are distinct from the smallest.
+ */
+void oracle_nearest_rotation(const double* A, double* R) {
+    double AtA[9], At[9], w[3], V[9];
+    m3_tr(A, At);
+    m3_mul(At, A, AtA);
+    sym3_eig(AtA, w, V);
+    /* sort eigenpairs descending */
+    int idx[3] = {0, 1, 2};
+    for (int i = 0; i < 3; ++i)
+        for (int j = i + 1; j < 3; ++j)
+            if (w[idx[j]] > w[idx[i]]) { int t = idx[i]; idx[i] = idx[j]; idx[j] = t; }
+    double v[3][3], u[3][3];
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) v[c][r] = V[3 * r + idx[c]];
+    for (int c = 0; c < 2; ++c) {
+        m3_vec(A, v[c], u[c]);
+        double n = norm3(u[c]);
+        if (n > 0) { u[c][0] /= n; u[c][1] /= n; u[c][2] /= n; }
+    }
+    /* re-orthogonalise u1 against u0 (robust for near-degenerate input) */
+    double d01 = u[0][0] * u[1][0] + u[0][1] * u[1][1] + u[0][2] * u[1][2];
+    for (int r = 0; r < 3; ++r) u[1][r] -= d01 * u[0][r];
+    double n1 = norm3(u[1]);
+    if (n1 > 0) { u[1][0] /= n1; u[1][1] /= n1; u[1][2] /= n1; }
+    u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
+    u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
+    u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
+    double detV = det3(V); /* +-1; columns of V permuted => sign folds in below */
+    double vm[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) vm[3 * r + c] = v[c][r];
+    detV = det3(vm);
+    /* det(U V^T) with u2 = u0 x u1 (det U = +1) equals det(V); choose d so det(R) = +1 */
+    double d = (detV < 0) ? -1.0 : 1.0;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) R[3 * r + c] = u[0][r] * v[0][c] + u[1][r] * v[1][c] + d * u[2][r] * v[2][c];
+}
+
+/* SO3d::Exp (LieUtils.cpp:203-219) — result re-projected like every SO3d construction */
+static void so3_exp(const double* w, double* R) {
+    double th = norm3(w);
+    double M[9];
+    if (th < EPS_D) {
+        hat3(w, M);
+        M[0] += 1; M[4] += 1; M[8] += 1;
+    } else {
+        double k[3] = {w[0] / th, w[1] / th, w[2] / th}, K[9], K2[9];
+        hat3(k, K);
+        m3_mul(K, K, K2);
+        double s = sin(th), c = 1.0 - cos(th);
+        for (int i = 0; i < 9; ++i) M[i] = s * K[i] + c * K2[i];
+        M[0] += 1; M[4] += 1; M[8] += 1;
+    }
+    oracle_nearest_rotation(M, R);
+}
+
+/* SE3d::exp (LieUtils.cpp:305-333), xi = [rho, phi] */
+static void se3_exp(const double* xi, double* R, double* t) {
+    const double* rho = xi;
+    const double* phi = xi + 3;
+    so3_exp(phi, R);
+    double th = norm3(phi);
+    if (th < EPS_D) {
+        t[0] = rho[0]; t[1] = rho[1]; t[2] = rho[2];
+    } else {
+        double P[9], P2[9], Vm[9];
+        hat3(phi, P);
+        m3_mul(P, P, P2);
+        double th2 = th * th, a = (1.0 - cos(th)) / th2, b = (th - sin(th)) / (th2 * th);
+        for (int i = 0; i < 9; ++i) Vm[i] = a * P[i] + b * P2[i];
+        Vm[0] += 1; Vm[4] += 1; Vm[8] += 1;
+        m3_vec(Vm, rho, t);
+    }
+}
+
+/* SE3d composition (LieUtils.h:268-271): (R1,t1)*(R2,t2), rotation re-projected */
+static void se3_mul(const double* R1, const double* t1, const double* R2, const double* t2, double* R, double* t) {
+    double M[9], tt[3];
+    m3_mul(R1, R2, M);
+    m3_vec(R1, t2, tt);
+    tt[0] += t1[0]; tt[1] += t1[1]; tt[2] += t1[2];
+    oracle_nearest_rotation(M, R);
+    memcpy(t, tt, sizeof tt);
+}
+/* SE3d::inverse (LieUtils.h:279-282) */
+static void se3_inv(const double* R, const double* t, double* Ri, double* ti) {
+    double Rt[9], nt[3] = {-t[0], -t[1], -t[2]};
+    m3_tr(R, Rt);
+    oracle_nearest_rotation(Rt, Ri);
+    m3_vec(Ri, nt, ti);
+}
+
+/* SO3 log as used by InertialFactorFixedGravity::log_SO3 (Factors.cpp:1507-1519) */
+static void imu_log_so3(const double* R, double* w) {
+    double tr = R[0] + R[4] + R[8];
+    double c = (tr - 1.0) / 2.0;
+    c = fmax(-1.0, fmin(1.0, c));
+    double th = acos(c);
+    double v[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
+    if (th < 1e-6) {
+        w[0] = v[0] / 2.0; w[1] = v[1] / 2.0; w[2] = v[2] / 2.0;
+        return;
+    }
+    double f = th / (2.0 * sin(th));
+    w[0] = f * v[0]; w[1] = f * v[1]; w[2] = f * v[2];
+}
+/* InertialFactorFixedGravity::right_jacobian_SO3 (Factors.cpp:1495-1505) */
+static void imu_right_jac(const double* phi, double* J) {
+    double th = norm3(phi);
+    if (th < 1e-6) {
+        for (int i = 0; i < 9; ++i) J[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    double P[9], P2[9];
+    hat3(phi, P);
+    m3_mul(P, P, P2);
+    double th2 = th * th, a = (1.0 - cos(th)) / th2, b = (th - sin(th)) / (th2 * th);
+    for (int i = 0; i < 9; ++i) J[i] = -a * P[i] + b * P2[i];
+    J[0] += 1; J[4] += 1; J[8] += 1;
+}
+/* plain SO3d::exp of a bias correction (SO3d::Exp, LieUtils.cpp:203-219) */
+static void so3_exp_plain(const double* w, double* R) { so3_exp(w, R); }
+
+/* general dense inverse by Gauss-Jordan with partial pivoting (Eigen .inverse() for 9x9) */
+static int dense_inverse(int n, const double* A, double* Ai) {
+    double* M = (double*)malloc(sizeof(double) * n * 2 * n);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < 2 * n; ++j) M[i * 2 * n + j] = j < n ? A[i * n + j] : (j - n == i ? 1.0 : 0.0);
+    for (int c = 0; c < n; ++c) {
+        int p = c;
+        for (int r = c + 1; r < n; ++r)
+            if (fabs(M[r * 2 * n + c]) > fabs(M[p * 2 * n + c])) p = r;
+        if (M[p * 2 * n + c] == 0.0) { free(M); return -1; }
+        if (p != c)
+            for (int j = 0; j < 2 * n; ++j) { double t = M[c * 2 * n + j]; M[c * 2 * n + j] = M[p * 2 * n + j]; M[p * 2 * n + j] = t; }
+        double iv = 1.0 / M[c * 2 * n + c];
+        for (int j = 0; j < 2 * n; ++j) M[c * 2 * n + j] *= iv;
+        for (int r = 0; r < n; ++r) {
+            if (r == c) continue;
+            double f = M[r * 2 * n + c];
+            if (f == 0.0) continue;
+            for (int j = 0; j < 2 * n; ++j) M[r * 2 * n + j] -= f * M[c * 2 * n + j];
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) Ai[i * n + j] = M[i * 2 * n + n + j];
+    free(M);
+    return 0;
+}
+/* in-place lower Cholesky of a dense SPD matrix (row-major, full storage); 0 on success */
+static int dense_llt(int n, double* A) {
+    for (int j = 0; j < n; ++j) {
+        double d = A[j * n + j];
+        for (int k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
+        if (!(d > 0.0)) return -1;
+        d = sqrt(d);
+        A[j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double s = A[i * n + j];
+            for (int k = 0; k < j; ++k) s -= A[i * n + k] * A[j * n + k];
+            A[i * n + j] = s / d;
+        }
+    }
+    return 0;
+}
+static void dense_llt_solve(int n, const double* L, double* b) {
+    for (int i = 0; i < n; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s -= L[i * n + k] * b[k];
+        b[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double s = b[i];
+        for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * b[k];
+        b[i] = s / L[i * n + i];
+    }
+}
+
+/* ========================================================================================= */
+/* Huber loss + Corrector                                                                     */
+/* ========================================================================================= */
+void oracle_huber(double delta, double s, double rho[3]) {
+    double b = delta * delta, a = delta;
+    if (s > b) {
+        double r = sqrt(s);
+        rho[0] = 2.0 * a * r - b;
+        rho[1] = fmax(DBL_MIN, a / r);
+        rho[2] = -rho[1] / (2.0 * s);
+    } else {
+        rho[0] = s; rho[1] = 1.0; rho[2] = 0.0;
+    }
+}
+/* Corrector: residual_scaling and alpha_sq_norm (corrector.cc:42-98) */
+void oracle_corrector(double sq_norm, const double rho[3], double* residual_scaling, double* alpha_sq_norm,
+                      double* sqrt_rho1) {
+    *sqrt_rho1 = sqrt(rho[1]);
+    if (sq_norm == 0.0 || rho[2] <= 0.0) {
+        *residual_scaling = *sqrt_rho1;
+        *alpha_sq_norm = 0.0;
+        return;
+    }
+    double D = 1.0 + 2.0 * sq_norm * rho[2] / rho[1];
+    double alpha = 1.0 - sqrt(D);
+    *residual_scaling = *sqrt_rho1 / (1 - alpha);
+    *alpha_sq_norm = alpha / sq_norm;
+}
+
+/* ========================================================================================= */
+/* Factors                                                                                    */
+/* ========================================================================================= */
+typedef struct {
+    double R_init[9], t_init[3]; /* SE3d(T_wb_init): SVD-projected */
+    double R_cb[9], t_cb[3];     /* SE3d(T_cb): SVD-projected */
+    double R_cb_raw[9];          /* m_Tcb.block<3,3> used verbatim in the Jacobians */
+} pose_ctx;
+
+/*
+ * BAFactor::Evaluate (Factors.cpp:327-542) / PnPFactor::Evaluate (:33-210).
+ * Returns 1 on success, 0 when the PnP variant fails (L<1e-10 → Evaluate returns false).
+ * r: weighted residual; Jp (2x6, row-major) and Jl (2x3) if non-NULL.
+ */
+static int factor_eval(const pose_ctx* pc, const double* delta, const double* Pw, double u_obs, double v_obs,
+                       double cols, double rows, const double* Lw /* chol(info) lower 2x2 or NULL */, int outlier,
+                       int is_pnp, double* r, double* Jp, double* Jl) {
+    if (outlier) {
+        r[0] = 640.0; r[1] = 480.0;
+        if (Jp) memset(Jp, 0, 12 * sizeof(double));
+        if (Jl) memset(Jl, 0, 6 * sizeof(double));
+        return 1;
+    }
+    double dR[9], dt[3], Rwb[9], twb[3], Rbw[9], tbw[3], Rcw[9], tcw[3];
+    se3_exp(delta, dR, dt);
+    se3_mul(pc->R_init, pc->t_init, dR, dt, Rwb, twb);
+    se3_inv(Rwb, twb, Rbw, tbw);
+    se3_mul(pc->R_cb, pc->t_cb, Rbw, tbw, Rcw, tcw);
+    double Pc[3];
+    m3_vec(Rcw, Pw, Pc);
+    Pc[0] += tcw[0]; Pc[1] += tcw[1]; Pc[2] += tcw[2];
+    double x = Pc[0], y = Pc[1], z = Pc[2];
+    double L = norm3(Pc);
+    if (L < 1e-10) {
+        if (Jp) memset(Jp, 0, 12 * sizeof(double));
+        if (Jl) memset(Jl, 0, 6 * sizeof(double));
+        if (is_pnp) return 0;
+        r[0] = 640.0; r[1] = 360.0;
+        return 1;
+    }
+    double theta = atan2(x, z);
+    double phi = -asin(y / L);
+    double u = cols * (0.5 + theta / (2.0 * M_PI));
+    double v = rows * (0.5 - phi / M_PI);
+    double du = u_obs - u, dv = v_obs - v;
+    if (du > cols / 2.0) du -= cols;
+    else if (du < -cols / 2.0) du += cols;
+    if (fabs(du) > 100.0 || fabs(dv) > 100.0) {
+        r[0] = 100.0; r[1] = 100.0;
+        if (Jp) memset(Jp, 0, 12 * sizeof(double));
+        if (Jl) memset(Jl, 0, 6 * sizeof(double));
+        return 1;
+    }
+    if (Lw) {
+        r[0] = Lw[0] * du;
+        r[1] = Lw[2] * du + Lw[3] * dv;
+    } else {
+        r[0] = du; r[1] = dv;
+    }
+    if (!Jp && !Jl) return 1;
+    double xz2 = x * x + z * z, L2 = L * L, xzn = sqrt(xz2);
+    if (xz2 < 1e-10 || L2 < 1e-10) {
+        if (Jp) memset(Jp, 0, 12 * sizeof(double));
+        if (Jl) memset(Jl, 0, 6 * sizeof(double));
+        return 1;
+    }
+    double Jc[6];
+    Jc[0] = -cols / (2.0 * M_PI) * z / xz2;
+    Jc[1] = 0.0;
+    Jc[2] = cols / (2.0 * M_PI) * x / xz2;
+    Jc[3] = rows / M_PI * (x * y) / (L2 * xzn);
+    Jc[4] = -rows / M_PI * xzn / L2;
+    Jc[5] = rows / M_PI * (y * z) / (L2 * xzn);
+    double Jw[6];
+    if (Lw) {
+        for (int j = 0; j < 3; ++j) {
+            Jw[j] = Lw[0] * Jc[j];
+            Jw[3 + j] = Lw[2] * Jc[j] + Lw[3] * Jc[3 + j];
+        }
+    } else {
+        memcpy(Jw, Jc, sizeof Jw);
+    }
+    if (Jp) {
+        double Pb[3], H[9], RH[9];
+        m3_vec(Rbw, Pw, Pb);
+        Pb[0] += tbw[0]; Pb[1] += tbw[1]; Pb[2] += tbw[2];
+        hat3(Pb, H);
+        m3_mul(pc->R_cb_raw, H, RH);
+        for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < 3; ++j) {
+                double st = 0, sr = 0;
+                for (int k = 0; k < 3; ++k) {
+                    st += Jw[3 * i + k] * (-pc->R_cb_raw[3 * k + j]);
+                    sr += Jw[3 * i + k] * RH[3 * k + j];
+                }
+                Jp[6 * i + j] = st;
+                Jp[6 * i + 3 + j] = sr;
+            }
+    }
+    if (Jl) {
+        double Cp[9];
+        m3_mul(pc->R_cb_raw, Rbw, Cp);
+        for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < 3; ++j) {
+                double s = 0;
+                for (int k = 0; k < 3; ++k) s += Jw[3 * i + k] * Cp[3 * k + j];
+                Jl[3 * i + j] = s;
+            }
+    }
+    return 1;
+}
+
+/* BAFactor::compute_chi_square (Factors.cpp:544-612); PnP variant (:212-265) ignores the flag */
+static double factor_chi2(const pose_ctx* pc, const double* delta, const double* Pw, double u_obs, double v_obs,
+                          double cols, double rows, const double* info, int outlier, int is_pnp) {
+    if (outlier && !is_pnp) return 0.0;
+    double dR[9], dt[3], Rwb[9], twb[3], Rbw[9], tbw[3], Rcw[9], tcw[3];
+    se3_exp(delta, dR, dt);
+    se3_mul(pc->R_init, pc->t_init, dR, dt, Rwb, twb);
+    se3_inv(Rwb, twb, Rbw, tbw);
+    se3_mul(pc->R_cb, pc->t_cb, Rbw, tbw, Rcw, tcw);
+    double Pc[3];
+    m3_vec(Rcw, Pw, Pc);
+    Pc[0] += tcw[0]; Pc[1] += tcw[1]; Pc[2] += tcw[2];
+    double L = norm3(Pc);
+    if (L < 1e-10) return is_pnp ? DBL_MAX : 1000.0;
+    double theta = atan2(Pc[0], Pc[2]);
+    double phi = -asin(Pc[1] / L);
+    double u = cols * (0.5 + theta / (2.0 * M_PI));
+    double v = rows * (0.5 - phi / M_PI);
+    double du = u_obs - u, dv = v_obs - v;
+    if (du > cols / 2.0) du -= cols;
+    else if (du < -cols / 2.0) du += cols;
+    return du * (info[0] * du + info[1] * dv) + dv * (info[2] * du + info[3] * dv);
+}
+
+/* InertialFactorFixedGravity (Factors.cpp:1299-1485) */
+typedef struct {
+    double sqrt_info[81];
+    double dR[9], dV[3], dP[3], JRg[9], JVg[9], JVa[9], JPg[9], JPa[9], bg0[3], ba0[3];
+    double dt;
+    double Ri_init[9], ti_init[3], Rj_init[9], tj_init[3];
+    double g[3];
+} imu_ctx;
+
+static void imu_ctx_init(imu_ctx* c, const vio_preint* p, const double* g, const vio_pose* Ti, const vio_pose* Tj) {
+    double cov[81], info[81];
+    for (int i = 0; i < 81; ++i) cov[i] = (double)p->cov9[i];
+    for (int i = 0; i < 9; ++i) cov[i * 9 + i] += 1e-8;
+    int ok = dense_inverse(9, cov, info) == 0;
+    if (ok) ok = dense_llt(9, info) == 0; /* info now holds L (lower) + stale upper */
+    for (int i = 0; i < 9; ++i)
+        for (int j = 0; j < 9; ++j) c->sqrt_info[i * 9 + j] = ok ? (j >= i ? info[j * 9 + i] : 0.0) : (i == j ? 1.0 : 0.0);
+    for (int i = 0; i < 9; ++i) {
+        c->dR[i] = p->delta_R[i]; c->JRg[i] = p->J_Rg[i]; c->JVg[i] = p->J_Vg[i];
+        c->JVa[i] = p->J_Va[i]; c->JPg[i] = p->J_Pg[i]; c->JPa[i] = p->J_Pa[i];
+    }
+    for (int i = 0; i < 3; ++i) {
+        c->dV[i] = p->delta_V[i]; c->dP[i] = p->delta_P[i];
+        c->bg0[i] = p->gyro_bias[i]; c->ba0[i] = p->accel_bias[i]; c->g[i] = g[i];
+    }
+    c->dt = p->dt_total;
+    oracle_nearest_rotation(Ti->R, c->Ri_init);
+    memcpy(c->ti_init, Ti->t, sizeof c->ti_init);
+    oracle_nearest_rotation(Tj->R, c->Rj_init);
+    memcpy(c->tj_init, Tj->t, sizeof c->tj_init);
+}
+
+/* r[9]; J_vi/J_bg/J_ba/J_vj 9x3 row-major (pose Jacobians are identically zero, :1415-1419) */
+static void imu_eval(const imu_ctx* c, const double* di, const double* vi, const double* bg, const double* ba,
+                     const double* dj, const double* vj, double* r, double* Jvi, double* Jbg, double* Jba,
+                     double* Jvj) {
+    double dR[9], dt3[3], Rwi[9], twi[3], Rwj[9], twj[3], Rbwi[9];
+    se3_exp(di, dR, dt3);
+    se3_mul(c->Ri_init, c->ti_init, dR, dt3, Rwi, twi);
+    se3_exp(dj, dR, dt3);
+    se3_mul(c->Rj_init, c->tj_init, dR, dt3, Rwj, twj);
+    m3_tr(Rwi, Rbwi);
+    double dt = c->dt;
+    double DR[9], DV[3], DP[3];
+    memcpy(DR, c->dR, sizeof DR);
+    memcpy(DV, c->dV, sizeof DV);
+    memcpy(DP, c->dP, sizeof DP);
+    double dbg[3] = {bg[0] - c->bg0[0], bg[1] - c->bg0[1], bg[2] - c->bg0[2]};
+    double dba[3] = {ba[0] - c->ba0[0], ba[1] - c->ba0[1], ba[2] - c->ba0[2]};
+    if (norm3(dbg) > 1e-6 || norm3(dba) > 1e-6) {
+        double w[3], E[9], t1[3], t2[3];
+        m3_vec(c->JRg, dbg, w);
+        so3_exp_plain(w, E);
+        m3_mul(DR, E, DR); /* plain Matrix3d product: delta_R is not an SO3d (Factors.cpp:1381) */
+        m3_vec(c->JVg, dbg, t1); m3_vec(c->JVa, dba, t2);
+        for (int i = 0; i < 3; ++i) DV[i] += t1[i] + t2[i];
+        m3_vec(c->JPg, dbg, t1); m3_vec(c->JPa, dba, t2);
+        for (int i = 0; i < 3; ++i) DP[i] += t1[i] + t2[i];
+    }
+    double raw[9];
+    {
+        double DRt[9], A[9], B[9];
+        m3_tr(DR, DRt);
+        m3_mul(DRt, Rbwi, A);
+        m3_mul(A, Rwj, B);
+        imu_log_so3(B, raw);
+        double tv[3], ev[3];
+        for (int i = 0; i < 3; ++i) tv[i] = vj[i] - vi[i] - c->g[i] * dt;
+        m3_vec(Rbwi, tv, ev);
+        for (int i = 0; i < 3; ++i) raw[3 + i] = ev[i] - DV[i];
+        for (int i = 0; i < 3; ++i) tv[i] = twj[i] - twi[i] - vi[i] * dt - 0.5 * c->g[i] * dt * dt;
+        m3_vec(Rbwi, tv, ev);
+        for (int i = 0; i < 3; ++i) raw[6 + i] = ev[i] - DP[i];
+    }
+    for (int i = 0; i < 9; ++i) {
+        double s = 0;
+        for (int k = 0; k < 9; ++k) s += c->sqrt_info[i * 9 + k] * raw[k];
+        r[i] = s;
+    }
+    if (!Jvi) return;
+    const double* S = c->sqrt_info;
+    /* J_vi: rows 3..5 = -S33(3,3) R_bwi ; rows 6..8 = -S(6,6) R_bwi dt */
+    memset(Jvi, 0, 27 * sizeof(double));
+    memset(Jvj, 0, 27 * sizeof(double));
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double a = 0, b = 0;
+            for (int k = 0; k < 3; ++k) {
+                a += S[(3 + i) * 9 + 3 + k] * Rbwi[3 * k + j];
+                b += S[(6 + i) * 9 + 6 + k] * Rbwi[3 * k + j];
+            }
+            Jvi[(3 + i) * 3 + j] = -a;
+            Jvi[(6 + i) * 3 + j] = -b * dt;
+            Jvj[(3 + i) * 3 + j] = a;
+        }
+    /* J_bg = S * [-Jr^{-1}(-er) J_Rg ; -J_Vg ; -J_Pg]  with er the WEIGHTED rotation residual */
+    double mer[3] = {-r[0], -r[1], -r[2]}, Jr[9], Jri[9], T[27], A[9];
+    imu_right_jac(mer, Jr);
+    dense_inverse(3, Jr, Jri);
+    m3_mul(Jri, c->JRg, A);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            T[i * 3 + j] = -A[3 * i + j];
+            T[(3 + i) * 3 + j] = -c->JVg[3 * i + j];
+            T[(6 + i) * 3 + j] = -c->JPg[3 * i + j];
+        }
+    for (int i = 0; i < 9; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0;
+            for (int k = 0; k < 9; ++k) s += S[i * 9 + k] * T[k * 3 + j];
+            Jbg[i * 3 + j] = s;
+        }
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            T[i * 3 + j] = 0.0;
+            T[(3 + i) * 3 + j] = -c->JVa[3 * i + j];
+            T[(6 + i) * 3 + j] = -c->JPa[3 * i + j];
+        }
+    for (int i = 0; i < 9; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0;
+            for (int k = 0; k < 9; ++k) s += S[i * 9 + k] * T[k * 3 + j];
+            Jba[i * 3 + j] = s;
+        }
+}
+
+/* exported single-factor evaluators for golden/FD tests */
+int oracle_ba_factor(const vio_pose* T_wb_init, const vio_pose* T_cb, const double* delta, const double* Pw,
+                     double u, double v, double cols, double rows, int outlier, int is_pnp, double* r,
+                     double* Jp, double* Jl) {
+    pose_ctx pc;
+    oracle_nearest_rotation(T_wb_init->R, pc.R_init);
+    memcpy(pc.t_init, T_wb_init->t, sizeof pc.t_init);
+    oracle_nearest_rotation(T_cb->R, pc.R_cb);
+    memcpy(pc.t_cb, T_cb->t, sizeof pc.t_cb);
+    memcpy(pc.R_cb_raw, T_cb->R, sizeof pc.R_cb_raw);
+    return factor_eval(&pc, delta, Pw, u, v, cols, rows, NULL, outlier, is_pnp, r, Jp, Jl);
+}
+void oracle_imu_factor(const vio_preint* p, const double* g, const vio_pose* Ti, const vio_pose* Tj,
+                       const double* di, const double* vi, const double* bg, const double* ba, const double* dj,
+                       const double* vj, double* r, double* Jvi, double* Jbg, double* Jba, double* Jvj,
+                       double* sqrt_info) {
+    imu_ctx c;
+    imu_ctx_init(&c, p, g, Ti, Tj);
+    imu_eval(&c, di, vi, bg, ba, dj, vj, r, Jvi, Jbg, Jba, Jvj);
+    if (sqrt_info) memcpy(sqrt_info, c.sqrt_info, sizeof c.sqrt_info);
+}
+
+/* ========================================================================================= */
+/* Generic Ceres-2.0 LM minimiser (TrustRegionMinimizer + LevenbergMarquardtStrategy)         */
+/* ========================================================================================= */
+typedef struct {
+    int n;
+    void* user;
+    /* evaluate at x; cost out; when want_jac, cache Jacobian + residuals internally and write the
+       unscaled gradient J^T r into g and squared column norms into colsq. Return 1 ok, 0 fail. */
+    int (*eval)(void* user, const double* x, double* cost, int want_jac, double* g, double* colsq);
+    /* solve (J~^T J~ + D^2) y = J~^T r with J~ = J diag(s); return 1 ok, 0 linear-solver failure */
+    int (*solve)(void* user, const double* s, const double* D, double* y);
+    /* model cost change -(J~ h)^T (r + J~ h / 2) for the scaled step h */
+    double (*model_change)(void* user, const double* s, const double* h);
+} lm_problem;
+
+typedef struct {
+    int max_iterations;
+    int fixed_iterations; /* disable all convergence tests */
+    double function_tolerance, gradient_tolerance, parameter_tolerance;
+    double initial_radius, max_radius, min_radius, min_relative_decrease;
+    double min_diagonal, max_diagonal;
+    int max_consecutive_invalid;
+    double fixed_cost;
+} lm_options;
+
+typedef struct {
+    int termination;
+    int iterations; /* iterations.size() */
+    int successful, unsuccessful;
+    double initial_cost, final_cost;
+    /* trace for tests */
+    int trace_n;
+    double trace_cost[64], trace_radius[64];
+    int trace_ok[64];
+} lm_summary;
+
+void oracle_lm_default_options(lm_options* o) {
+    o->max_iterations = 50;
+    o->fixed_iterations = 0;
+    o->function_tolerance = 1e-6;
+    o->gradient_tolerance = 1e-10;
+    o->parameter_tolerance = 1e-8;
+    o->initial_radius = 1e4;
+    o->max_radius = 1e16;
+    o->min_radius = 1e-32;
+    o->min_relative_decrease = 1e-3;
+    o->min_diagonal = 1e-6;
+    o->max_diagonal = 1e32;
+    o->max_consecutive_invalid = 5;
+    o->fixed_cost = 0.0;
+}
+
+/* LevenbergMarquardtStrategy radius updates (levenberg_marquardt_strategy.cc:147-160) */
+typedef struct { double radius, decrease_factor, max_radius; } lm_radius;
+void oracle_lm_step_accepted(lm_radius* s, double q) {
+    s->radius = s->radius / fmax(1.0 / 3.0, 1.0 - pow(2.0 * q - 1.0, 3));
+    s->radius = fmin(s->max_radius, s->radius);
+    s->decrease_factor = 2.0;
+}
+void oracle_lm_step_rejected(lm_radius* s) {
+    s->radius = s->radius / s->decrease_factor;
+    s->decrease_factor *= 2.0;
+}
+
+static void push_trace(lm_summary* sum, double cost, double radius, int ok) {
+    if (sum->trace_n < 64) {
+        sum->trace_cost[sum->trace_n] = cost;
+        sum->trace_radius[sum->trace_n] = radius;
+        sum->trace_ok[sum->trace_n] = ok;
+        sum->trace_n++;
+    }
+}
+
+/* LM diagonal D = sqrt(clamp(diag(J~^T J~), min, max) / radius) (levenberg_marquardt_strategy.cc:76-88),
+   with diag(J~^T J~) = colsq .* s .* s for the Jacobi-scaled Jacobian */
+void oracle_lm_diagonal(int n, const double* colsq, const double* s, double radius, double dmin, double dmax,
+                        double* D) {
+    for (int i = 0; i < n; ++i) {
+        double d = colsq[i] * s[i] * s[i];
+        d = fmin(fmax(d, dmin), dmax);
+        D[i] = sqrt(d / radius);
+    }
+}
+
+/* x in/out: on return holds the solution Ceres would copy back to the user */
+int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_user, lm_summary* sum) {
+    const int n = P->n;
+    memset(sum, 0, sizeof *sum);
+    sum->termination = VIO_TERM_NO_CONVERGENCE;
+    double* x = (double*)malloc(sizeof(double) * n);
+    double* x0 = (double*)malloc(sizeof(double) * n);
+    double* g = (double*)malloc(sizeof(double) * n);
+    double* colsq = (double*)malloc(sizeof(double) * n);
+    double* s = (double*)malloc(sizeof(double) * n);
+    double* D = (double*)malloc(sizeof(double) * n);
+    double* y = (double*)malloc(sizeof(double) * n);
+    double* delta = (double*)malloc(sizeof(double) * n);
+    double* cand = (double*)malloc(sizeof(double) * n);
+    memcpy(x, x_user, sizeof(double) * n);
+    memcpy(x0, x_user, sizeof(double) * n);
+    double x_norm = -1.0; /* trust_region_minimizer.cc:185 */
+    double x_cost = DBL_MAX;
+    double minimum_cost = DBL_MAX;
+    lm_radius rad = {opt->initial_radius, 2.0, opt->max_radius};
+    int consecutive_invalid = 0;
+    const int fixed = opt->fixed_iterations;
+
+    /* IterationZero */
+    if (!P->eval(P->user, x, &x_cost, 1, g, colsq)) {
+        sum->termination = VIO_TERM_FAILURE;
+        sum->initial_cost = opt->fixed_cost; /* never set by Ceres on this path */
+        sum->final_cost = sum->initial_cost;
+        goto done;
+    }
+    for (int i = 0; i < n; ++i) s[i] = 1.0 / (1.0 + sqrt(colsq[i]));
+    double gmax = 0;
+    for (int i = 0; i < n; ++i) gmax = fmax(gmax, fabs(g[i]));
+    sum->initial_cost = x_cost + opt->fixed_cost;
+    double step_evaluator_current = x_cost;
+    int iteration = 0;
+    int step_successful = 1;
+    double iter_cost = x_cost + opt->fixed_cost;
+    double final_cost = sum->initial_cost;
+    double model_change = 0, cand_cost = 0;
+
+    for (;;) {
+        /* FinalizeIterationAndCheckIfMinimizerCanContinue */
+        if (step_successful) {
+            sum->successful++;
+            if (x_cost < minimum_cost) {
+                minimum_cost = x_cost;
+                memcpy(x_user, x, sizeof(double) * n);
+            }
+        } else {
+            sum->unsuccessful++;
+        }
+        sum->iterations++;
+        final_cost = fmin(final_cost, iter_cost);
+        push_trace(sum, iter_cost, rad.radius, step_successful);
+        if (iteration >= opt->max_iterations) { sum->termination = VIO_TERM_NO_CONVERGENCE; break; }
+        if (!fixed && step_successful && gmax <= opt->gradient_tolerance) { sum->termination = VIO_TERM_CONVERGENCE; break; }
+        if (!fixed && rad.radius <= opt->min_radius) { sum->termination = VIO_TERM_CONVERGENCE; break; }
+
+        iteration++;
+        /* ComputeTrustRegionStep */
+        oracle_lm_diagonal(n, colsq, s, rad.radius, opt->min_diagonal, opt->max_diagonal, D);
+        int valid = P->solve(P->user, s, D, y);
+        if (valid) {
+            for (int i = 0; i < n; ++i)
+                if (!isfinite(y[i])) valid = 0;
+        }
+        if (valid) {
+            for (int i = 0; i < n; ++i) y[i] = -y[i]; /* trust_region_step */
+            model_change = P->model_change(P->user, s, y);
+            valid = model_change > 0.0;
+        }
+        if (!valid) {
+            /* HandleInvalidStep */
+            if (++consecutive_invalid >= opt->max_consecutive_invalid) {
+                sum->termination = VIO_TERM_FAILURE;
+                break;
+            }
+            oracle_lm_step_rejected(&rad);
+            step_successful = 0;
+            iter_cost = x_cost + opt->fixed_cost;
+            continue;
+        }
+        consecutive_invalid = 0;
+        for (int i = 0; i < n; ++i) delta[i] = y[i] * s[i];
+        for (int i = 0; i < n; ++i) cand[i] = x[i] + delta[i];
+        if (!P->eval(P->user, cand, &cand_cost, 0, NULL, NULL)) cand_cost = DBL_MAX;
+
+        /* ParameterToleranceReached */
+        double step_norm = 0;
+        for (int i = 0; i < n; ++i) { double d = x[i] - cand[i]; step_norm += d * d; }
+        step_norm = sqrt(step_norm);
+        if (!fixed && step_norm <= opt->parameter_tolerance * (x_norm + opt->parameter_tolerance)) {
+            sum->termination = VIO_TERM_CONVERGENCE;
+            break;
+        }
+        /* FunctionToleranceReached */
+        if (!fixed && fabs(x_cost - cand_cost) <= opt->function_tolerance * x_cost) {
+            sum->termination = VIO_TERM_CONVERGENCE;
+            break;
+        }
+        /* IsStepSuccessful */
+        double rel;
+        if (cand_cost >= DBL_MAX) rel = -DBL_MAX;
+        else rel = (step_evaluator_current - cand_cost) / model_change;
+        if (rel > opt->min_relative_decrease) {
+            /* HandleSuccessfulStep */
+            memcpy(x, cand, sizeof(double) * n);
+            double xn = 0;
+            for (int i = 0; i < n; ++i) xn += x[i] * x[i];
+            x_norm = sqrt(xn);
+            if (!P->eval(P->user, x, &x_cost, 1, g, colsq)) {
+                sum->termination = VIO_TERM_FAILURE;
+                break;
+            }
+            gmax = 0;
+            for (int i = 0; i < n; ++i) gmax = fmax(gmax, fabs(g[i]));
+            step_successful = 1;
+            oracle_lm_step_accepted(&rad, rel);
+            step_evaluator_current = cand_cost;
+            iter_cost = x_cost + opt->fixed_cost;
+        } else {
+            step_successful = 0;
+            iter_cost = cand_cost + opt->fixed_cost;
+            oracle_lm_step_rejected(&rad);
+        }
+    }
+    sum->final_cost = final_cost;
+done:
+    if (sum->termination == VIO_TERM_FAILURE) memcpy(x_user, x0, sizeof(double) * n);
+    free(x); free(x0); free(g); free(colsq); free(s); free(D); free(y); free(delta); free(cand);
+    return 0;
+}
+
+/* ========================================================================================= */
+/* BA problem on top of the generic minimiser                                                 */
+/* ========================================================================================= */
+typedef struct {
+    const vio_ba_problem* p;
+    int K, L, N;
+    int is_pnp, is_vi;
+    pose_ctx* pc;       /* K */
+    double Lw[4];       /* chol(info) lower */
+    double info[4];
+    /* parameter layout */
+    int* pose_off;      /* K: offset into x or -1 (constant or unused) */
+    int* lm_off;        /* L: offset (e-block) or -1 */
+    int* vel_off;       /* K */
+    int bg_off, ba_off;
+    int nf;             /* number of f-parameters (poses, velocities, biases) */
+    int n;              /* total */
+    int* f_index;       /* map f-param global offset -> 0..nf-1 (size n, -1 for points) */
+    /* current values of every block (constant ones included) */
+    double* pose_val;   /* K*6 */
+    double* lm_val;     /* L*3 */
+    double* vel_val;    /* K*3 */
+    double bg_val[3], ba_val[3];
+    /* residual blocks */
+    uint8_t* obs_active; /* N */
+    uint8_t* obs_outlier;/* N (PnP rounds) */
+    imu_ctx* imu;        /* K (entry k links k-1 -> k) */
+    uint8_t* imu_active; /* K */
+    /* cached linearisation */
+    double* r;           /* N*2 corrected residuals */
+    double* Jp;          /* N*12 */
+    double* Jl;          /* N*6 */
+    double* ri;          /* K*9 */
+    double* Ji;          /* K*4*27 (vi, bg, ba, vj) */
+    /* CSR of observations per landmark */
+    int* lm_ptr;
+    int* lm_obs;
+    int eval_failed;
+} ba_ctx;
+
+static void ba_unpack(ba_ctx* c, const double* x) {
+    for (int k = 0; k < c->K; ++k) {
+        if (c->pose_off[k] >= 0) memcpy(c->pose_val + 6 * k, x + c->pose_off[k], 6 * sizeof(double));
+        if (c->vel_off && c->vel_off[k] >= 0) memcpy(c->vel_val + 3 * k, x + c->vel_off[k], 3 * sizeof(double));
+    }
+    for (int l = 0; l < c->L; ++l)
+        if (c->lm_off[l] >= 0) memcpy(c->lm_val + 3 * l, x + c->lm_off[l], 3 * sizeof(double));
+    if (c->bg_off >= 0) memcpy(c->bg_val, x + c->bg_off, 3 * sizeof(double));
+    if (c->ba_off >= 0) memcpy(c->ba_val, x + c->ba_off, 3 * sizeof(double));
+}
+
+/* evaluate one visual residual block with the loss applied; returns 0 on factor failure */
+static int ba_eval_obs(ba_ctx* c, int o, double* cost, double* r, double* Jp, double* Jl) {
+    const vio_ba_problem* p = c->p;
+    int k = p->obs_kf[o], l = p->obs_lm[o];
+    double rr[2];
+    int ok = factor_eval(&c->pc[k], c->pose_val + 6 * k, c->lm_val + 3 * l, (double)p->obs_uv[2 * o],
+                         (double)p->obs_uv[2 * o + 1], p->cols, p->rows, c->Lw, c->obs_outlier[o], c->is_pnp, rr, Jp, Jl);
+    if (!ok) return 0;
+    double sq = rr[0] * rr[0] + rr[1] * rr[1], rho[3];
+    oracle_huber(p->huber_delta, sq, rho);
+    *cost = 0.5 * rho[0];
+    double rs, asq, sr1;
+    oracle_corrector(sq, rho, &rs, &asq, &sr1);
+    if (Jp || Jl) {
+        /* CorrectJacobian uses the UNcorrected residual (residual_block.cc:178-189) */
+        double* Js[2] = {Jp, Jl};
+        int nc[2] = {6, 3};
+        for (int b = 0; b < 2; ++b) {
+            double* J = Js[b];
+            if (!J) continue;
+            if (asq == 0.0) {
+                for (int i = 0; i < 2 * nc[b]; ++i) J[i] *= sr1;
+            } else {
+                for (int cc = 0; cc < nc[b]; ++cc) {
+                    double rtj = J[cc] * rr[0] + J[nc[b] + cc] * rr[1];
+                    for (int row = 0; row < 2; ++row)
+                        J[row * nc[b] + cc] = sr1 * (J[row * nc[b] + cc] - asq * rr[row] * rtj);
+                }
+            }
+        }
+    }
+    r[0] = rr[0] * rs;
+    r[1] = rr[1] * rs;
+    return 1;
+}
+
+static int ba_eval(void* user, const double* x, double* cost, int want_jac, double* g, double* colsq) {
+    ba_ctx* c = (ba_ctx*)user;
+    ba_unpack(c, x);
+    double total = 0.0;
+    if (want_jac) {
+        memset(g, 0, sizeof(double) * c->n);
+        memset(colsq, 0, sizeof(double) * c->n);
+    }
+    for (int o = 0; o < c->N; ++o) {
+        if (!c->obs_active[o]) continue;
+        int k = c->p->obs_kf[o], l = c->p->obs_lm[o];
+        double cst, r[2];
+        double* Jp = want_jac ? c->Jp + 12 * o : NULL;
+        double* Jl = want_jac ? c->Jl + 6 * o : NULL;
+        if (!ba_eval_obs(c, o, &cst, r, Jp, Jl)) return 0;
+        total += cst;
+        if (want_jac) {
+            c->r[2 * o] = r[0];
+            c->r[2 * o + 1] = r[1];
+            int po = c->pose_off[k], lo = c->lm_off[l];
+            if (po >= 0)
+                for (int j = 0; j < 6; ++j) {
+                    g[po + j] += Jp[j] * r[0] + Jp[6 + j] * r[1];
+                    colsq[po + j] += Jp[j] * Jp[j] + Jp[6 + j] * Jp[6 + j];
+                }
+            if (lo >= 0)
+                for (int j = 0; j < 3; ++j) {
+                    g[lo + j] += Jl[j] * r[0] + Jl[3 + j] * r[1];
+                    colsq[lo + j] += Jl[j] * Jl[j] + Jl[3 + j] * Jl[3 + j];
+                }
+        }
+    }
+    if (c->is_vi) {
+        for (int k = 1; k < c->K; ++k) {
+            if (!c->imu_active[k]) continue;
+            double r[9];
+            double* J = c->Ji + 108 * k;
+            imu_eval(&c->imu[k], c->pose_val + 6 * (k - 1), c->vel_val + 3 * (k - 1), c->bg_val, c->ba_val,
+                     c->pose_val + 6 * k, c->vel_val + 3 * k, r, want_jac ? J : NULL, want_jac ? J + 27 : NULL,
+                     want_jac ? J + 54 : NULL, want_jac ? J + 81 : NULL);
+            double sq = 0;
+            for (int i = 0; i < 9; ++i) sq += r[i] * r[i];
+            total += 0.5 * sq;
+            if (want_jac) {
+                memcpy(c->ri + 9 * k, r, sizeof r);
+                int offs[4] = {c->vel_off[k - 1], c->bg_off, c->ba_off, c->vel_off[k]};
+                for (int b = 0; b < 4; ++b) {
+                    if (offs[b] < 0) continue;
+                    for (int j = 0; j < 3; ++j)
+                        for (int i = 0; i < 9; ++i) {
+                            double v = J[27 * b + 3 * i + j];
+                            g[offs[b] + j] += v * r[i];
+                            colsq[offs[b] + j] += v * v;
+                        }
+                }
+            }
+        }
+    }
+    *cost = total;
+    return 1;
+}
+
+/* Schur complement solve: points are the e-blocks, everything else the reduced system */
+static int ba_solve(void* user, const double* s, const double* D, double* y) {
+    ba_ctx* c = (ba_ctx*)user;
+    const vio_ba_problem* p = c->p;
+    int nf = c->nf;
+    double* S = (double*)calloc((size_t)(nf > 0 ? nf : 1) * (nf > 0 ? nf : 1), sizeof(double));
+    double* bf = (double*)calloc(nf > 0 ? nf : 1, sizeof(double));
+    /* f-block normal equations: scaled J^T J and J^T r */
+    for (int o = 0; o < c->N; ++o) {
+        if (!c->obs_active[o]) continue;
+        int po = c->pose_off[p->obs_kf[o]];
+        if (po < 0) continue;
+        int fi = c->f_index[po];
+        const double* J = c->Jp + 12 * o;
+        const double* r = c->r + 2 * o;
+        for (int a = 0; a < 6; ++a) {
+            bf[fi + a] += s[po + a] * (J[a] * r[0] + J[6 + a] * r[1]);
+            for (int b = 0; b < 6; ++b)
+                S[(fi + a) * nf + fi + b] += s[po + a] * s[po + b] * (J[a] * J[b] + J[6 + a] * J[6 + b]);
+        }
+    }
+    if (c->is_vi) {
+        for (int k = 1; k < c->K; ++k) {
+            if (!c->imu_active[k]) continue;
+            const double* J = c->Ji + 108 * k;
+            const double* r = c->ri + 9 * k;
+            int offs[4] = {c->vel_off[k - 1], c->bg_off, c->ba_off, c->vel_off[k]};
+            for (int a = 0; a < 4; ++a) {
+                if (offs[a] < 0) continue;
+                int fa = c->f_index[offs[a]];
+                for (int i = 0; i < 3; ++i) {
+                    double gsum = 0;
+                    for (int q = 0; q < 9; ++q) gsum += J[27 * a + 3 * q + i] * r[q];
+                    bf[fa + i] += s[offs[a] + i] * gsum;
+                }
+                for (int b = 0; b < 4; ++b) {
+                    if (offs[b] < 0) continue;
+                    int fb = c->f_index[offs[b]];
+                    for (int i = 0; i < 3; ++i)
+                        for (int j = 0; j < 3; ++j) {
+                            double h = 0;
+                            for (int q = 0; q < 9; ++q) h += J[27 * a + 3 * q + i] * J[27 * b + 3 * q + j];
+                            S[(fa + i) * nf + fb + j] += s[offs[a] + i] * s[offs[b] + j] * h;
+                        }
+                }
+            }
+        }
+    }
+    for (int i = 0; i < c->n; ++i)
+        if (c->f_index[i] >= 0) S[c->f_index[i] * nf + c->f_index[i]] += D[i] * D[i];
+    /* eliminate points (SchurEliminator::Eliminate) */
+    double* Vinv = (double*)malloc(sizeof(double) * 9 * (c->L > 0 ? c->L : 1));
+    double* gl = (double*)malloc(sizeof(double) * 3 * (c->L > 0 ? c->L : 1));
+    for (int l = 0; l < c->L; ++l) {
+        int lo = c->lm_off[l];
+        if (lo < 0) continue;
+        double V[9] = {0}, g[3] = {0};
+        for (int q = c->lm_ptr[l]; q < c->lm_ptr[l + 1]; ++q) {
+            int o = c->lm_obs[q];
+            if (!c->obs_active[o]) continue;
+            const double* J = c->Jl + 6 * o;
+            const double* r = c->r + 2 * o;
+            for (int a = 0; a < 3; ++a) {
+                g[a] += s[lo + a] * (J[a] * r[0] + J[3 + a] * r[1]);
+                for (int b = 0; b < 3; ++b) V[3 * a + b] += s[lo + a] * s[lo + b] * (J[a] * J[b] + J[3 + a] * J[3 + b]);
+            }
+        }
+        for (int a = 0; a < 3; ++a) V[4 * a] += D[lo + a] * D[lo + a];
+        /* inverse via LLT */
+        double Lc[9];
+        memcpy(Lc, V, sizeof Lc);
+        if (dense_llt(3, Lc) != 0) { free(S); free(bf); free(Vinv); free(gl); return 0; }
+        double* Vi = Vinv + 9 * l;
+        for (int cc = 0; cc < 3; ++cc) {
+            double e[3] = {0, 0, 0};
+            e[cc] = 1.0;
+            dense_llt_solve(3, Lc, e);
+            for (int rr = 0; rr < 3; ++rr) Vi[3 * rr + cc] = e[rr];
+        }
+        memcpy(gl + 3 * l, g, sizeof g);
+        /* Y_a = W~_a V^-1 (6x3) for each obs; S -= Y_a W~_b^T ; b -= Y_a g */
+        for (int qa = c->lm_ptr[l]; qa < c->lm_ptr[l + 1]; ++qa) {
+            int oa = c->lm_obs[qa];
+            if (!c->obs_active[oa]) continue;
+            int pa = c->pose_off[p->obs_kf[oa]];
+            if (pa < 0) continue;
+            int fa = c->f_index[pa];
+            double W[18], Y[18];
+            const double* Jp = c->Jp + 12 * oa;
+            const double* Jl = c->Jl + 6 * oa;
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 3; ++j)
+                    W[3 * i + j] = s[pa + i] * s[lo + j] * (Jp[i] * Jl[j] + Jp[6 + i] * Jl[3 + j]);
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 3; ++j)
+                    Y[3 * i + j] = W[3 * i] * Vi[j] + W[3 * i + 1] * Vi[3 + j] + W[3 * i + 2] * Vi[6 + j];
+            for (int i = 0; i < 6; ++i) bf[fa + i] -= Y[3 * i] * g[0] + Y[3 * i + 1] * g[1] + Y[3 * i + 2] * g[2];
+            for (int qb = c->lm_ptr[l]; qb < c->lm_ptr[l + 1]; ++qb) {
+                int ob = c->lm_obs[qb];
+                if (!c->obs_active[ob]) continue;
+                int pb = c->pose_off[p->obs_kf[ob]];
+                if (pb < 0) continue;
+                int fb = c->f_index[pb];
+                const double* Jpb = c->Jp + 12 * ob;
+                const double* Jlb = c->Jl + 6 * ob;
+                double Wb[18];
+                for (int i = 0; i < 6; ++i)
+                    for (int j = 0; j < 3; ++j)
+                        Wb[3 * i + j] = s[pb + i] * s[lo + j] * (Jpb[i] * Jlb[j] + Jpb[6 + i] * Jlb[3 + j]);
+                for (int i = 0; i < 6; ++i)
+                    for (int j = 0; j < 6; ++j)
+                        S[(fa + i) * nf + fb + j] -= Y[3 * i] * Wb[3 * j] + Y[3 * i + 1] * Wb[3 * j + 1] + Y[3 * i + 2] * Wb[3 * j + 2];
+            }
+        }
+    }
+    /* reduced solve (dense LLT; SPARSE_SCHUR's LDLT is the same factorisation up to roundoff) */
+    if (nf > 0) {
+        if (dense_llt(nf, S) != 0) { free(S); free(bf); free(Vinv); free(gl); return 0; }
+        dense_llt_solve(nf, S, bf);
+    }
+    for (int i = 0; i < c->n; ++i)
+        if (c->f_index[i] >= 0) y[i] = bf[c->f_index[i]];
+    /* back-substitution (SchurEliminator::BackSubstitute) */
+    for (int l = 0; l < c->L; ++l) {
+        int lo = c->lm_off[l];
+        if (lo < 0) continue;
+        double rhs[3] = {gl[3 * l], gl[3 * l + 1], gl[3 * l + 2]};
+        for (int q = c->lm_ptr[l]; q < c->lm_ptr[l + 1]; ++q) {
+            int o = c->lm_obs[q];
+            if (!c->obs_active[o]) continue;
+            int po = c->pose_off[p->obs_kf[o]];
+            if (po < 0) continue;
+            const double* Jp = c->Jp + 12 * o;
+            const double* Jl = c->Jl + 6 * o;
+            for (int j = 0; j < 3; ++j) {
+                double w = 0;
+                for (int i = 0; i < 6; ++i) w += s[po + i] * s[lo + j] * (Jp[i] * Jl[j] + Jp[6 + i] * Jl[3 + j]) * y[po + i];
+                rhs[j] -= w;
+            }
+        }
+        const double* Vi = Vinv + 9 * l;
+        for (int j = 0; j < 3; ++j) y[lo + j] = Vi[3 * j] * rhs[0] + Vi[3 * j + 1] * rhs[1] + Vi[3 * j + 2] * rhs[2];
+    }
+    free(S); free(bf); free(Vinv); free(gl);
+    return 1;
+}
+
+static double ba_model_change(void* user, const double* s, const double* h) {
+    ba_ctx* c = (ba_ctx*)user;
+    const vio_ba_problem* p = c->p;
+    double mc = 0.0;
+    for (int o = 0; o < c->N; ++o) {
+        if (!c->obs_active[o]) continue;
+        int po = c->pose_off[p->obs_kf[o]], lo = c->lm_off[p->obs_lm[o]];
+        double m[2] = {0, 0};
+        if (po >= 0)
+            for (int j = 0; j < 6; ++j) {
+                double hj = s[po + j] * h[po + j];
+                m[0] += c->Jp[12 * o + j] * hj;
+                m[1] += c->Jp[12 * o + 6 + j] * hj;
+            }
+        if (lo >= 0)
+            for (int j = 0; j < 3; ++j) {
+                double hj = s[lo + j] * h[lo + j];
+                m[0] += c->Jl[6 * o + j] * hj;
+                m[1] += c->Jl[6 * o + 3 + j] * hj;
+            }
+        mc -= m[0] * (c->r[2 * o] + m[0] / 2.0) + m[1] * (c->r[2 * o + 1] + m[1] / 2.0);
+    }
+    if (c->is_vi) {
+        for (int k = 1; k < c->K; ++k) {
+            if (!c->imu_active[k]) continue;
+            const double* J = c->Ji + 108 * k;
+            int offs[4] = {c->vel_off[k - 1], c->bg_off, c->ba_off, c->vel_off[k]};
+            double m[9] = {0};
+            for (int b = 0; b < 4; ++b) {
+                if (offs[b] < 0) continue;
+                for (int i = 0; i < 9; ++i)
+                    for (int j = 0; j < 3; ++j) m[i] += J[27 * b + 3 * i + j] * s[offs[b] + j] * h[offs[b] + j];
+            }
+            for (int i = 0; i < 9; ++i) mc -= m[i] * (c->ri[9 * k + i] + m[i] / 2.0);
+        }
+    }
+    return mc;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+static void pose_ctx_init(pose_ctx* pc, const vio_pose* Twb, const vio_pose* Tcb) {
+    oracle_nearest_rotation(Twb->R, pc->R_init);
+    memcpy(pc->t_init, Twb->t, sizeof pc->t_init);
+    oracle_nearest_rotation(Tcb->R, pc->R_cb);
+    memcpy(pc->t_cb, Tcb->t, sizeof pc->t_cb);
+    memcpy(pc->R_cb_raw, Tcb->R, sizeof pc->R_cb_raw);
+}
+
+static int ba_ctx_build(ba_ctx* c, const vio_ba_problem* p) {
+    memset(c, 0, sizeof *c);
+    c->p = p;
+    c->K = p->num_kf; c->L = p->num_lm; c->N = p->num_obs;
+    c->is_pnp = p->variant == VIO_PNP;
+    c->is_vi = p->variant == VIO_BA_VI;
+    int K = c->K, L = c->L, N = c->N;
+    c->pc = (pose_ctx*)malloc(sizeof(pose_ctx) * K);
+    for (int k = 0; k < K; ++k) pose_ctx_init(&c->pc[k], &p->T_wb_init[k], &p->T_cb[k]);
+    /* chol(info): identity info → L = I (Eigen LLT of the 2x2) */
+    memcpy(c->info, p->info, sizeof c->info);
+    {
+        double a = p->info[0], b = p->info[2], d = p->info[3];
+        if (a > 0) {
+            double l00 = sqrt(a), l10 = b / l00, t = d - l10 * l10;
+            if (t > 0) { c->Lw[0] = l00; c->Lw[1] = 0; c->Lw[2] = l10; c->Lw[3] = sqrt(t); }
+            else { c->Lw[0] = 1; c->Lw[1] = 0; c->Lw[2] = 0; c->Lw[3] = 1; }
+        } else { c->Lw[0] = 1; c->Lw[1] = 0; c->Lw[2] = 0; c->Lw[3] = 1; }
+    }
+    c->pose_val = (double*)calloc(6 * K, sizeof(double));
+    c->lm_val = (double*)malloc(sizeof(double) * 3 * (L > 0 ? L : 1));
+    memcpy(c->lm_val, p->lm_xyz, sizeof(double) * 3 * L);
+    c->vel_val = (double*)calloc(3 * K, sizeof(double));
+    if (c->is_vi) {
+        memcpy(c->vel_val, p->vel, sizeof(double) * 3 * K);
+        memcpy(c->bg_val, p->bg, sizeof c->bg_val);
+        memcpy(c->ba_val, p->ba, sizeof c->ba_val);
+    }
+    c->obs_active = (uint8_t*)calloc(N > 0 ? N : 1, 1);
+    c->obs_outlier = (uint8_t*)calloc(N > 0 ? N : 1, 1);
+    c->r = (double*)calloc(2 * (size_t)(N > 0 ? N : 1), sizeof(double));
+    c->Jp = (double*)calloc(12 * (size_t)(N > 0 ? N : 1), sizeof(double));
+    c->Jl = (double*)calloc(6 * (size_t)(N > 0 ? N : 1), sizeof(double));
+    c->imu = (imu_ctx*)calloc(K, sizeof(imu_ctx));
+    c->imu_active = (uint8_t*)calloc(K, 1);
+    c->ri = (double*)calloc(9 * K, sizeof(double));
+    c->Ji = (double*)calloc(108 * K, sizeof(double));
+    /* which blocks are variable and used */
+    uint8_t* pose_used = (uint8_t*)calloc(K, 1);
+    uint8_t* lm_used = (uint8_t*)calloc(L > 0 ? L : 1, 1);
+    uint8_t* vel_used = (uint8_t*)calloc(K, 1);
+    int bias_used = 0;
+    for (int o = 0; o < N; ++o) {
+        int k = p->obs_kf[o], l = p->obs_lm[o];
+        int kvar = !p->kf_const[k];
+        int lvar = !c->is_pnp && !p->lm_const[l];
+        if (kvar || lvar) {
+            c->obs_active[o] = 1;
+            if (kvar) pose_used[k] = 1;
+            if (lvar) lm_used[l] = 1;
+        }
+    }
+    if (c->is_vi) {
+        for (int k = 1; k < K; ++k) {
+            if (!p->preint_valid[k]) continue;
+            c->imu_active[k] = 1; /* velocities and biases are never constant in RunVIBA */
+            imu_ctx_init(&c->imu[k], &p->preint[k], p->gravity, &p->T_wb_init[k - 1], &p->T_wb_init[k]);
+            vel_used[k - 1] = vel_used[k] = 1;
+            bias_used = 1;
+            /* pose blocks of an IMU factor enter the problem through it as well */
+            if (!p->kf_const[k - 1]) pose_used[k - 1] = 1;
+            if (!p->kf_const[k]) pose_used[k] = 1;
+        }
+    }
+    c->pose_off = (int*)malloc(sizeof(int) * K);
+    c->vel_off = (int*)malloc(sizeof(int) * K);
+    c->lm_off = (int*)malloc(sizeof(int) * (L > 0 ? L : 1));
+    int off = 0;
+    for (int k = 0; k < K; ++k) { c->pose_off[k] = pose_used[k] ? off : -1; if (pose_used[k]) off += 6; }
+    for (int k = 0; k < K; ++k) { c->vel_off[k] = vel_used[k] ? off : -1; if (vel_used[k]) off += 3; }
+    c->bg_off = bias_used ? off : -1; if (bias_used) off += 3;
+    c->ba_off = bias_used ? off : -1; if (bias_used) off += 3;
+    c->nf = off;
+    for (int l = 0; l < L; ++l) { c->lm_off[l] = lm_used[l] ? off : -1; if (lm_used[l]) off += 3; }
+    c->n = off;
+    c->f_index = (int*)malloc(sizeof(int) * (off > 0 ? off : 1));
+    for (int i = 0; i < off; ++i) c->f_index[i] = i < c->nf ? i : -1;
+    /* CSR by landmark */
+    c->lm_ptr = (int*)calloc(L + 1, sizeof(int));
+    c->lm_obs = (int*)malloc(sizeof(int) * (N > 0 ? N : 1));
+    for (int o = 0; o < N; ++o) c->lm_ptr[p->obs_lm[o] + 1]++;
+    for (int l = 0; l < L; ++l) c->lm_ptr[l + 1] += c->lm_ptr[l];
+    int* fill = (int*)calloc(L > 0 ? L : 1, sizeof(int));
+    for (int o = 0; o < N; ++o) {
+        int l = p->obs_lm[o];
+        c->lm_obs[c->lm_ptr[l] + fill[l]++] = o;
+    }
+    free(fill);
+    free(pose_used); free(lm_used); free(vel_used);
+    return 0;
+}
+
+static void ba_ctx_free(ba_ctx* c) {
+    free(c->pc); free(c->pose_val); free(c->lm_val); free(c->vel_val); free(c->obs_active); free(c->obs_outlier);
+    free(c->r); free(c->Jp); free(c->Jl); free(c->imu); free(c->imu_active); free(c->ri); free(c->Ji);
+    free(c->pose_off); free(c->vel_off); free(c->lm_off); free(c->f_index); free(c->lm_ptr); free(c->lm_obs);
+}
+
+/* cost of the residual blocks whose parameters are all constant (program.cc:305-390) */
+static double ba_fixed_cost(ba_ctx* c) {
+    double fc = 0.0;
+    for (int o = 0; o < c->N; ++o) {
+        if (c->obs_active[o]) continue;
+        double cst, r[2];
+        if (ba_eval_obs(c, o, &cst, r, NULL, NULL)) fc += cst;
+    }
+    return fc;
+}
+
+static void ba_pack(ba_ctx* c, double* x) {
+    for (int k = 0; k < c->K; ++k) {
+        if (c->pose_off[k] >= 0) memcpy(x + c->pose_off[k], c->pose_val + 6 * k, 6 * sizeof(double));
+        if (c->vel_off[k] >= 0) memcpy(x + c->vel_off[k], c->vel_val + 3 * k, 3 * sizeof(double));
+    }
+    for (int l = 0; l < c->L; ++l)
+        if (c->lm_off[l] >= 0) memcpy(x + c->lm_off[l], c->lm_val + 3 * l, 3 * sizeof(double));
+    if (c->bg_off >= 0) memcpy(x + c->bg_off, c->bg_val, 3 * sizeof(double));
+    if (c->ba_off >= 0) memcpy(x + c->ba_off, c->ba_val, 3 * sizeof(double));
+}
+
+/* one ceres::Solve on the current block values; updates them in place */
+static void ba_ceres_solve(ba_ctx* c, const lm_options* base, lm_summary* sum) {
+    lm_options opt = *base;
+    opt.fixed_cost = ba_fixed_cost(c);
+    if (c->n == 0) {
+        memset(sum, 0, sizeof *sum);
+        sum->termination = VIO_TERM_CONVERGENCE;
+        sum->initial_cost = sum->final_cost = opt.fixed_cost;
+        return;
+    }
+    double* x = (double*)malloc(sizeof(double) * c->n);
+    ba_pack(c, x);
+    lm_problem P = {c->n, c, ba_eval, ba_solve, ba_model_change};
+    oracle_lm_minimize(&P, &opt, x, sum);
+    ba_unpack(c, x);
+    free(x);
+}
+
+static void write_pose(const pose_ctx* pc, const double* delta, vio_pose* out) {
+    double dR[9], dt[3];
+    se3_exp(delta, dR, dt);
+    se3_mul(pc->R_init, pc->t_init, dR, dt, out->R, out->t);
+}
+
+int oracle_ba_solve(const vio_ba_problem* p, vio_ba_output* out) {
+    if (!p || !out || p->num_kf <= 0 || p->num_lm < 0 || p->num_obs < 0) return VIO_EINVAL;
+    if (p->variant == VIO_BA_VI && (!p->preint || !p->preint_valid || !p->vel)) return VIO_EINVAL;
+    ba_ctx c;
+    ba_ctx_build(&c, p);
+    lm_options opt;
+    oracle_lm_default_options(&opt);
+    opt.max_iterations = p->max_iterations;
+    opt.fixed_iterations = p->fixed_iterations;
+    lm_summary sum;
+    vio_ba_summary S;
+    memset(&S, 0, sizeof S);
+    int N = c.N, L = c.L, K = c.K;
+    double* chi2 = (double*)malloc(sizeof(double) * (N > 0 ? N : 1));
+    uint8_t* outl = (uint8_t*)calloc(N > 0 ? N : 1, 1);
+    const uint8_t* marg = c.is_pnp ? p->lm_const : p->lm_marg;
+
+    if (c.is_pnp) {
+        int rounds = p->num_rounds > 0 ? p->num_rounds : 4;
+        for (int round = 0; round < rounds; ++round) {
+            memset(c.pose_val, 0, sizeof(double) * 6 * K);
+            ba_ceres_solve(&c, &opt, &sum);
+            if (round == 0) S.initial_cost = sum.initial_cost;
+            S.iterations += sum.iterations;
+            S.num_successful_steps += sum.successful;
+            S.num_unsuccessful_steps += sum.unsuccessful;
+            int nin = 0, nout = 0;
+            double inl_sum = 0;
+            for (int o = 0; o < N; ++o) {
+                int k = p->obs_kf[o], l = p->obs_lm[o];
+                double ch = factor_chi2(&c.pc[k], c.pose_val + 6 * k, c.lm_val + 3 * l, (double)p->obs_uv[2 * o],
+                                        (double)p->obs_uv[2 * o + 1], p->cols, p->rows, c.info, c.obs_outlier[o], 1);
+                int m = marg ? marg[l] : 0;
+                int is_out = !m && (ch > p->chi2_threshold);
+                chi2[o] = ch;
+                c.obs_outlier[o] = (uint8_t)is_out;
+                if (is_out) nout++;
+                else { nin++; inl_sum += ch; }
+            }
+            S.num_inliers = nin;
+            S.num_outliers = nout;
+            S.termination = sum.termination;
+            S.success = sum.termination != VIO_TERM_FAILURE;
+            S.final_cost = sum.final_cost;
+            if (nin > 0) S.final_cost = inl_sum / nin;
+        }
+        memcpy(outl, c.obs_outlier, N);
+        if (S.num_inliers < 10) S.success = 0;
+        S.fixed_cost = 0;
+    } else {
+        ba_ceres_solve(&c, &opt, &sum);
+        S.initial_cost = sum.initial_cost;
+        S.final_cost = sum.final_cost;
+        S.iterations = sum.iterations;
+        S.num_successful_steps = sum.successful;
+        S.num_unsuccessful_steps = sum.unsuccessful;
+        S.termination = sum.termination;
+        S.success = sum.termination != VIO_TERM_FAILURE;
+        S.fixed_cost = opt.fixed_cost; /* recomputed inside; same value */
+        S.fixed_cost = ba_fixed_cost(&c);
+        int* lin = (int*)calloc(L > 0 ? L : 1, sizeof(int));
+        int* lout = (int*)calloc(L > 0 ? L : 1, sizeof(int));
+        for (int o = 0; o < N; ++o) {
+            int k = p->obs_kf[o], l = p->obs_lm[o];
+            double ch = factor_chi2(&c.pc[k], c.pose_val + 6 * k, c.lm_val + 3 * l, (double)p->obs_uv[2 * o],
+                                    (double)p->obs_uv[2 * o + 1], p->cols, p->rows, c.info, 0, 0);
+            chi2[o] = ch;
+            int is_out = ch > p->chi2_threshold;
+            outl[o] = (uint8_t)is_out;
+            if (is_out) { S.num_outliers++; lout[l]++; }
+            else { S.num_inliers++; lin[l]++; }
+        }
+        for (int l = 0; l < L; ++l) {
+            int m = marg ? marg[l] : 0;
+            int bad = !m && lin[l] == 0 && lout[l] >= 2;
+            if (out->lm_bad) out->lm_bad[l] = (uint8_t)bad;
+            S.num_bad_lm += bad;
+        }
+        free(lin); free(lout);
+    }
+    if (out->T_wb)
+        for (int k = 0; k < K; ++k) write_pose(&c.pc[k], c.pose_val + 6 * k, &out->T_wb[k]);
+    if (out->lm_xyz) memcpy(out->lm_xyz, c.lm_val, sizeof(double) * 3 * L);
+    if (out->obs_chi2) memcpy(out->obs_chi2, chi2, sizeof(double) * N);
+    if (out->obs_outlier) memcpy(out->obs_outlier, outl, N);
+    if (c.is_pnp && out->lm_bad) memset(out->lm_bad, 0, L);
+    if (c.is_vi) {
+        if (out->vel) memcpy(out->vel, c.vel_val, sizeof(double) * 3 * K);
+        if (out->bg) memcpy(out->bg, c.bg_val, sizeof(double) * 3);
+        if (out->ba) memcpy(out->ba, c.ba_val, sizeof(double) * 3);
+    }
+    if (out->summary) *out->summary = S;
+    free(chi2); free(outl);
+    ba_ctx_free(&c);
+    return VIO_OK;
+}
+
+/* ========================================================================================= */
+/* Test hooks for the restated Ceres known-answer tests                                       */
+/* ========================================================================================= */
+/* Powell's singular function (trust_region_minimizer_test.cc:262-294): dense 4x4 problem */
+typedef struct { double J[16], r[4]; } powell_ctx;
+static void powell_residuals(const double* x, double* r, double* J) {
+    double x1 = x[0], x2 = x[1], x3 = x[2], x4 = x[3];
+    r[0] = x1 + 10.0 * x2;
+    r[1] = sqrt(5.0) * (x3 - x4);
+    r[2] = (x2 - 2.0 * x3) * (x2 - 2.0 * x3);
+    r[3] = sqrt(10.0) * (x1 - x4) * (x1 - x4);
+    if (J) {
+        memset(J, 0, 16 * sizeof(double));
+        J[0] = 1.0; J[1] = 10.0;
+        J[6] = sqrt(5.0); J[7] = -sqrt(5.0);
+        J[9] = 2.0 * (x2 - 2.0 * x3); J[10] = -4.0 * (x2 - 2.0 * x3);
+        J[12] = 2.0 * sqrt(10.0) * (x1 - x4); J[15] = -2.0 * sqrt(10.0) * (x1 - x4);
+    }
+}
+static int powell_eval(void* u, const double* x, double* cost, int want, double* g, double* colsq) {
+    powell_ctx* c = (powell_ctx*)u;
+    double r[4], J[16];
+    powell_residuals(x, r, J);
+    *cost = 0.5 * (r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3]);
+    if (want) {
+        memcpy(c->J, J, sizeof J);
+        memcpy(c->r, r, sizeof r);
+        for (int j = 0; j < 4; ++j) {
+            g[j] = 0; colsq[j] = 0;
+            for (int i = 0; i < 4; ++i) { g[j] += J[4 * i + j] * r[i]; colsq[j] += J[4 * i + j] * J[4 * i + j]; }
+        }
+    }
+    return 1;
+}
+static int powell_solve(void* u, const double* s, const double* D, double* y) {
+    powell_ctx* c = (powell_ctx*)u;
+    double A[16] = {0}, b[4] = {0};
+    for (int a = 0; a < 4; ++a) {
+        for (int i = 0; i < 4; ++i) b[a] += c->J[4 * i + a] * s[a] * c->r[i];
+        for (int bb = 0; bb < 4; ++bb)
+            for (int i = 0; i < 4; ++i) A[4 * a + bb] += c->J[4 * i + a] * s[a] * c->J[4 * i + bb] * s[bb];
+        A[5 * a] += D[a] * D[a];
+    }
+    if (dense_llt(4, A) != 0) return 0;
+    dense_llt_solve(4, A, b);
+    memcpy(y, b, sizeof b);
+    return 1;
+}
+static double powell_model(void* u, const double* s, const double* h) {
+    powell_ctx* c = (powell_ctx*)u;
+    double mc = 0;
+    for (int i = 0; i < 4; ++i) {
+        double m = 0;
+        for (int j = 0; j < 4; ++j) m += c->J[4 * i + j] * s[j] * h[j];
+        mc -= m * (c->r[i] + m / 2.0);
+    }
+    return mc;
+}
+/* IsTrustRegionSolveSuccessful<col1..col4> (trust_region_minimizer_test.cc:224-266) */
+typedef struct { powell_ctx base; int mask[4]; int na; } powell_masked;
+static void powell_full(const powell_masked* m, const double* xa, double* x4) {
+    static const double zero = 0.0;
+    (void)zero;
+    int q = 0;
+    for (int i = 0; i < 4; ++i) x4[i] = m->mask[i] ? xa[q++] : 0.0;
+}
+static int powellm_eval(void* u, const double* xa, double* cost, int want, double* g, double* colsq) {
+    powell_masked* m = (powell_masked*)u;
+    double x4[4], g4[4], c4[4];
+    powell_full(m, xa, x4);
+    powell_eval(&m->base, x4, cost, want, g4, c4);
+    if (want) {
+        int q = 0;
+        for (int i = 0; i < 4; ++i)
+            if (m->mask[i]) { g[q] = g4[i]; colsq[q] = c4[i]; q++; }
+    }
+    return 1;
+}
+/* DENSE_QR as in the Ceres test: Householder QR of the augmented [J~; D] (dense_qr_solver.cc) */
+static int powellm_solve(void* u, const double* s, const double* D, double* y) {
+    powell_masked* m = (powell_masked*)u;
+    int na = m->na, cols[4], q = 0;
+    for (int i = 0; i < 4; ++i)
+        if (m->mask[i]) cols[q++] = i;
+    int rows = 4 + na;
+    double A[8][4] = {{0}}, b[8] = {0};
+    for (int i = 0; i < 4; ++i) {
+        for (int j = 0; j < na; ++j) A[i][j] = m->base.J[4 * i + cols[j]] * s[j];
+        b[i] = m->base.r[i];
+    }
+    for (int j = 0; j < na; ++j) A[4 + j][j] = D[j];
+    for (int j = 0; j < na; ++j) {
+        double nrm = 0;
+        for (int i = j; i < rows; ++i) nrm += A[i][j] * A[i][j];
+        nrm = sqrt(nrm);
+        if (nrm == 0.0) return 0;
+        double alpha = A[j][j] > 0 ? -nrm : nrm;
+        double v[8] = {0};
+        for (int i = j; i < rows; ++i) v[i] = A[i][j];
+        v[j] -= alpha;
+        double vn = 0;
+        for (int i = j; i < rows; ++i) vn += v[i] * v[i];
+        if (vn == 0.0) continue;
+        for (int c = j; c < na; ++c) {
+            double d = 0;
+            for (int i = j; i < rows; ++i) d += v[i] * A[i][c];
+            d = 2.0 * d / vn;
+            for (int i = j; i < rows; ++i) A[i][c] -= d * v[i];
+        }
+        double d = 0;
+        for (int i = j; i < rows; ++i) d += v[i] * b[i];
+        d = 2.0 * d / vn;
+        for (int i = j; i < rows; ++i) b[i] -= d * v[i];
+    }
+    for (int j = na - 1; j >= 0; --j) {
+        double t = b[j];
+        for (int c = j + 1; c < na; ++c) t -= A[j][c] * y[c];
+        y[j] = t / A[j][j];
+    }
+    return 1;
+}
+static double powellm_model(void* u, const double* s, const double* h) {
+    powell_masked* m = (powell_masked*)u;
+    int cols[4], q = 0;
+    for (int i = 0; i < 4; ++i)
+        if (m->mask[i]) cols[q++] = i;
+    double mc = 0;
+    for (int i = 0; i < 4; ++i) {
+        double mm = 0;
+        for (int j = 0; j < m->na; ++j) mm += m->base.J[4 * i + cols[j]] * s[j] * h[j];
+        mc -= mm * (m->base.r[i] + mm / 2.0);
+    }
+    return mc;
+}
+/* x: 4 values in/out (inactive entries are forced to 0, the optimum) */
+int oracle_powell(const int* mask, double* x, int* iterations, double* final_cost, int* termination) {
+    powell_masked m;
+    m.na = 0;
+    for (int i = 0; i < 4; ++i) { m.mask[i] = mask[i] != 0; m.na += m.mask[i]; }
+    double xa[4];
+    int q = 0;
+    for (int i = 0; i < 4; ++i)
+        if (m.mask[i]) xa[q++] = x[i];
+    lm_problem P = {m.na, &m, powellm_eval, powellm_solve, powellm_model};
+    lm_options o;
+    oracle_lm_default_options(&o);
+    o.function_tolerance = 1e-26;
+    o.gradient_tolerance = 1e-26;
+    o.parameter_tolerance = 1e-26;
+    o.initial_radius = 1e4;
+    o.max_radius = 1e20;
+    lm_summary s;
+    oracle_lm_minimize(&P, &o, xa, &s);
+    powell_full(&m, xa, x);
+    *iterations = s.iterations;
+    *final_cost = s.final_cost;
+    *termination = s.termination;
+    return 0;
+}
+
+/* radius schedule hook: apply a sequence of accept(q>0)/reject(q<=0) events */
+void oracle_lm_radius_schedule(double initial_radius, double max_radius, const double* q, int n, double* radii) {
+    lm_radius s = {initial_radius, 2.0, max_radius};
+    for (int i = 0; i < n; ++i) {
+        if (q[i] > 0) oracle_lm_step_accepted(&s, q[i]);
+        else oracle_lm_step_rejected(&s);
+        radii[i] = s.radius;
+    }
+}
+
+/* summary trace for one solve (LM trace goldens): runs the problem and returns the trace */
+int oracle_ba_trace(const vio_ba_problem* p, double* costs, double* radii, int* ok, int cap, int* n_out) {
+    ba_ctx c;
+    ba_ctx_build(&c, p);
+    lm_options opt;
+    oracle_lm_default_options(&opt);
+    opt.max_iterations = p->max_iterations;
+    opt.fixed_iterations = p->fixed_iterations;
+    lm_summary sum;
+    ba_ceres_solve(&c, &opt, &sum);
+    int n = sum.trace_n < cap ? sum.trace_n : cap;
+    for (int i = 0; i < n; ++i) { costs[i] = sum.trace_cost[i]; radii[i] = sum.trace_radius[i]; ok[i] = sum.trace_ok[i]; }
+    *n_out = n;
+    ba_ctx_free(&c);
+    return 0;
+}

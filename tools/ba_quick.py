@@ -1,0 +1,71 @@
+"""Quick GPU-vs-oracle BA comparison (diagnostic script)."""
+import ctypes as C
+import importlib
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+vio = importlib.import_module("360_visual_inertial_odometry_amd")
+synth = importlib.import_module("360_visual_inertial_odometry_amd.synth")
+import oracle_lib  # noqa: E402
+
+orc = oracle_lib.load()
+
+
+def oracle(prob):
+    O = vio.BaOutput(prob.K, prob.L, prob.N)
+    rc = orc.oracle_ba_solve(C.byref(prob.c), C.byref(O.c))
+    assert rc == 0
+    return O.result()
+
+
+def cmp(a, b):
+    dt = np.abs(a["T_wb"][:, :3, 3] - b["T_wb"][:, :3, 3]).max()
+    dR = np.abs(a["T_wb"][:, :3, :3] - b["T_wb"][:, :3, :3]).max()
+    dl = np.abs(a["lm_xyz"] - b["lm_xyz"]).max() if len(a["lm_xyz"]) else 0
+    return dict(dt=dt, dR=dR, dl=dl, it=(a["iterations"], b["iterations"]), cost=(a["final_cost"], b["final_cost"]),
+                init=(a["initial_cost"], b["initial_cost"]), term=(a["termination"], b["termination"]),
+                out=(int(a["obs_outlier"].sum()), int(b["obs_outlier"].sum())))
+
+
+ctx = vio.Context(0)
+cases = [
+    ("cfg2-local", synth.config2(), vio.VIO_BA_LOCAL),
+    ("cfg2-full", synth.config2(), vio.VIO_BA_FULL),
+    ("cfg3-vi", synth.config3(), vio.VIO_BA_VI),
+    ("local-marg-outl", synth.make_window(K=8, L=150, seed=3, marg_frac=0.2, outlier_frac=0.05, all_visible=False), vio.VIO_BA_LOCAL),
+    ("pnp", synth.make_pnp(synth.config2(), outlier_frac=0.1, marg_frac=0.1), vio.VIO_PNP),
+]
+for name, w, var in cases:
+    p = vio.BaProblem(w, variant=var)
+    t0 = time.time(); o = oracle(p); t1 = time.time()
+    g = ctx.ba_solve([p])[0]; t2 = time.time()
+    print(name, "oracle %.3fs gpu %.3fs" % (t1 - t0, t2 - t1), cmp(o, g), flush=True)
+
+# timing: batched config 3, fixed 10 iterations
+for nwin in (1, 256):
+    probs = [vio.BaProblem(synth.config3(synth.SEED + i), variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1) for i in range(nwin)]
+    b = vio.BaBatch(ctx, probs)
+    b.run(); b.sync(); b.kernel_ms()
+    t = time.time()
+    for _ in range(5):
+        b.run()
+    b.sync()
+    el = (time.time() - t) / 5
+    ms, cnt = b.kernel_ms()
+    print(f"windows={nwin} wall/step={el*1e3:.3f} ms kernel={ms:.3f} ms -> {nwin*10/el:.1f} window-iters/s", flush=True)
+    b.profile(True)
+    b.run(); b.sync()
+    pc = b.phase_cycles()
+    tot = sum(pc.values())
+    print("  phases (cycles/window):", {k: round(v / nwin) for k, v in pc.items()}, "total", round(tot / nwin), flush=True)
+    b.profile(False)
+    if nwin == 1:
+        res = b.download()[0]
+        o = oracle(probs[0])
+        print("fixed10 parity", cmp(o, res))
