@@ -579,6 +579,13 @@ static void imu_eval(const imu_ctx* c, const double* di, const double* vi, const
 }
 
 /* exported single-factor evaluators for golden/FD tests */
+static void pose_ctx_init_(pose_ctx* pc, const vio_pose* Twb, const vio_pose* Tcb) {
+    oracle_nearest_rotation(Twb->R, pc->R_init);
+    memcpy(pc->t_init, Twb->t, sizeof pc->t_init);
+    oracle_nearest_rotation(Tcb->R, pc->R_cb);
+    memcpy(pc->t_cb, Tcb->t, sizeof pc->t_cb);
+    memcpy(pc->R_cb_raw, Tcb->R, sizeof pc->R_cb_raw);
+}
 int oracle_ba_factor(const vio_pose* T_wb_init, const vio_pose* T_cb, const double* delta, const double* Pw,
                      double u, double v, double cols, double rows, int outlier, int is_pnp, double* r,
                      double* Jp, double* Jl) {
@@ -589,6 +596,13 @@ int oracle_ba_factor(const vio_pose* T_wb_init, const vio_pose* T_cb, const doub
     memcpy(pc.t_cb, T_cb->t, sizeof pc.t_cb);
     memcpy(pc.R_cb_raw, T_cb->R, sizeof pc.R_cb_raw);
     return factor_eval(&pc, delta, Pw, u, v, cols, rows, NULL, outlier, is_pnp, r, Jp, Jl);
+}
+double oracle_ba_chi2(const vio_pose* T_wb_init, const vio_pose* T_cb, const double* delta, const double* Pw,
+                      double u, double v, double cols, double rows, int outlier, int is_pnp) {
+    pose_ctx pc;
+    pose_ctx_init_(&pc, T_wb_init, T_cb);
+    const double info[4] = {1.0, 0.0, 0.0, 1.0};
+    return factor_chi2(&pc, delta, Pw, u, v, cols, rows, info, outlier, is_pnp);
 }
 void oracle_imu_factor(const vio_preint* p, const double* g, const vio_pose* Ti, const vio_pose* Tj,
                        const double* di, const double* vi, const double* bg, const double* ba, const double* dj,

@@ -1,0 +1,79 @@
+"""CPU checks of the C-ABI boundary: libvio360.so loads, exports every entry point include/vio360.h
+declares, and the ctypes mirror (abi.py) is byte-identical to the header structs."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vio360.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*([a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_library_exports_every_header_symbol(vio):
+    lib = C.CDLL(vio.LIB_PATH)
+    names = header_functions()
+    assert len(names) >= 20, names
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # the Python wrapper's export list is the header's
+    assert set(vio.EXPORTS) <= set(names)
+
+
+def test_abi_version(vio):
+    assert vio.lib().vio_abi_version() == 1
+
+
+STRUCTS = {
+    "vio_pose": ("VioPose", ["R", "t"]),
+    "vio_preint": ("VioPreint", ["delta_R", "delta_V", "delta_P", "J_Rg", "cov9", "gyro_bias", "accel_bias", "dt_total"]),
+    "vio_ba_problem": ("VioBaProblem", ["variant", "num_kf", "cols", "info", "chi2_threshold", "T_cb", "T_wb_init",
+                                        "kf_const", "lm_xyz", "obs_uv", "preint", "vel", "bg", "gravity",
+                                        "max_iterations", "fixed_iterations", "num_rounds"]),
+    "vio_ba_summary": ("VioBaSummary", ["success", "num_bad_lm", "initial_cost", "fixed_cost"]),
+    "vio_ba_output": ("VioBaOutput", ["T_wb", "lm_xyz", "obs_outlier", "summary"]),
+    "erp_klt_params": ("ErpKltParams", ["win", "max_level", "epsilon", "min_eig_threshold"]),
+    "erp_tracker_params": ("ErpTrackerParams", ["n_pts", "ransac_thresh_rad", "quality", "min_dist",
+                                                "boundary_margin", "polar_ratio"]),
+}
+
+
+def test_struct_layout_matches_header(vio, tmp_path):
+    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
+    for cs, (_, fields) in STRUCTS.items():
+        lines.append(f'printf("{cs} sizeof %zu\\n", sizeof({cs}));')
+        for f in fields:
+            lines.append(f'printf("{cs} {f} %zu\\n", offsetof({cs}, {f}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-o", str(exe), str(src)])
+    out = subprocess.check_output([str(exe)]).decode().split("\n")
+    got = {}
+    for ln in out:
+        if ln:
+            s, f, v = ln.split()
+            got[(s, f)] = int(v)
+    for cs, (py, fields) in STRUCTS.items():
+        cls = getattr(vio.abi, py)
+        assert C.sizeof(cls) == got[(cs, "sizeof")], cs
+        for f in fields:
+            assert getattr(cls, f).offset == got[(cs, f)], (cs, f)
+
+
+def test_no_device_fails_loudly(vio):
+    """Without a GPU the product path must raise (there is no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(vio.VioError):
+        vio.Context(0)

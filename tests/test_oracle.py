@@ -1,0 +1,188 @@
+"""CPU tests of the oracle (oracle/ba_oracle.c): pinned by the Ceres known-answer tests the
+reference ships (thirdparty/ceres-solver/internal/ceres/*_test.cc, restated here because they
+cannot be compiled without Eigen) and by the independent numpy golden vectors in tests/golden/."""
+import ctypes as C
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+dp = C.POINTER(C.c_double)
+
+
+def _d(a):
+    a = np.ascontiguousarray(a, np.float64)
+    return a, a.ctypes.data_as(dp)
+
+
+def test_lm_radius_schedule_kat():
+    """levenberg_marquardt_strategy_test.cc:81-111 (AcceptRejectStepRadiusScaling)."""
+    L = oracle_lib.load()
+    q = np.array([0.0, -1.0, 1.0, 1.0, 0.25, 1.0, 1.0, 1.0])
+    radii = np.zeros(len(q))
+    L.oracle_lm_radius_schedule(C.c_double(2.0), C.c_double(20.0), _d(q)[1], len(q), radii.ctypes.data_as(dp))
+    exp = [1.0, 0.25, 0.25 * 3, 0.25 * 9, 0.25 * 9 / 1.125, 0.25 * 9 / 1.125 * 3, 0.25 * 9 / 1.125 * 9, 20.0]
+    assert radii.tolist() == exp  # EXPECT_EQ: exact
+
+
+def test_lm_diagonal_kat():
+    """levenberg_marquardt_strategy_test.cc:113-166: D = sqrt(clamp(diag)/radius)."""
+    L = oracle_lib.load()
+    L.oracle_lm_diagonal.argtypes = [C.c_int, dp, dp, C.c_double, C.c_double, C.c_double, dp]
+    # J = [[0,1,100],[0,1,0]] -> diag(J^T J) = [0, 2, 10000], no scaling
+    colsq, s, D = np.array([0.0, 2.0, 1e4]), np.ones(3), np.zeros(3)
+    L.oracle_lm_diagonal(3, _d(colsq)[1], _d(s)[1], 2.0, 1e-2, 1e2, D.ctypes.data_as(dp))
+    assert np.allclose(D, np.sqrt(np.array([1e-2, 2.0, 1e2]) / 2.0), rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("delta", [0.7, 1.3])
+@pytest.mark.parametrize("s", [0.357, 1.792])
+def test_huber_kat(delta, s):
+    """loss_function_test.cc:92-103 (AssertLossFunctionIsValid for HuberLoss)."""
+    L = oracle_lib.load()
+    L.oracle_huber.argtypes = [C.c_double, C.c_double, dp]
+
+    def ev(x):
+        r = np.zeros(3)
+        L.oracle_huber(delta, x, r.ctypes.data_as(dp))
+        return r
+
+    rho, fwd, bwd, h = ev(s), ev(s + 1e-4), ev(s - 1e-4), 1e-4
+    assert abs((fwd[0] - bwd[0]) / (2 * h) - rho[1]) < 1e-6
+    assert abs((fwd[0] - 2 * rho[0] + bwd[0]) / (h * h) - rho[2]) < 1e-6
+    assert np.allclose(ev(0.0), [0, 1, 0], atol=1e-6)
+
+
+def test_corrector_scalar_kat():
+    """corrector_test.cc:57-83: rho''<0 -> alpha = 0, scale sqrt(rho')."""
+    L = oracle_lib.load()
+    L.oracle_corrector.argtypes = [C.c_double, dp, dp, dp, dp]
+    r, j = math.sqrt(3.0), 10.0
+    rho = np.array([3.0, 0.1, -0.01])
+    rs, asq, sr1 = C.c_double(), C.c_double(), C.c_double()
+    L.oracle_corrector(3.0, rho.ctypes.data_as(dp), C.byref(rs), C.byref(asq), C.byref(sr1))
+    assert abs(r * rs.value - r * math.sqrt(0.1)) < 1e-6
+    assert asq.value == 0.0 and abs(sr1.value * j - math.sqrt(0.1) * j) < 1e-6
+
+
+MASKS = [(1, 1, 1, 1), (1, 1, 1, 0), (1, 0, 1, 1), (0, 1, 1, 1), (1, 1, 0, 0), (1, 0, 1, 0), (0, 1, 1, 0),
+         (1, 0, 0, 1), (0, 1, 0, 1), (0, 0, 1, 1), (1, 0, 0, 0), (0, 1, 0, 0), (0, 0, 1, 0), (0, 0, 0, 1)]
+
+
+@pytest.mark.parametrize("mask", MASKS)
+def test_powell_lm_kat(mask):
+    """trust_region_minimizer_test.cc:224-294: LM on Powell's singular function reaches 0 +- 1e-3
+    from (3,-1,0,1) for the 14 column masks the Ceres test runs."""
+    L = oracle_lib.load()
+    m = (C.c_int * 4)(*mask)
+    x = np.array([3.0, -1.0, 0.0, 1.0]) * np.array(mask)
+    it, fc, term = C.c_int(), C.c_double(), C.c_int()
+    L.oracle_powell(m, x.ctypes.data_as(dp), C.byref(it), C.byref(fc), C.byref(term))
+    assert np.all(np.abs(x) < 1e-3), (mask, x)
+
+
+def test_nearest_rotation_matches_svd():
+    """oracle_nearest_rotation == SO3d(Matrix3d) SVD projection (LieUtils.cpp:275-288)."""
+    L = oracle_lib.load()
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        A = rng.normal(size=(3, 3))
+        if rng.random() < 0.5:  # near-orthonormal (f32-rounded rotation) like every input pose
+            q, _ = np.linalg.qr(A)
+            A = (q * np.sign(np.linalg.det(q))).astype(np.float32).astype(np.float64)
+        U, _, Vt = np.linalg.svd(A)
+        R = U @ Vt
+        if np.linalg.det(R) < 0:
+            U[:, 2] *= -1
+            R = U @ Vt
+        out = np.zeros(9)
+        L.oracle_nearest_rotation(_d(A.reshape(-1))[1], out.ctypes.data_as(dp))
+        assert np.abs(out.reshape(3, 3) - R).max() < 1e-12
+
+
+def _pose(vio, T):
+    return vio.abi.poses_to_c(T[None])
+
+
+def test_factor_golden(vio):
+    """C oracle BAFactor/PnPFactor vs the independent numpy golden vectors (rel 1e-12)."""
+    L = oracle_lib.load()
+    g = np.load(os.path.join(GOLDEN, "factor_golden.npz"))
+    Tcb = _pose(vio, g["T_cb"])
+    L.oracle_ba_chi2.restype = C.c_double
+    n = len(g["ok"])
+    branches = set()
+    for i in range(n):
+        T = _pose(vio, g["T"][i])
+        r, Jp, Jl = np.zeros(2), np.zeros(12), np.zeros(6)
+        delta, Pw = _d(g["delta"][i]), _d(g["Pw"][i])
+        ok = L.oracle_ba_factor(T, Tcb, delta[1], Pw[1], C.c_double(g["obs"][i][0]), C.c_double(g["obs"][i][1]),
+                                C.c_double(float(g["cols"])), C.c_double(float(g["rows"])), int(g["outlier"][i]),
+                                int(g["is_pnp"][i]), r.ctypes.data_as(dp), Jp.ctypes.data_as(dp), Jl.ctypes.data_as(dp))
+        assert bool(ok) == bool(g["ok"][i])
+        if not ok:
+            branches.add("pnp-fail")
+            continue
+        scale = 1.0 + np.abs(g["r"][i]).max()
+        # x^2+z^2 < 1e-10 (landmark ~above the camera): atan2 of ~1e-6 m components amplifies the
+        # 1e-16 rounding of Pc to ~1e-8 px, so that branch is compared at 1e-5 px
+        degenerate = not np.any(g["Jp"][i]) and tuple(g["r"][i]) not in ((640.0, 480.0), (640.0, 360.0), (100.0, 100.0))
+        tol = 1e-5 if degenerate else 1e-10 * scale
+        assert np.abs(r - g["r"][i]).max() <= tol, (i, r, g["r"][i])
+        js = 1.0 + np.abs(g["Jp"][i]).max()
+        assert np.abs(Jp - g["Jp"][i].reshape(-1)).max() <= 1e-11 * js, i
+        assert np.abs(Jl - g["Jl"][i].reshape(-1)).max() <= 1e-11 * js, i
+        c2 = L.oracle_ba_chi2(T, Tcb, delta[1], Pw[1], C.c_double(g["obs"][i][0]), C.c_double(g["obs"][i][1]),
+                              C.c_double(float(g["cols"])), C.c_double(float(g["rows"])), int(g["outlier"][i]),
+                              int(g["is_pnp"][i]))
+        ref = g["chi2"][i]
+        assert abs(c2 - ref) <= (1e-3 if degenerate else 1e-9) * (1 + abs(ref)), (i, c2, ref)
+        if tuple(g["r"][i]) in ((640.0, 480.0), (640.0, 360.0), (100.0, 100.0)):
+            branches.add(tuple(g["r"][i]))
+        elif not np.any(g["Jp"][i]):
+            branches.add("jzero")
+    # every special branch of Factors.cpp:331-476 is exercised
+    assert {(640.0, 480.0), (640.0, 360.0), (100.0, 100.0), "jzero", "pnp-fail"} <= branches
+
+
+def test_factor_jacobian_finite_difference(vio):
+    """J_point is the true derivative; J_pose is the right-perturbation derivative at delta = 0
+    (Factors.cpp:500-534) — check both by central differences."""
+    L = oracle_lib.load()
+    g = np.load(os.path.join(GOLDEN, "factor_golden.npz"))
+    Tcb = _pose(vio, g["T_cb"])
+    checked = 0
+    for i in range(len(g["ok"])):
+        if g["outlier"][i] or g["is_pnp"][i] or not np.any(g["Jp"][i]):
+            continue
+        T = _pose(vio, g["T"][i])
+        obs = g["obs"][i]
+
+        def res(delta, Pw):
+            r = np.zeros(2)
+            L.oracle_ba_factor(T, Tcb, _d(delta)[1], _d(Pw)[1], C.c_double(obs[0]), C.c_double(obs[1]),
+                               C.c_double(960.0), C.c_double(480.0), 0, 0, r.ctypes.data_as(dp), None, None)
+            return r
+
+        d0, P0 = np.zeros(6), g["Pw"][i]
+        Jp, Jl, r0 = np.zeros(12), np.zeros(6), np.zeros(2)
+        L.oracle_ba_factor(T, Tcb, _d(d0)[1], _d(P0)[1], C.c_double(obs[0]), C.c_double(obs[1]), C.c_double(960.0),
+                           C.c_double(480.0), 0, 0, r0.ctypes.data_as(dp), Jp.ctypes.data_as(dp),
+                           Jl.ctypes.data_as(dp))
+        if np.abs(r0).max() > 90:
+            continue
+        h = 1e-6
+        for j in range(6):
+            e = np.zeros(6); e[j] = h
+            fd = (res(d0 + e, P0) - res(d0 - e, P0)) / (2 * h)
+            assert np.allclose(fd, Jp.reshape(2, 6)[:, j], rtol=1e-4, atol=1e-3), (i, j)
+        for j in range(3):
+            e = np.zeros(3); e[j] = h
+            fd = (res(d0, P0 + e) - res(d0, P0 - e)) / (2 * h)
+            assert np.allclose(fd, Jl.reshape(2, 3)[:, j], rtol=1e-4, atol=1e-3), (i, j)
+        checked += 1
+    assert checked >= 20
