@@ -11,7 +11,7 @@ import numpy as np
 
 from . import abi
 from .abi import (VIO_BA_FULL, VIO_BA_LOCAL, VIO_BA_VI, VIO_PNP, BaOutput, BaProblem,  # noqa: F401
-                  default_klt_params)
+                  ErpKltParams, ErpTrackerParams, default_klt_params, default_tracker_params)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VIO360_LIB") or os.path.join(_HERE, "libvio360.so")
@@ -22,9 +22,10 @@ EXPORTS = [
     "vio_ba_solve", "vio_ba_solve_batched", "vio_ba_batch_create", "vio_ba_batch_run",
     "vio_ba_batch_sync", "vio_ba_batch_download", "vio_ba_batch_kernel_ms", "vio_ba_batch_destroy",
     "vio_ba_batch_profile", "vio_ba_batch_phase_cycles",
-    "erp_klt_track", "erp_gftt", "erp_rot_ransac", "erp_tracker_create", "erp_tracker_upload",
-    "erp_tracker_set_points", "erp_tracker_run", "erp_tracker_sync", "erp_tracker_download",
-    "erp_tracker_kernel_ms", "erp_tracker_destroy",
+    "erp_klt_track", "erp_gftt", "erp_rot_ransac", "erp_ransac_samples", "erp_tracker_create",
+    "erp_tracker_upload", "erp_tracker_device_frame", "erp_tracker_swap", "erp_tracker_set_points",
+    "erp_tracker_run", "erp_tracker_sync", "erp_tracker_download", "erp_tracker_stage_ms",
+    "erp_tracker_destroy",
 ]
 
 
@@ -53,6 +54,24 @@ def lib():
     L.vio_ba_batch_destroy.argtypes = [C.c_void_p]
     L.vio_ba_batch_profile.argtypes = [C.c_void_p, C.c_int]
     L.vio_ba_batch_phase_cycles.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+    vp = C.c_void_p
+    L.erp_klt_track.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, vp, vp,
+                                C.POINTER(abi.ErpKltParams)]
+    L.erp_gftt.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, vp,
+                           C.POINTER(C.c_int)]
+    L.erp_rot_ransac.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_float, vp,
+                                 C.POINTER(C.c_int)]
+    L.erp_ransac_samples.argtypes = [C.c_uint32, C.c_int, C.c_int, vp]
+    L.erp_tracker_create.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.erp_tracker_upload.argtypes = [vp, C.c_int, vp, C.c_int]
+    L.erp_tracker_device_frame.argtypes = [vp, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int)]
+    L.erp_tracker_swap.argtypes = [vp]
+    L.erp_tracker_set_points.argtypes = [vp, vp, C.c_int]
+    L.erp_tracker_run.argtypes = [vp, C.POINTER(abi.ErpKltParams), C.POINTER(abi.ErpTrackerParams)]
+    L.erp_tracker_sync.argtypes = [vp]
+    L.erp_tracker_download.argtypes = [vp, vp, vp, vp, vp, C.POINTER(C.c_int)]
+    L.erp_tracker_stage_ms.argtypes = [vp] + [C.POINTER(C.c_double)] * 5
+    L.erp_tracker_destroy.argtypes = [vp]
     _lib = L
     return L
 
@@ -92,6 +111,129 @@ class Context:
         O = (abi.VioBaOutput * n)(*[o.c for o in outs])
         self.check(lib().vio_ba_solve_batched(self.h, P, O, n), "vio_ba_solve_batched")
         return [o.result() for o in outs]
+
+
+    # ---- ERP feature tracking ----
+    def klt_track(self, prev, curr, pts, params=None):
+        """cv::calcOpticalFlowPyrLK as FeatureTracker::TrackOpticalFlow calls it -> (next, status, err)."""
+        prev, curr = _u8img(prev), _u8img(curr)
+        H, W = prev.shape
+        pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+        n = len(pts)
+        nxt = np.zeros((n, 2), np.float32)
+        st = np.zeros(n, np.uint8)
+        err = np.zeros(n, np.float32)
+        prm = params or default_klt_params()
+        self.check(lib().erp_klt_track(self.h, _p(prev), _p(curr), W, H, W, _p(pts), n, _p(nxt), _p(st), _p(err),
+                                       C.byref(prm)), "erp_klt_track")
+        return nxt, st, err
+
+    def gftt(self, img, mask=None, max_corners=1000, quality=0.01, min_dist=30.0):
+        """cv::goodFeaturesToTrack(blockSize 3, useHarris false) -> (k, 2) float32 corners."""
+        img = _u8img(img)
+        H, W = img.shape
+        m = None if mask is None else _u8img(mask)
+        cap = max_corners if max_corners > 0 else W * H
+        out = np.zeros((cap, 2), np.float32)
+        n = C.c_int()
+        self.check(lib().erp_gftt(self.h, _p(img), _p(m) if m is not None else None, W, H, W, int(max_corners),
+                                  float(quality), float(min_dist), _p(out), C.byref(n)), "erp_gftt")
+        return out[: n.value].copy()
+
+    def rot_ransac(self, p0, p1, W, H, samples, thresh_rad=None):
+        """RejectOutliersRotationRANSAC on an injected sample stream -> (mask u8, n_inliers)."""
+        p0 = np.ascontiguousarray(p0, np.float32).reshape(-1, 2)
+        p1 = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+        samples = np.ascontiguousarray(samples, np.int32).reshape(-1)
+        n = len(p0)
+        thr = ransac_threshold() if thresh_rad is None else thresh_rad
+        mask = np.zeros(n, np.uint8)
+        nin = C.c_int()
+        self.check(lib().erp_rot_ransac(self.h, _p(p0), _p(p1), n, W, H, _p(samples), len(samples) // 3,
+                                        float(thr), _p(mask), C.byref(nin)), "erp_rot_ransac")
+        return mask, nin.value
+
+
+def _u8img(a):
+    return np.ascontiguousarray(a, np.uint8)
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def ransac_threshold(deg=2.0):
+    """threshold_rad = m_ransac_threshold * M_PI / 180.0f (FeatureTracker.cpp:305), as float."""
+    return float(np.float32(np.float64(np.float32(deg)) * np.pi / np.float64(np.float32(180.0))))
+
+
+def ransac_samples(seed, n, iters=1000):
+    """The reference's mt19937 + uniform_int_distribution sample stream with an injected seed."""
+    out = np.zeros(3 * iters, np.int32)
+    rc = lib().erp_ransac_samples(int(seed) & 0xffffffff, int(n), int(iters), _p(out))
+    if rc != 0:
+        raise VioError(f"erp_ransac_samples failed ({rc})")
+    return out
+
+
+class Tracker:
+    """Device-resident frame pipeline (erp_tracker_*): pyramids + LK + RANSAC + GFTT re-detection."""
+
+    def __init__(self, ctx, W, H, max_points=2048, max_corners=2048):
+        self.ctx, self.W, self.H = ctx, W, H
+        self.max_points, self.max_corners = max_points, max_corners
+        h = C.c_void_p()
+        ctx.check(lib().erp_tracker_create(ctx.h, W, H, max_points, max_corners, C.byref(h)), "erp_tracker_create")
+        self.h = h
+        self.n = 0
+
+    def upload(self, slot, img):
+        img = _u8img(img)
+        self.ctx.check(lib().erp_tracker_upload(self.h, slot, _p(img), img.shape[1]), "erp_tracker_upload")
+
+    def swap(self):
+        self.ctx.check(lib().erp_tracker_swap(self.h), "erp_tracker_swap")
+
+    def set_points(self, pts):
+        pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+        self.n = len(pts)
+        self._pts = pts
+        self.ctx.check(lib().erp_tracker_set_points(self.h, _p(pts), self.n), "erp_tracker_set_points")
+
+    def run(self, params=None, klt=None):
+        prm = params or default_tracker_params()
+        kp = klt or default_klt_params()
+        self.ctx.check(lib().erp_tracker_run(self.h, C.byref(kp), C.byref(prm)), "erp_tracker_run")
+
+    def sync(self):
+        self.ctx.check(lib().erp_tracker_sync(self.h), "erp_tracker_sync")
+
+    def download(self):
+        n = self.n
+        nxt = np.zeros((max(n, 1), 2), np.float32)
+        st = np.zeros(max(n, 1), np.uint8)
+        kept = np.zeros(max(n, 1), np.uint8)
+        cor = np.zeros((self.max_corners, 2), np.float32)
+        nc = C.c_int()
+        self.ctx.check(lib().erp_tracker_download(self.h, _p(nxt), _p(st), _p(kept), _p(cor), C.byref(nc)),
+                       "erp_tracker_download")
+        return {"next": nxt[:n], "status": st[:n], "kept": kept[:n], "corners": cor[: nc.value].copy()}
+
+    def stage_ms(self):
+        v = [C.c_double() for _ in range(5)]
+        self.ctx.check(lib().erp_tracker_stage_ms(self.h, *[C.byref(x) for x in v]), "erp_tracker_stage_ms")
+        return dict(zip(["pyramids", "lk", "ransac", "gftt", "total"], [x.value for x in v]))
+
+    def close(self):
+        if self.h:
+            lib().erp_tracker_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class BaBatch:

@@ -69,7 +69,7 @@ class ErpKltParams(C.Structure):
 
 
 class ErpTrackerParams(C.Structure):
-    _fields_ = [("n_pts", C.c_int32), ("ransac_iters", C.c_int32), ("ransac_thresh_rad", C.c_float),
+    _fields_ = [("ransac_iters", C.c_int32), ("ransac_thresh_rad", C.c_float), ("ransac_seed", C.c_uint32),
                 ("max_corners", C.c_int32), ("quality", C.c_double), ("min_dist", C.c_double),
                 ("boundary_margin", C.c_int32), ("polar_ratio", C.c_float)]
 
@@ -77,6 +77,13 @@ class ErpTrackerParams(C.Structure):
 def default_klt_params():
     """FeatureTracker's hard-coded LK settings (src/processing/FeatureTracker.cpp:33-35,240)."""
     return ErpKltParams(21, 3, 30, 0.01, 0.01, 0)
+
+
+def default_tracker_params(max_corners=300, seed=0):
+    """FeatureTracker's settings (src/processing/FeatureTracker.cpp:36-38, config feature_detection.*;
+    quality_level is a float member, so 0.01f reaches OpenCV as a double)."""
+    thr = float(np.float32(np.float64(np.float32(2.0)) * np.pi / np.float64(np.float32(180.0))))
+    return ErpTrackerParams(1000, thr, seed, max_corners, float(np.float32(0.01)), 30.0, 20, 0.15)
 
 
 def _ptr(a, ctype):

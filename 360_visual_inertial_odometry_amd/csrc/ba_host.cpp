@@ -34,7 +34,7 @@ void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes) {
         ctx->caps.resize(slot + 1, 0);
     }
     if (ctx->caps[slot] >= bytes && ctx->bufs[slot]) return ctx->bufs[slot];
-    if (ctx->bufs[slot]) hipFree(ctx->bufs[slot]);
+    if (ctx->bufs[slot]) (void)hipFree(ctx->bufs[slot]);
     ctx->bufs[slot] = nullptr;
     ctx->caps[slot] = 0;
     size_t cap = std::max<size_t>(bytes, 256);
@@ -287,12 +287,12 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
 }
 
 static void free_batch(BaDevice& d) {
-    for (void* p : d.allocs) hipFree(p);
+    for (void* p : d.allocs) (void)hipFree(p);
     d.allocs.clear();
-    if (d.prof_buf) hipFree(d.prof_buf);
+    if (d.prof_buf) (void)hipFree(d.prof_buf);
     d.prof_buf = nullptr;
-    if (d.ev0) hipEventDestroy(d.ev0);
-    if (d.ev1) hipEventDestroy(d.ev1);
+    if (d.ev0) (void)hipEventDestroy(d.ev0);
+    if (d.ev1) (void)hipEventDestroy(d.ev1);
     d.ev0 = d.ev1 = nullptr;
 }
 
@@ -407,10 +407,10 @@ int vio_ctx_create(int device, vio_ctx** out) {
 
 void vio_ctx_destroy(vio_ctx* ctx) {
     if (!ctx) return;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     for (void* p : ctx->bufs)
-        if (p) hipFree(p);
-    if (ctx->stream) hipStreamDestroy(ctx->stream);
+        if (p) (void)hipFree(p);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
@@ -421,7 +421,7 @@ const char* vio_ctx_last_error(const vio_ctx* ctx) {
 int vio_ba_batch_create(vio_ctx* ctx, const vio_ba_problem* probs, int n, vio_ba_batch** out) {
     if (!ctx || !probs || n <= 0 || !out) return VIO_EINVAL;
     *out = nullptr;
-    hipSetDevice(ctx->device);
+    (void)hipSetDevice(ctx->device);
     vio_ba_batch* b = new vio_ba_batch();
     b->ctx = ctx;
     b->dev.n = n;
@@ -502,8 +502,8 @@ int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out16) {
 
 void vio_ba_batch_destroy(vio_ba_batch* b) {
     if (!b) return;
-    hipSetDevice(b->ctx->device);
-    hipStreamSynchronize(b->ctx->stream);
+    (void)hipSetDevice(b->ctx->device);
+    (void)hipStreamSynchronize(b->ctx->stream);
     free_batch(b->dev);
     delete b;
 }

@@ -1,0 +1,874 @@
+// tracker.hip — ERP feature tracking on MI355X (gfx950): the numeric path of
+// FeatureTracker::TrackFeatures (src/processing/FeatureTracker.cpp:61-379).
+//
+//   pyr_down_kernel      cv::pyrDown inside buildOpticalFlowPyramid: 5x5 [1 4 6 4 1]^2/256,
+//                        BORDER_REFLECT_101; both frames of a pair in one launch (blockIdx.z).
+//   lk_kernel            cv::calcOpticalFlowPyrLK's LKTrackerInvoker, one wavefront per point,
+//                        all pyramid levels in one launch; the Scharr derivatives of the previous
+//                        frame are computed on the fly from an LDS-staged 24x24 tile (never
+//                        materialised for the whole image), the 21x21 patch, its derivatives and
+//                        every 22x22 next-frame tile live in LDS; gradient/mismatch sums are exact
+//                        int64 wave reductions.
+//   ransac_*             RejectOutliersRotationRANSAC: one wavefront per hypothesis.
+//   gftt_*               cv::goodFeaturesToTrack(blockSize 3, Sobel 3): the min-eigenvalue map is
+//                        never written to HBM — pass 1 reduces its masked maximum, pass 2
+//                        recomputes it on a haloed LDS tile, applies THRESH_TOZERO + 3x3 dilate
+//                        NMS + mask and appends (response, address) keys; a radix sort and one
+//                        workgroup's greedy min-distance pass finish.
+// Float expressions follow tracker_oracle.c literally and the file is built with
+// -ffp-contract=off, so results are bitwise those of the oracle.
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "tracker_types.h"
+
+namespace vio360 {
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+    return p;
+}
+
+// ------------------------------------------------------------------------------------------
+// pyrDown.  Block = 64x4 outputs; LDS tile of (2*64+4) x (2*4+4) source pixels.
+constexpr int PD_BX = 64, PD_BY = 4;
+constexpr int PD_TW = 2 * PD_BX + 4, PD_TH = 2 * PD_BY + 4;
+
+__global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLevelPair dst) {
+    __shared__ uint8_t tile[PD_TH][PD_TW + 4];
+    const int f = blockIdx.z;
+    const uint8_t* s = f == 0 ? src.p0 : src.p1;
+    uint8_t* d = f == 0 ? dst.p0 : dst.p1;
+    const int sw = src.w, sh = src.h, sp = src.pitch;
+    const int dw = dst.w, dh = dst.h, dp = dst.pitch;
+    const int ox = blockIdx.x * PD_BX, oy = blockIdx.y * PD_BY;
+    const int sx0 = 2 * ox - 2, sy0 = 2 * oy - 2;
+    for (int e = threadIdx.x; e < PD_TW * PD_TH; e += 256) {
+        int ty = e / PD_TW, tx = e % PD_TW;
+        tile[ty][tx] = s[(size_t)reflect101(sy0 + ty, sh) * sp + reflect101(sx0 + tx, sw)];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x % PD_BX, ty = threadIdx.x / PD_BX;
+    const int x = ox + tx, y = oy + ty;
+    if (x >= dw || y >= dh) return;
+    int tot = 0;
+#pragma unroll
+    for (int ky = 0; ky < 5; ++ky) {
+        const uint8_t* r = &tile[2 * ty + ky][2 * tx];
+        int rs = r[0] + 4 * r[1] + 6 * r[2] + 4 * r[3] + r[4];
+        tot += (ky == 0 || ky == 4 ? 1 : (ky == 2 ? 6 : 4)) * rs;
+    }
+    d[(size_t)y * dp + x] = (uint8_t)((tot + 128) >> 8);
+}
+
+// ------------------------------------------------------------------------------------------
+// LK.  One wavefront per point.
+constexpr int LK_WAVES = 4;
+constexpr int LK_WIN_MAX = 21;
+constexpr int LK_T = LK_WIN_MAX + 3;  // prev tile (patch + 1 bilinear + 1 Scharr each side)
+constexpr int LK_D = LK_WIN_MAX + 1;  // derivative / next tile
+
+struct LkShared {
+    uint8_t It[LK_T * LK_T];
+    int16_t dx[LK_D * LK_D], dy[LK_D * LK_D];
+    int16_t Iw[LK_WIN_MAX * LK_WIN_MAX];
+    int16_t dIx[LK_WIN_MAX * LK_WIN_MAX], dIy[LK_WIN_MAX * LK_WIN_MAX];
+    uint8_t Jt[LK_D * LK_D];
+};
+
+__device__ __forceinline__ long long wave_sum_i64(long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+#define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
+
+__device__ __forceinline__ void lk_weights(float a, float b, int& w00, int& w01, int& w10, int& w11) {
+    w00 = (int)rintf((1.f - a) * (1.f - b) * 16384.f);
+    w01 = (int)rintf(a * (1.f - b) * 16384.f);
+    w10 = (int)rintf((1.f - a) * b * 16384.f);
+    w11 = 16384 - w00 - w01 - w10;
+}
+
+// load the (win+1)x(win+1) next-frame tile at (ix, iy) with the REFLECT_101 pad semantics
+__device__ __forceinline__ void lk_load_J(uint8_t* Jt, const uint8_t* J, int w, int h, int pitch, int ix, int iy,
+                                          int win, int lane) {
+    const int n = (win + 1) * (win + 1);
+    for (int e = lane; e < n; e += 64) {
+        int ty = e / (win + 1), tx = e % (win + 1);
+        Jt[e] = J[(size_t)reflect101(iy + ty, h) * pitch + reflect101(ix + tx, w)];
+    }
+}
+
+// Σ |diff| or the b-vector over the window for the current J tile
+__global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
+    __shared__ LkShared shm[LK_WAVES];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int pt = blockIdx.x * LK_WAVES + wid;
+    if (pt >= A.n) return;  // whole wave exits together (wave-uniform)
+    LkShared& S = shm[wid];
+    const int win = A.win;
+    const float hw = (win - 1) * 0.5f;
+    const float FLT_SCALE = 1.f / (1 << 20);
+    const int np = win * win;
+    float prev_x = A.pts[2 * pt], prev_y = A.pts[2 * pt + 1];
+    float nxt_x = 0.f, nxt_y = 0.f;
+    int status = 1;
+    float err = 0.f;
+    for (int level = A.levels; level >= 0; --level) {
+        const LkLevel& Lv = A.lv[level];
+        const int w = Lv.w, h = Lv.h;
+        const uint8_t* I = Lv.prev;
+        const uint8_t* J = Lv.curr;
+        const float sc = (float)(1. / (1 << level));
+        float px = prev_x * sc, py = prev_y * sc;
+        float nx, ny;
+        if (level == A.levels) { nx = px; ny = py; }
+        else { nx = nxt_x * 2.f; ny = nxt_y * 2.f; }
+        nxt_x = nx; nxt_y = ny;
+        px -= hw; py -= hw;
+        const int ipx = (int)floorf(px), ipy = (int)floorf(py);
+        if (ipx < -win || ipx >= w || ipy < -win || ipy >= h) {
+            if (level == 0) { status = 0; err = 0.f; }
+            continue;
+        }
+        // stage the prev tile: rows ipy-1 .. ipy+win+1, cols ipx-1 .. ipx+win+1
+        const int T = win + 3;
+        for (int e = lane; e < T * T; e += 64) {
+            int ty = e / T, tx = e % T;
+            S.It[e] = I[(size_t)reflect101(ipy - 1 + ty, h) * Lv.pitch + reflect101(ipx - 1 + tx, w)];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // Scharr derivatives at (ipx+tx, ipy+ty), tx,ty in [0, win]; zero outside the image
+        const int D = win + 1;
+        for (int e = lane; e < D * D; e += 64) {
+            int ty = e / D, tx = e % D;
+            int X = ipx + tx, Y = ipy + ty;
+            int gx = 0, gy = 0;
+            if (X >= 0 && Y >= 0 && X < w && Y < h) {
+                const uint8_t* r0 = &S.It[ty * T + tx];      // (X-1, Y-1)
+                const uint8_t* r1 = r0 + T;
+                const uint8_t* r2 = r1 + T;
+                int t0m = (r0[0] + r2[0]) * 3 + r1[0] * 10, t0p = (r0[2] + r2[2]) * 3 + r1[2] * 10;
+                int t1m = r2[0] - r0[0], t1c = r2[1] - r0[1], t1p = r2[2] - r0[2];
+                gx = (int16_t)(t0p - t0m);
+                gy = (int16_t)((t1p + t1m) * 3 + t1c * 10);
+            }
+            S.dx[e] = (int16_t)gx;
+            S.dy[e] = (int16_t)gy;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        float a = px - ipx, b = py - ipy;
+        int w00, w01, w10, w11;
+        lk_weights(a, b, w00, w01, w10, w11);
+        long long sA11 = 0, sA12 = 0, sA22 = 0;
+        for (int e = lane; e < np; e += 64) {
+            int y = e / win, x = e % win;
+            const uint8_t* t = &S.It[(y + 1) * T + x + 1];
+            int ival = DESCALE(t[0] * w00 + t[1] * w01 + t[T] * w10 + t[T + 1] * w11, 9);
+            int q = y * D + x;
+            int ixv = DESCALE(S.dx[q] * w00 + S.dx[q + 1] * w01 + S.dx[q + D] * w10 + S.dx[q + D + 1] * w11, 14);
+            int iyv = DESCALE(S.dy[q] * w00 + S.dy[q + 1] * w01 + S.dy[q + D] * w10 + S.dy[q + D + 1] * w11, 14);
+            S.Iw[e] = (int16_t)ival;
+            S.dIx[e] = (int16_t)ixv;
+            S.dIy[e] = (int16_t)iyv;
+            sA11 += (long long)ixv * ixv;
+            sA12 += (long long)ixv * iyv;
+            sA22 += (long long)iyv * iyv;
+        }
+        sA11 = wave_sum_i64(sA11);
+        sA12 = wave_sum_i64(sA12);
+        sA22 = wave_sum_i64(sA22);
+        const float A11 = (float)sA11 * FLT_SCALE, A12 = (float)sA12 * FLT_SCALE, A22 = (float)sA22 * FLT_SCALE;
+        float Dt = A11 * A22 - A12 * A12;
+        const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
+        if (minEig < A.min_eig || Dt < FLT_EPSILON) {
+            if (level == 0) status = 0;
+            continue;
+        }
+        Dt = 1.f / Dt;
+        nx -= hw; ny -= hw;
+        float pdx = 0.f, pdy = 0.f;
+        for (int j = 0; j < A.max_iters; ++j) {
+            const int inx = (int)floorf(nx), iny = (int)floorf(ny);
+            if (inx < -win || inx >= w || iny < -win || iny >= h) {
+                if (level == 0) status = 0;
+                break;
+            }
+            a = nx - inx; b = ny - iny;
+            lk_weights(a, b, w00, w01, w10, w11);
+            __builtin_amdgcn_wave_barrier();
+            lk_load_J(S.Jt, J, w, h, Lv.pitch, inx, iny, win, lane);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            long long ib1 = 0, ib2 = 0;
+            for (int e = lane; e < np; e += 64) {
+                int y = e / win, x = e % win;
+                const uint8_t* t = &S.Jt[y * D + x];
+                int diff = DESCALE(t[0] * w00 + t[1] * w01 + t[D] * w10 + t[D + 1] * w11, 9) - S.Iw[e];
+                ib1 += (long long)diff * S.dIx[e];
+                ib2 += (long long)diff * S.dIy[e];
+            }
+            ib1 = wave_sum_i64(ib1);
+            ib2 = wave_sum_i64(ib2);
+            const float b1 = (float)ib1 * FLT_SCALE, b2 = (float)ib2 * FLT_SCALE;
+            const float ddx = (A12 * b2 - A22 * b1) * Dt;
+            const float ddy = (A12 * b1 - A11 * b2) * Dt;
+            nx += ddx; ny += ddy;
+            nxt_x = nx + hw; nxt_y = ny + hw;
+            if ((double)ddx * ddx + (double)ddy * ddy <= A.eps2) break;
+            if (j > 0 && fabs((double)(ddx + pdx)) < 0.01 && fabs((double)(ddy + pdy)) < 0.01) {
+                nxt_x -= ddx * 0.5f;
+                nxt_y -= ddy * 0.5f;
+                break;
+            }
+            pdx = ddx; pdy = ddy;
+        }
+        if (status && level == 0) {
+            const float fx = nxt_x - hw, fy = nxt_y - hw;
+            const int ix = (int)floorf(fx), iy = (int)floorf(fy);
+            if (ix < -win || ix >= w || iy < -win || iy >= h) {
+                status = 0;
+            } else {
+                lk_weights(fx - ix, fy - iy, w00, w01, w10, w11);
+                __builtin_amdgcn_wave_barrier();
+                lk_load_J(S.Jt, J, w, h, Lv.pitch, ix, iy, win, lane);
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                long long es = 0;
+                for (int e = lane; e < np; e += 64) {
+                    int y = e / win, x = e % win;
+                    const uint8_t* t = &S.Jt[y * D + x];
+                    int diff = DESCALE(t[0] * w00 + t[1] * w01 + t[D] * w10 + t[D + 1] * w11, 9) - S.Iw[e];
+                    es += diff < 0 ? -diff : diff;
+                }
+                es = wave_sum_i64(es);
+                err = (float)es * (1.f / (32 * win * win));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) {
+        A.next[2 * pt] = nxt_x;
+        A.next[2 * pt + 1] = nxt_y;
+        A.status[pt] = (uint8_t)status;
+        A.err[pt] = err;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// bearings / filter / RANSAC
+__device__ void pixel_to_bearing(float u, float v, int W, int H, float* b) {
+    float un = u / (float)W, vn = v / (float)H;
+    float lon = (float)((double)((un - 0.5f) * 2.0f) * M_PI);
+    float lat = (float)((double)(-(vn - 0.5f)) * M_PI);
+    float cl = (float)cos((double)lat), sl = (float)sin((double)lat);
+    float so = (float)sin((double)lon), co = (float)cos((double)lon);
+    float x = cl * so, y = -sl, z = cl * co;
+    float sq = (x * x + y * y) + z * z;
+    if (sq > 0.f) {
+        float nr = sqrtf(sq);
+        x /= nr; y /= nr; z /= nr;
+    }
+    b[0] = x; b[1] = y; b[2] = z;
+}
+
+// order-preserving compaction of the RANSAC input (single workgroup of 1024 threads):
+//   mode 0: all n points (erp_rot_ransac); mode 1: status ∧ !polar ∧ !boundary (pipeline)
+__global__ void __launch_bounds__(1024) ransac_prep_kernel(RansacArgs R) {
+    __shared__ int wsum[16];
+    __shared__ int base;
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    const int n = R.n;
+    for (int c0 = 0; c0 < n; c0 += 1024) {
+        int i = c0 + threadIdx.x;
+        int good = 0;
+        if (i < n) {
+            if (R.mode == 0) good = 1;
+            else {
+                float x = R.p1[2 * i], y = R.p1[2 * i + 1];
+                float vr = y / (float)R.H;
+                bool polar = (vr < R.polar_ratio) || (vr > (1.0f - R.polar_ratio));
+                float m = (float)R.margin;
+                bool nearb = (x < m) || (x > (float)R.W - m) || (y < m) || (y > (float)R.H - m);
+                good = R.status[i] && !polar && !nearb;
+            }
+            R.kept[i] = 0;
+        }
+        unsigned long long bal = __ballot(good);
+        int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        int pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wid] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int k = 0; k < wid; ++k) off += wsum[k];
+        if (good) {
+            int j = off + pre;
+            R.gidx[j] = i;
+            pixel_to_bearing(R.p0[2 * i], R.p0[2 * i + 1], R.W, R.H, R.b0 + 3 * j);
+            pixel_to_bearing(R.p1[2 * i], R.p1[2 * i + 1], R.W, R.H, R.b1 + 3 * j);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int k = 0; k < 16; ++k) t += wsum[k];
+            base += t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *R.n_good = base;
+}
+
+// mt19937 + libstdc++-11 uniform_int_distribution (Lemire) — the reference's sampler
+// (FeatureTracker.cpp:273-288) with an injected seed; one thread (the stream is sequential).
+struct Mt19937 {
+    uint32_t mt[624];
+    int idx;
+    __device__ void seed(uint32_t s) {
+        mt[0] = s;
+        for (int i = 1; i < 624; ++i) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+        idx = 624;
+    }
+    __device__ uint32_t next() {
+        if (idx >= 624) {
+            for (int i = 0; i < 624; ++i) {
+                uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
+                mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            }
+            idx = 0;
+        }
+        uint32_t y = mt[idx++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        return y;
+    }
+};
+__device__ uint32_t uniform_below(Mt19937& g, uint32_t range) {  // uniform in [0, range)
+    uint64_t prod = (uint64_t)g.next() * range;
+    uint32_t low = (uint32_t)prod;
+    if (low < range) {
+        uint32_t thr = (uint32_t)(-range) % range;
+        while (low < thr) {
+            prod = (uint64_t)g.next() * range;
+            low = (uint32_t)prod;
+        }
+    }
+    return (uint32_t)(prod >> 32);
+}
+
+__global__ void __launch_bounds__(64) ransac_sample_kernel(RansacArgs R) {
+    __shared__ Mt19937 g;
+    if (threadIdx.x != 0) return;
+    const int n = *R.n_good;
+    if (n < 3) return;
+    g.seed(R.seed);
+    for (int it = 0; it < R.iters; ++it) {
+        int got[3];
+        int k = 0;
+        while (k < 3) {
+            int idx = (int)uniform_below(g, (uint32_t)n);
+            bool dup = false;
+            for (int q = 0; q < k; ++q) dup |= got[q] == idx;
+            if (!dup) got[k++] = idx;
+        }
+        R.samples[3 * it] = got[0];
+        R.samples[3 * it + 1] = got[1];
+        R.samples[3 * it + 2] = got[2];
+    }
+}
+
+__device__ void jacobi3(double* A, double* V) {
+    for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 12; ++sweep) {
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                double apq = A[3 * p + q];
+                if (apq == 0.0) continue;
+                double app = A[3 * p + p], aqq = A[3 * q + q];
+                double theta = (aqq - app) / (2.0 * apq);
+                double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 3; ++k) {
+                    double akp = A[3 * k + p], akq = A[3 * k + q];
+                    A[3 * k + p] = c * akp - s * akq;
+                    A[3 * k + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    double apk = A[3 * p + k], aqk = A[3 * q + k];
+                    A[3 * p + k] = c * apk - s * aqk;
+                    A[3 * q + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    double vkp = V[3 * k + p], vkq = V[3 * k + q];
+                    V[3 * k + p] = c * vkp - s * vkq;
+                    V[3 * k + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+}
+
+// EstimateRotation (FeatureTracker.cpp:330-355): nearest proper rotation of H (see oracle)
+__device__ void kabsch_rotation(const float* Hf, float* Rf) {
+    double H[9], HtH[9], V[9];
+    for (int i = 0; i < 9; ++i) H[i] = Hf[i];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) HtH[3 * i + j] = H[i] * H[j] + H[3 + i] * H[3 + j] + H[6 + i] * H[6 + j];
+    jacobi3(HtH, V);
+    double w[3] = {HtH[0], HtH[4], HtH[8]};
+    int idx[3] = {0, 1, 2};
+    for (int i = 0; i < 3; ++i)
+        for (int j = i + 1; j < 3; ++j)
+            if (w[idx[j]] > w[idx[i]]) { int t = idx[i]; idx[i] = idx[j]; idx[j] = t; }
+    double v[3][3], u[3][3];
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) v[c][r] = V[3 * r + idx[c]];
+    for (int c = 0; c < 2; ++c) {
+        for (int r = 0; r < 3; ++r) u[c][r] = H[3 * r] * v[c][0] + H[3 * r + 1] * v[c][1] + H[3 * r + 2] * v[c][2];
+        double nn = sqrt(u[c][0] * u[c][0] + u[c][1] * u[c][1] + u[c][2] * u[c][2]);
+        if (nn > 0) { u[c][0] /= nn; u[c][1] /= nn; u[c][2] /= nn; }
+    }
+    double d01 = u[0][0] * u[1][0] + u[0][1] * u[1][1] + u[0][2] * u[1][2];
+    for (int r = 0; r < 3; ++r) u[1][r] -= d01 * u[0][r];
+    double n1 = sqrt(u[1][0] * u[1][0] + u[1][1] * u[1][1] + u[1][2] * u[1][2]);
+    if (n1 > 0) { u[1][0] /= n1; u[1][1] /= n1; u[1][2] /= n1; }
+    u[2][0] = u[0][1] * u[1][2] - u[0][2] * u[1][1];
+    u[2][1] = u[0][2] * u[1][0] - u[0][0] * u[1][2];
+    u[2][2] = u[0][0] * u[1][1] - u[0][1] * u[1][0];
+    double dV = v[0][0] * (v[1][1] * v[2][2] - v[1][2] * v[2][1]) - v[1][0] * (v[0][1] * v[2][2] - v[0][2] * v[2][1]) +
+                v[2][0] * (v[0][1] * v[1][2] - v[0][2] * v[1][1]);
+    double d = dV < 0 ? -1.0 : 1.0;
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) Rf[3 * r + c] = (float)(u[0][r] * v[0][c] + u[1][r] * v[1][c] + d * u[2][r] * v[2][c]);
+}
+
+__device__ __forceinline__ float det3f(const float* m) {
+    return m[0] * (m[4] * m[8] - m[7] * m[5]) - m[3] * (m[1] * m[8] - m[7] * m[2]) + m[6] * (m[1] * m[5] - m[4] * m[2]);
+}
+
+__device__ __forceinline__ bool rot_inlier(const float* R, const float* a, const float* q, float thr) {
+    float r0 = (R[0] * a[0] + R[1] * a[1]) + R[2] * a[2];
+    float r1 = (R[3] * a[0] + R[4] * a[1]) + R[5] * a[2];
+    float r2 = (R[6] * a[0] + R[7] * a[1]) + R[8] * a[2];
+    float c = (r0 * q[0] + r1 * q[1]) + r2 * q[2];
+    c = c < -1.f ? -1.f : (c > 1.f ? 1.f : c);
+    return (float)acos((double)c) < thr;
+}
+
+// one wavefront per hypothesis: count[it] = inliers, or -1 when |det R - 1| > 0.1 (skipped)
+__global__ void __launch_bounds__(256) ransac_hyp_kernel(RansacArgs R) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int it = blockIdx.x * 4 + wid;
+    if (it >= R.iters) return;
+    const int n = *R.n_good;
+    if (n < 3) return;
+    float Hm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < 3; ++s) {
+        int k = R.samples[3 * it + s];
+        const float* q = R.b1 + 3 * k;
+        const float* a = R.b0 + 3 * k;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) Hm[3 * r + c] += q[r] * a[c];
+    }
+    float Rm[9];
+    kabsch_rotation(Hm, Rm);
+    if (fabsf(det3f(Rm) - 1.0f) > 0.1f) {
+        if (lane == 0) R.count[it] = -1;
+        return;
+    }
+    int cnt = 0;
+    for (int i = lane; i < n; i += 64) cnt += rot_inlier(Rm, R.b0 + 3 * i, R.b1 + 3 * i, R.thresh) ? 1 : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (lane == 0) R.count[it] = cnt;
+}
+
+// first strictly-best hypothesis -> mask over the good points, scattered to the input order
+__global__ void __launch_bounds__(256) ransac_select_kernel(RansacArgs R) {
+    __shared__ int sbest[256], sidx[256];
+    __shared__ float Rs[9];
+    const int n = *R.n_good;
+    int best = 0, bi = -1;
+    if (n >= 3)
+        for (int it = threadIdx.x; it < R.iters; it += 256) {
+            int c = R.count[it];
+            if (c > best) { best = c; bi = it; }  // strictly greater keeps the earliest of this thread
+        }
+    sbest[threadIdx.x] = best;
+    sidx[threadIdx.x] = bi;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            int b2 = sbest[threadIdx.x + s], i2 = sidx[threadIdx.x + s];
+            if (b2 > sbest[threadIdx.x] || (b2 == sbest[threadIdx.x] && b2 > 0 && i2 < sidx[threadIdx.x])) {
+                sbest[threadIdx.x] = b2;
+                sidx[threadIdx.x] = i2;
+            }
+        }
+        __syncthreads();
+    }
+    const int bit = sidx[0];
+    if (threadIdx.x == 0) {
+        *R.n_in = n < 3 ? n : sbest[0];
+        if (bit >= 0) {
+            float Hm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            for (int s = 0; s < 3; ++s) {
+                int k = R.samples[3 * bit + s];
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) Hm[3 * r + c] += R.b1[3 * k + r] * R.b0[3 * k + c];
+            }
+            kabsch_rotation(Hm, Rs);
+        }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += 256) {
+        uint8_t m = 1;
+        if (n >= 3 && bit >= 0) m = rot_inlier(Rs, R.b0 + 3 * j, R.b1 + 3 * j, R.thresh) ? 1 : 0;
+        R.kept[R.gidx[j]] = m;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// GFTT.  Tile = 64 x 8 outputs.  Source tile with a halo of H_ (2 for the eig map, 3 when the
+// 3x3 NMS needs eig at a 1-pixel halo).
+constexpr int GF_BX = 64, GF_BY = 8;
+
+template <int HALO>
+struct GfTile {
+    static constexpr int EW = GF_BX + 2 * (HALO - 2), EH = GF_BY + 2 * (HALO - 2);  // eig positions
+    static constexpr int SW = EW + 4, SH = EH + 4;                                   // source pixels
+    static constexpr int CW = EW + 2, CH = EH + 2;                                   // cov positions
+};
+
+__device__ __forceinline__ bool gf_masked_in(const GfArgs& G, int x, int y) {
+    if (G.mask) return G.mask[(size_t)y * G.mask_pitch + x] != 0;
+    if (y < G.top_rows || y >= G.bottom_start || x < G.margin || x >= G.W - G.margin) return false;
+    if (G.disc_bits) {
+        uint32_t wbits = G.disc_bits[(size_t)y * G.disc_words + (x >> 5)];
+        if ((wbits >> (x & 31)) & 1u) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ uint32_t ord_f32(float v) {
+    uint32_t u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// compute eig for the EW x EH positions starting at (ex0, ey0) into eig[] (LDS)
+template <int HALO>
+__device__ void gf_eig_tile(const GfArgs& G, int ex0, int ey0, uint8_t (*src)[GfTile<HALO>::SW + 4],
+                            float (*cov)[GfTile<HALO>::CW][3], float (*eig)[GfTile<HALO>::EW]) {
+    using T = GfTile<HALO>;
+    const int W = G.W, H = G.H;
+    const int sx0 = ex0 - 2, sy0 = ey0 - 2;
+    for (int e = threadIdx.x; e < T::SW * T::SH; e += 256) {
+        int ty = e / T::SW, tx = e % T::SW;
+        src[ty][tx] = G.img[(size_t)reflect101(sy0 + ty, H) * G.pitch + reflect101(sx0 + tx, W)];
+    }
+    __syncthreads();
+    const float scale = (float)(1.0 / 3060.0);
+    // cov at positions (ex0-1+cx, ey0-1+cy): Sobel of reflect101 neighbours.  The tile holds
+    // source rows/cols sy0.. with reflect applied per coordinate, so for a cov position p the
+    // neighbours p±1 must be reflected relative to the image, not the tile: re-derive them.
+    for (int e = threadIdx.x; e < T::CW * T::CH; e += 256) {
+        int cy = e / T::CW, cx = e % T::CW;
+        int X = reflect101(ex0 - 1 + cx, W), Y = reflect101(ey0 - 1 + cy, H);
+        // tile coordinates of X-1, X, X+1 (reflected about the image) — map back into the tile
+        int xm = reflect101(X - 1, W) - sx0, xc = X - sx0, xp = reflect101(X + 1, W) - sx0;
+        int ym = reflect101(Y - 1, H) - sy0, yc = Y - sy0, yp = reflect101(Y + 1, H) - sy0;
+        int sx, sy;
+        if (xm >= 0 && xp < T::SW && ym >= 0 && yp < T::SH && xc >= 0 && xc < T::SW && yc >= 0 && yc < T::SH) {
+            const uint8_t* r0 = src[ym];
+            const uint8_t* r1 = src[yc];
+            const uint8_t* r2 = src[yp];
+            sx = (r0[xp] - r0[xm]) + 2 * (r1[xp] - r1[xm]) + (r2[xp] - r2[xm]);
+            sy = (r2[xm] + 2 * r2[xc] + r2[xp]) - (r0[xm] + 2 * r0[xc] + r0[xp]);
+        } else {  // tile edge folded by a reflection: read the image directly
+            const uint8_t* r0 = G.img + (size_t)reflect101(Y - 1, H) * G.pitch;
+            const uint8_t* r1 = G.img + (size_t)Y * G.pitch;
+            const uint8_t* r2 = G.img + (size_t)reflect101(Y + 1, H) * G.pitch;
+            int gxm = reflect101(X - 1, W), gxp = reflect101(X + 1, W);
+            sx = (r0[gxp] - r0[gxm]) + 2 * (r1[gxp] - r1[gxm]) + (r2[gxp] - r2[gxm]);
+            sy = (r2[gxm] + 2 * r2[X] + r2[gxp]) - (r0[gxm] + 2 * r0[X] + r0[gxp]);
+        }
+        float dx = (float)sx * scale, dy = (float)sy * scale;
+        cov[cy][cx][0] = dx * dx;
+        cov[cy][cx][1] = dx * dy;
+        cov[cy][cx][2] = dy * dy;
+    }
+    __syncthreads();
+    // 3x3 box (reflect101 about the image) + min eigenvalue
+    for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
+        int ey = e / T::EW, ex = e % T::EW;
+        int X = ex0 + ex, Y = ey0 + ey;
+        if (X < 0 || Y < 0 || X >= W || Y >= H) {  // outside the image: never read (dilate ignores it)
+            eig[ey][ex] = 0.f;
+            continue;
+        }
+        double s0 = 0, s1 = 0, s2 = 0;
+        if (X >= 1 && X < W - 1 && Y >= 1 && Y < H - 1) {
+            for (int ky = 0; ky < 3; ++ky)
+                for (int kx = 0; kx < 3; ++kx) {
+                    const float* c = cov[ey + ky][ex + kx];
+                    s0 += c[0]; s1 += c[1]; s2 += c[2];
+                }
+        } else {
+            // border pixel: neighbours reflect about the image; cov positions of (X+k) live at
+            // tile index reflect101(X+k) - (ex0-1), valid for every in-image X of this tile
+            for (int ky = -1; ky <= 1; ++ky) {
+                int yy = reflect101(Y + ky, H) - (ey0 - 1);
+                for (int kx = -1; kx <= 1; ++kx) {
+                    int xx = reflect101(X + kx, W) - (ex0 - 1);
+                    const float* c = cov[yy][xx];
+                    s0 += c[0]; s1 += c[1]; s2 += c[2];
+                }
+            }
+        }
+        float a = (float)s0 * 0.5f, b = (float)s1, c = (float)s2 * 0.5f;
+        eig[ey][ex] = (a + c) - sqrtf((a - c) * (a - c) + b * b);
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) gftt_max_kernel(GfArgs G) {
+    using T = GfTile<2>;
+    __shared__ uint8_t src[T::SH][T::SW + 4];
+    __shared__ float cov[T::CH][T::CW][3];
+    __shared__ float eig[T::EH][T::EW];
+    __shared__ uint32_t red[4];
+    const int ex0 = blockIdx.x * GF_BX, ey0 = blockIdx.y * GF_BY;
+    gf_eig_tile<2>(G, ex0, ey0, src, cov, eig);
+    uint32_t m = 0;  // ord(-inf-ish): any value beats 0
+    for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
+        int ey = e / T::EW, ex = e % T::EW;
+        int X = ex0 + ex, Y = ey0 + ey;
+        if (X < G.W && Y < G.H && gf_masked_in(G, X, Y)) m = max(m, ord_f32(eig[ey][ex]));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (t) atomicMax(G.max_ord, t);
+    }
+}
+
+__global__ void __launch_bounds__(256) gftt_cand_kernel(GfArgs G) {
+    using T = GfTile<3>;
+    __shared__ uint8_t src[T::SH][T::SW + 4];
+    __shared__ float cov[T::CH][T::CW][3];
+    __shared__ float eig[T::EH][T::EW];
+    const int ox = blockIdx.x * GF_BX, oy = blockIdx.y * GF_BY;
+    gf_eig_tile<3>(G, ox - 1, oy - 1, src, cov, eig);
+    // threshold (THRESH_TOZERO with the float threshold) in place
+    const uint32_t mo = *G.max_ord;
+    double maxv = mo ? (double)unord_f32(mo) : 0.0;  // minMaxLoc over the mask, 0 when empty
+    if (maxv < 0.0) maxv = 0.0;
+    const float thr = (float)(maxv * G.quality);
+    for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
+        int ey = e / T::EW, ex = e % T::EW;
+        if (!(eig[ey][ex] > thr)) eig[ey][ex] = 0.f;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < GF_BX * GF_BY; e += 256) {
+        int ty = e / GF_BX, tx = e % GF_BX;
+        int X = ox + tx, Y = oy + ty;
+        bool c = false;
+        float v = 0.f;
+        if (X >= 1 && X < G.W - 1 && Y >= 1 && Y < G.H - 1) {
+            v = eig[ty + 1][tx + 1];
+            if (v != 0.f && gf_masked_in(G, X, Y)) {
+                float m = v;
+                for (int ky = 0; ky < 3; ++ky)
+                    for (int kx = 0; kx < 3; ++kx) m = fmaxf(m, eig[ty + ky][tx + kx]);
+                c = (v == m);
+            }
+        }
+        unsigned long long bal = __ballot(c);
+        int lane = threadIdx.x & 63;
+        int cnt = __popcll(bal);
+        unsigned int base = 0;
+        if (cnt) {
+            if (lane == __ffsll((long long)bal) - 1) base = atomicAdd(G.n_cand, (unsigned int)cnt);
+            base = __shfl(base, __ffsll((long long)bal) - 1, 64);
+        }
+        if (c) {
+            unsigned int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+            if (pos < G.cand_cap)
+                G.cand[pos] = ((unsigned long long)__float_as_uint(v) << 32) | (unsigned int)(Y * G.W + X);
+        }
+    }
+}
+
+// greedy min-distance selection over the sorted candidates (goodFeaturesToTrack tail).
+// One workgroup.  Accepted corners live in a grid of cell = round(min_dist) with <= 3 per cell.
+constexpr int GS_THREADS = 256;
+constexpr int GS_SLOTS = 3;
+__global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G) {
+    extern __shared__ uint32_t grid_lds[];
+    __shared__ int s_good[GS_THREADS];
+    __shared__ int s_acc;
+    __shared__ int s_stop;
+    uint32_t* grid = G.grid_global ? G.grid_global : grid_lds;
+    const int ncell = G.gw * G.gh;
+    for (int e = threadIdx.x; e < ncell * GS_SLOTS; e += GS_THREADS) grid[e] = 0xffffffffu;
+    if (threadIdx.x == 0) { s_acc = 0; s_stop = 0; }
+    __syncthreads();
+    const unsigned int total = min(*G.n_cand, G.cand_cap);
+    const int cell = G.cell;
+    const double md2 = G.min_dist * G.min_dist;
+    auto conflicts = [&](int x, int y, int slot_lane_only) -> bool {
+        int xc = x / cell, yc = y / cell;
+        int x1 = max(xc - 1, 0), y1 = max(yc - 1, 0), x2 = min(xc + 1, G.gw - 1), y2 = min(yc + 1, G.gh - 1);
+        for (int yy = y1; yy <= y2; ++yy)
+            for (int xx = x1; xx <= x2; ++xx)
+                for (int s = 0; s < GS_SLOTS; ++s) {
+                    uint32_t p = grid[(yy * G.gw + xx) * GS_SLOTS + s];
+                    if (p == 0xffffffffu) break;
+                    float ddx = (float)x - (float)(p & 0xffffu), ddy = (float)y - (float)(p >> 16);
+                    if ((double)(ddx * ddx + ddy * ddy) < md2) return true;
+                }
+        return false;
+    };
+    for (unsigned int c0 = 0; c0 < total; c0 += GS_THREADS) {
+        // (1) parallel pre-filter against the corners accepted in earlier batches
+        unsigned int ci = c0 + threadIdx.x;
+        int good = 0;
+        if (ci < total) {
+            unsigned int idx = (unsigned int)(G.cand_sorted[ci] & 0xffffffffu);
+            good = !conflicts((int)(idx % G.W), (int)(idx / G.W), 0);
+        }
+        s_good[threadIdx.x] = good;
+        __syncthreads();
+        // (2) in-order resolution inside the batch by wave 0 (lane k checks grid slot k)
+        if (threadIdx.x < 64) {
+            const int lane = threadIdx.x;
+            const int nb = min((unsigned int)GS_THREADS, total - c0);
+            for (int j = 0; j < nb; ++j) {
+                if (!s_good[j]) continue;
+                unsigned int idx = (unsigned int)(G.cand_sorted[c0 + j] & 0xffffffffu);
+                int x = (int)(idx % G.W), y = (int)(idx / G.W);
+                int xc = x / cell, yc = y / cell;
+                // 9 cells x 3 slots = 27 lanes
+                bool conf = false;
+                if (lane < 27) {
+                    int cc = lane / GS_SLOTS, s = lane % GS_SLOTS;
+                    int xx = xc - 1 + cc % 3, yy = yc - 1 + cc / 3;
+                    if (xx >= 0 && yy >= 0 && xx < G.gw && yy < G.gh) {
+                        uint32_t p = grid[(yy * G.gw + xx) * GS_SLOTS + s];
+                        if (p != 0xffffffffu) {
+                            float ddx = (float)x - (float)(p & 0xffffu), ddy = (float)y - (float)(p >> 16);
+                            conf = (double)(ddx * ddx + ddy * ddy) < md2;
+                        }
+                    }
+                }
+                if (__ballot(conf) != 0ull) continue;
+                if (lane == 0) {
+                    int k = s_acc;
+                    uint32_t* cellp = &grid[(yc * G.gw + xc) * GS_SLOTS];
+                    int s = 0;
+                    while (s < GS_SLOTS - 1 && cellp[s] != 0xffffffffu) ++s;
+                    cellp[s] = ((uint32_t)y << 16) | (uint32_t)x;
+                    G.corners[2 * k] = (float)x;
+                    G.corners[2 * k + 1] = (float)y;
+                    s_acc = k + 1;
+                    if (G.max_corners > 0 && k + 1 == G.max_corners) s_stop = 1;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                if (s_stop) break;
+            }
+        }
+        __syncthreads();
+        if (s_stop) break;
+    }
+    if (threadIdx.x == 0) *G.n_out = s_acc;
+}
+
+// rasterise the discs of CreateFeatureMask (cv::circle filled, LINE_8; half-widths precomputed
+// on the host from OpenCV's midpoint Circle()) into a 1-bit-per-pixel exclusion mask
+__global__ void __launch_bounds__(128) disc_mask_kernel(DiscArgs D) {
+    const int k = blockIdx.x;
+    if (k >= *D.n_pts_dev) return;
+    if (D.kept && !D.kept[D.src_index ? D.src_index[k] : k]) return;
+    const int i = D.src_index ? D.src_index[k] : k;
+    const float fx = D.pts[2 * i], fy = D.pts[2 * i + 1];
+    const int cx = (int)rintf(fx), cy = (int)rintf(fy);  // Point2f -> Point (cvRound)
+    const int r = D.radius;
+    for (int dy = -r + (int)threadIdx.x; dy <= r; dy += 128) {
+        int y = cy + dy;
+        if (y < 0 || y >= D.H) continue;
+        int hwd = D.halfw[dy < 0 ? -dy : dy];
+        int x0 = max(cx - hwd, 0), x1 = min(cx + hwd, D.W - 1);
+        for (int x = x0; x <= x1;) {
+            int wi = x >> 5;
+            int b0 = x & 31;
+            int b1 = min(31, x1 - (wi << 5));
+            uint32_t m = (b1 - b0 == 31) ? 0xffffffffu : (((1u << (b1 - b0 + 1)) - 1u) << b0);
+            atomicOr(&D.bits[(size_t)y * D.words + wi], m);
+            x = (wi + 1) << 5;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers
+hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int frames, hipStream_t st) {
+    dim3 g((d.w + PD_BX - 1) / PD_BX, (d.h + PD_BY - 1) / PD_BY, frames);
+    hipLaunchKernelGGL(pyr_down_kernel, g, dim3(256), 0, st, s, d);
+    return hipGetLastError();
+}
+hipError_t launch_lk(const LkArgs& a, hipStream_t st) {
+    if (a.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lk_kernel, dim3((a.n + LK_WAVES - 1) / LK_WAVES), dim3(64 * LK_WAVES), 0, st, a);
+    return hipGetLastError();
+}
+hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st) {
+    hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(1024), 0, st, r);
+    if (gen_samples) hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(64), 0, st, r);
+    if (r.iters > 0) hipLaunchKernelGGL(ransac_hyp_kernel, dim3((r.iters + 3) / 4), dim3(256), 0, st, r);
+    hipLaunchKernelGGL(ransac_select_kernel, dim3(1), dim3(256), 0, st, r);
+    return hipGetLastError();
+}
+hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st) {
+    if (max_pts <= 0) return hipSuccess;
+    hipLaunchKernelGGL(disc_mask_kernel, dim3(max_pts), dim3(128), 0, st, d);
+    return hipGetLastError();
+}
+hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {
+    dim3 blk(256);
+    dim3 grd((g.W + GF_BX - 1) / GF_BX, (g.H + GF_BY - 1) / GF_BY);
+    hipLaunchKernelGGL(gftt_max_kernel, grd, blk, 0, st, g);
+    hipLaunchKernelGGL(gftt_cand_kernel, grd, blk, 0, st, g);
+    // sort all cand_cap slots (unused slots hold 0 and sort to the end)
+    size_t tb = sort_tmp_bytes;
+    hipError_t e = hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.cand, g.cand_sorted, (int)g.cand_cap,
+                                                               0, 64, st);
+    if (e != hipSuccess) return e;
+    size_t lds = g.grid_global ? 0 : (size_t)g.gw * g.gh * GS_SLOTS * sizeof(uint32_t);
+    hipLaunchKernelGGL(gftt_select_kernel, dim3(1), dim3(GS_THREADS), lds, st, g);
+    return hipGetLastError();
+}
+size_t gftt_sort_tmp_bytes(unsigned int cap) {
+    size_t tb = 0;
+    hipcub::DeviceRadixSort::SortKeysDescending((void*)nullptr, tb, (unsigned long long*)nullptr,
+                                                (unsigned long long*)nullptr, (int)cap, 0, 64, (hipStream_t)0);
+    return tb;
+}
+hipError_t gftt_select_set_lds(size_t bytes) {
+    return hipFuncSetAttribute((const void*)gftt_select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+}  // namespace vio360

@@ -1,0 +1,538 @@
+// tracker_host.cpp — C-ABI of the ERP feature tracker (erp_*), host side.
+//
+// Owns the device state of a tracker (frame pyramids, point / RANSAC / GFTT buffers) and enqueues
+// the tracker.hip kernels on the context stream.  The standalone entry points erp_klt_track /
+// erp_gftt / erp_rot_ransac mirror the three OpenCV / Eigen calls of FeatureTracker
+// (src/processing/FeatureTracker.cpp:222-223, 238-240, 253-379); erp_tracker_run chains them for a
+// frame pair without a host round trip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "ctx.h"
+#include "tracker_types.h"
+
+using namespace vio360;
+
+namespace {
+
+constexpr int kMaxIters = 1 << 16;
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// OpenCV imgproc/drawing.cpp Circle(..., fill=1): union of the midpoint-algorithm spans, as the
+// half-width of the filled disc on every row offset 0..r
+std::vector<int> circle_half_widths(int r) {
+    std::vector<int> hw(r + 1, -1);
+    int err = 0, dx = r, dy = 0, plus = 1, minus = (r << 1) - 1;
+    while (dx >= dy) {
+        hw[dy] = std::max(hw[dy], dx);  // rows cy±dy: [cx-dx, cx+dx]
+        if (dx <= r) hw[dx] = std::max(hw[dx], dy);  // rows cy±dx: [cx-dy, cx+dy]
+        dy++;
+        err += plus;
+        plus += 2;
+        int mask = (err <= 0) - 1;
+        err -= minus & mask;
+        dx += mask;
+        minus -= mask & 2;
+    }
+    return hw;
+}
+
+}  // namespace
+
+struct erp_tracker {
+    vio_ctx* ctx = nullptr;
+    int W = 0, H = 0, max_points = 0, max_corners = 0;
+    int nlev = 0;                        // levels allocated (maxLevel + 1 upper bound)
+    int lw[TRK_MAX_LEVELS], lh[TRK_MAX_LEVELS], lp[TRK_MAX_LEVELS];
+    uint8_t* lvl[2][TRK_MAX_LEVELS] = {};
+    // points
+    float *d_pts = nullptr, *d_next = nullptr, *d_err = nullptr, *d_b0 = nullptr, *d_b1 = nullptr;
+    uint8_t *d_status = nullptr, *d_kept = nullptr;
+    int *d_gidx = nullptr, *d_count = nullptr;
+    int32_t* d_samples = nullptr;
+    int iters_cap = 0;
+    int n_pts = 0;
+    // scalars: [0] n_good [1] n_in [2] max_ord [3] n_cand [4] n_out [5] n_pts
+    int* d_scal = nullptr;
+    // gftt
+    unsigned long long *d_cand = nullptr, *d_cand_sorted = nullptr;
+    unsigned int cand_cap = 0;
+    void* d_sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    uint32_t* d_grid = nullptr;
+    size_t grid_bytes = 0;
+    float* d_corners = nullptr;
+    uint32_t* d_disc = nullptr;
+    int disc_words = 0;
+    int* d_halfw = nullptr;
+    int halfw_r = -1;
+    uint8_t* d_mask = nullptr;  // explicit mask (erp_gftt)
+    hipEvent_t ev[6] = {};
+    bool ran = false;
+    std::vector<void*> allocs;
+};
+
+namespace {
+
+template <class T>
+int dalloc(erp_tracker* t, T** p, size_t bytes) {
+    void* q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(bytes, 64)) != hipSuccess) {
+        set_error(t->ctx, "hipMalloc failed in the tracker");
+        return VIO_ENOMEM;
+    }
+    t->allocs.push_back(q);
+    *p = (T*)q;
+    return VIO_OK;
+}
+
+void tracker_free(erp_tracker* t) {
+    for (void* p : t->allocs) (void)hipFree(p);
+    t->allocs.clear();
+    for (auto& e : t->ev)
+        if (e) (void)hipEventDestroy(e);
+}
+
+int ensure_iters(erp_tracker* t, int iters) {
+    if (iters <= t->iters_cap) return VIO_OK;
+    if (iters > kMaxIters) { set_error(t->ctx, "ransac_iters too large"); return VIO_EINVAL; }
+    int cap = std::max(iters, 1024);
+    int rc;
+    if ((rc = dalloc(t, &t->d_samples, sizeof(int32_t) * 3 * cap)) != VIO_OK) return rc;
+    if ((rc = dalloc(t, &t->d_count, sizeof(int) * cap)) != VIO_OK) return rc;
+    t->iters_cap = cap;
+    return VIO_OK;
+}
+
+int ensure_gftt(erp_tracker* t, double min_dist) {
+    int rc;
+    if (!t->d_cand) {
+        // NMS leaves at most one candidate per 2x2 block except on exact plateaus; W*H/4 (+slack)
+        t->cand_cap = (unsigned int)std::min<size_t>((size_t)t->W * t->H / 4 + 4096, (size_t)1 << 26);
+        if ((rc = dalloc(t, &t->d_cand, sizeof(unsigned long long) * t->cand_cap)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_cand_sorted, sizeof(unsigned long long) * t->cand_cap)) != VIO_OK) return rc;
+        t->sort_tmp_bytes = gftt_sort_tmp_bytes(t->cand_cap);
+        if ((rc = dalloc(t, (char**)&t->d_sort_tmp, t->sort_tmp_bytes)) != VIO_OK) return rc;
+    }
+    if (min_dist >= 1) {
+        int cell = (int)std::lrint(min_dist);
+        int gw = (t->W + cell - 1) / cell, gh = (t->H + cell - 1) / cell;
+        size_t bytes = (size_t)gw * gh * 3 * sizeof(uint32_t);
+        if (bytes > 96 * 1024 && bytes > t->grid_bytes) {
+            if ((rc = dalloc(t, &t->d_grid, bytes)) != VIO_OK) return rc;
+            t->grid_bytes = bytes;
+        }
+    }
+    return VIO_OK;
+}
+
+int tracker_alloc(erp_tracker* t) {
+    int rc;
+    int w = t->W, h = t->H;
+    t->nlev = 0;
+    for (int l = 0; l < TRK_MAX_LEVELS; ++l) {
+        t->lw[l] = w; t->lh[l] = h;
+        t->lp[l] = (int)align_up(w, 128);
+        for (int s = 0; s < 2; ++s)
+            if ((rc = dalloc(t, &t->lvl[s][l], (size_t)t->lp[l] * h)) != VIO_OK) return rc;
+        t->nlev = l + 1;
+        if (w <= 2 || h <= 2) break;
+        w = (w + 1) / 2; h = (h + 1) / 2;
+    }
+    const int P = std::max(t->max_points, 1);
+    if ((rc = dalloc(t, &t->d_pts, sizeof(float) * 2 * P))) return rc;
+    if ((rc = dalloc(t, &t->d_next, sizeof(float) * 2 * P))) return rc;
+    if ((rc = dalloc(t, &t->d_err, sizeof(float) * P))) return rc;
+    if ((rc = dalloc(t, &t->d_status, P))) return rc;
+    if ((rc = dalloc(t, &t->d_kept, P))) return rc;
+    if ((rc = dalloc(t, &t->d_gidx, sizeof(int) * P))) return rc;
+    if ((rc = dalloc(t, &t->d_b0, sizeof(float) * 3 * P))) return rc;
+    if ((rc = dalloc(t, &t->d_b1, sizeof(float) * 3 * P))) return rc;
+    if ((rc = dalloc(t, &t->d_scal, sizeof(int) * 16))) return rc;
+    if ((rc = dalloc(t, &t->d_corners, sizeof(float) * 2 * std::max(t->max_corners, 1)))) return rc;
+    t->disc_words = (t->W + 31) / 32;
+    if ((rc = dalloc(t, &t->d_disc, sizeof(uint32_t) * t->disc_words * t->H))) return rc;
+    if ((rc = ensure_iters(t, 1024))) return rc;
+    for (auto& e : t->ev)
+        if (hipEventCreate(&e) != hipSuccess) return hip_fail(t->ctx, hipErrorUnknown, "hipEventCreate");
+    return VIO_OK;
+}
+
+// top LK level: buildOpticalFlowPyramid stops when the next level would be <= winSize
+int lk_top_level(const erp_tracker* t, int win, int max_level) {
+    int lvl = 0;
+    for (int l = 0; l <= max_level && l < t->nlev; ++l) {
+        lvl = l;
+        int nw = (t->lw[l] + 1) / 2, nh = (t->lh[l] + 1) / 2;
+        if (nw <= win || nh <= win || l + 1 >= t->nlev) break;
+    }
+    return lvl;
+}
+
+int build_pyramids(erp_tracker* t, int top) {
+    for (int l = 1; l <= top; ++l) {
+        PyrLevelPair s{t->lvl[0][l - 1], t->lvl[1][l - 1], t->lw[l - 1], t->lh[l - 1], t->lp[l - 1]};
+        PyrLevelPair d{t->lvl[0][l], t->lvl[1][l], t->lw[l], t->lh[l], t->lp[l]};
+        hipError_t e = launch_pyr_down(s, d, 2, t->ctx->stream);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "pyr_down_kernel");
+    }
+    return VIO_OK;
+}
+
+int check_klt(vio_ctx* ctx, const erp_klt_params* p) {
+    if (!p) { set_error(ctx, "null erp_klt_params"); return VIO_EINVAL; }
+    if (p->win <= 2 || p->win > 21 || p->max_level < 0 || p->max_level >= TRK_MAX_LEVELS) {
+        set_error(ctx, "unsupported LK window / level (win in [3,21], max_level < 8)");
+        return VIO_ENOSYS;
+    }
+    return VIO_OK;
+}
+
+int enqueue_lk(erp_tracker* t, const erp_klt_params* p, int n) {
+    LkArgs a;
+    std::memset(&a, 0, sizeof a);
+    int top = lk_top_level(t, p->win, p->max_level);
+    int rc = build_pyramids(t, top);
+    if (rc) return rc;
+    for (int l = 0; l <= top; ++l) a.lv[l] = LkLevel{t->lvl[0][l], t->lvl[1][l], t->lw[l], t->lh[l], t->lp[l]};
+    a.levels = top;
+    a.pts = t->d_pts;
+    a.next = t->d_next;
+    a.status = t->d_status;
+    a.err = t->d_err;
+    a.n = n;
+    a.win = p->win;
+    // TermCriteria clamps (lkpyramid.cpp): maxCount in [0,100], epsilon in [0,10], squared
+    a.max_iters = std::min(std::max(p->max_iters, 0), 100);
+    double eps = std::min(std::max((double)p->epsilon, 0.0), 10.0);
+    a.eps2 = eps * eps;
+    a.min_eig = p->min_eig_threshold;
+    if (t->ev[1]) (void)hipEventRecord(t->ev[1], t->ctx->stream);
+    hipError_t e = launch_lk(a, t->ctx->stream);
+    if (e != hipSuccess) return hip_fail(t->ctx, e, "lk_kernel");
+    return VIO_OK;
+}
+
+RansacArgs ransac_args(erp_tracker* t, int n, int mode, int iters, uint32_t seed, float thr, float polar, int margin,
+                       const float* p0, const float* p1) {
+    RansacArgs r;
+    std::memset(&r, 0, sizeof r);
+    r.p0 = p0; r.p1 = p1; r.status = t->d_status;
+    r.n = n; r.W = t->W; r.H = t->H; r.mode = mode;
+    r.polar_ratio = polar; r.margin = margin;
+    r.gidx = t->d_gidx; r.n_good = t->d_scal + 0;
+    r.b0 = t->d_b0; r.b1 = t->d_b1;
+    r.samples = t->d_samples; r.iters = iters; r.seed = seed; r.thresh = thr;
+    r.count = t->d_count; r.kept = t->d_kept; r.n_in = t->d_scal + 1;
+    return r;
+}
+
+int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* mask, int mask_pitch, int max_corners,
+                 double quality, double min_dist, bool discs, int margin, float polar) {
+    int rc = ensure_gftt(t, min_dist);
+    if (rc) return rc;
+    GfArgs g;
+    std::memset(&g, 0, sizeof g);
+    g.img = img; g.W = t->W; g.H = t->H; g.pitch = pitch;
+    g.mask = mask; g.mask_pitch = mask_pitch;
+    // Camera::CreatePolarMask (Camera.cpp:100-118) + the left/right boundary mask (FeatureTracker.cpp:49-58)
+    g.top_rows = (int)((float)t->H * polar);
+    g.bottom_start = (int)((float)t->H * (1.0f - polar));
+    g.margin = margin;
+    g.disc_bits = discs ? t->d_disc : nullptr;
+    g.disc_words = t->disc_words;
+    g.quality = quality; g.min_dist = min_dist; g.max_corners = max_corners;
+    g.max_ord = (uint32_t*)(t->d_scal + 2);
+    g.cand = t->d_cand; g.cand_sorted = t->d_cand_sorted;
+    g.n_cand = (unsigned int*)(t->d_scal + 3);
+    g.cand_cap = t->cand_cap;
+    g.cell = min_dist >= 1 ? (int)std::lrint(min_dist) : 1;
+    g.gw = (t->W + g.cell - 1) / g.cell;
+    g.gh = (t->H + g.cell - 1) / g.cell;
+    size_t lds = (size_t)g.gw * g.gh * 3 * sizeof(uint32_t);
+    g.grid_global = lds > 96 * 1024 ? t->d_grid : nullptr;
+    g.corners = t->d_corners;
+    g.n_out = t->d_scal + 4;
+    if (!g.grid_global) {
+        hipError_t e = gftt_select_set_lds(std::max<size_t>(lds, 4));
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "hipFuncSetAttribute(gftt_select)");
+    }
+    VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal + 2, 0, 3 * sizeof(int), t->ctx->stream));
+    VIO_HIP(t->ctx, hipMemsetAsync(t->d_cand, 0, sizeof(unsigned long long) * t->cand_cap, t->ctx->stream));
+    hipError_t e = launch_gftt(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+    if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt kernels");
+    return VIO_OK;
+}
+
+int upload_frame(erp_tracker* t, int slot, const uint8_t* img, int stride) {
+    if (!img || stride < t->W) { set_error(t->ctx, "bad frame"); return VIO_EINVAL; }
+    VIO_HIP(t->ctx, hipMemcpy2DAsync(t->lvl[slot][0], t->lp[0], img, stride, t->W, t->H, hipMemcpyHostToDevice,
+                                     t->ctx->stream));
+    return VIO_OK;
+}
+
+int read_corners(erp_tracker* t, float* out_xy, int* n_out) {
+    int n = 0;
+    VIO_HIP(t->ctx, hipMemcpyAsync(&n, t->d_scal + 4, sizeof(int), hipMemcpyDeviceToHost, t->ctx->stream));
+    VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    if (n > 0 && out_xy)
+        VIO_HIP(t->ctx, hipMemcpy(out_xy, t->d_corners, sizeof(float) * 2 * n, hipMemcpyDeviceToHost));
+    *n_out = n;
+    return VIO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int erp_ransac_samples(uint32_t seed, int n, int iters, int32_t* out) {
+    if (n < 3 || iters < 0 || (iters > 0 && !out)) return VIO_EINVAL;
+    std::mt19937 gen(seed);
+    std::uniform_int_distribution<> dis(0, n - 1);
+    for (int it = 0; it < iters; ++it) {
+        int got[3], k = 0;
+        while (k < 3) {
+            int idx = dis(gen);
+            bool dup = false;
+            for (int q = 0; q < k; ++q) dup |= got[q] == idx;
+            if (!dup) got[k++] = idx;
+        }
+        out[3 * it] = got[0]; out[3 * it + 1] = got[1]; out[3 * it + 2] = got[2];
+    }
+    return VIO_OK;
+}
+
+int erp_tracker_create(vio_ctx* ctx, int W, int H, int max_points, int max_corners, erp_tracker** out) {
+    if (!ctx || !out || W < 8 || H < 8 || W > 65535 || H > 65535 || max_points < 0 || max_corners < 0)
+        return VIO_EINVAL;
+    *out = nullptr;
+    (void)hipSetDevice(ctx->device);
+    erp_tracker* t = new erp_tracker();
+    t->ctx = ctx; t->W = W; t->H = H; t->max_points = max_points; t->max_corners = max_corners;
+    int rc = tracker_alloc(t);
+    if (rc) { tracker_free(t); delete t; return rc; }
+    *out = t;
+    return VIO_OK;
+}
+
+void erp_tracker_destroy(erp_tracker* t) {
+    if (!t) return;
+    (void)hipSetDevice(t->ctx->device);
+    (void)hipStreamSynchronize(t->ctx->stream);
+    tracker_free(t);
+    delete t;
+}
+
+int erp_tracker_upload(erp_tracker* t, int slot, const uint8_t* img, int stride) {
+    if (!t || slot < 0 || slot > 1) return VIO_EINVAL;
+    return upload_frame(t, slot, img, stride);
+}
+
+int erp_tracker_device_frame(erp_tracker* t, int slot, uint8_t** dev_ptr, int* pitch) {
+    if (!t || slot < 0 || slot > 1 || !dev_ptr || !pitch) return VIO_EINVAL;
+    *dev_ptr = t->lvl[slot][0];
+    *pitch = t->lp[0];
+    return VIO_OK;
+}
+
+int erp_tracker_swap(erp_tracker* t) {
+    if (!t) return VIO_EINVAL;
+    for (int l = 0; l < t->nlev; ++l) std::swap(t->lvl[0][l], t->lvl[1][l]);
+    return VIO_OK;
+}
+
+int erp_tracker_set_points(erp_tracker* t, const float* pts, int n) {
+    if (!t || n < 0 || n > t->max_points || (n > 0 && !pts)) {
+        if (t) set_error(t->ctx, "point count exceeds max_points");
+        return VIO_EINVAL;
+    }
+    t->n_pts = n;
+    if (n) VIO_HIP(t->ctx, hipMemcpyAsync(t->d_pts, pts, sizeof(float) * 2 * n, hipMemcpyHostToDevice, t->ctx->stream));
+    return VIO_OK;
+}
+
+int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p) {
+    if (!t || !p) return VIO_EINVAL;
+    int rc = check_klt(t->ctx, klt);
+    if (rc) return rc;
+    if (p->ransac_iters < 0 || p->max_corners < 0 || p->max_corners > t->max_corners || p->quality <= 0 ||
+        p->min_dist < 0) {
+        set_error(t->ctx, "bad erp_tracker_params");
+        return VIO_EINVAL;
+    }
+    if ((rc = ensure_iters(t, std::max(p->ransac_iters, 1)))) return rc;
+    hipStream_t st = t->ctx->stream;
+    const int n = t->n_pts;
+    VIO_HIP(t->ctx, hipEventRecord(t->ev[0], st));
+    if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK
+    VIO_HIP(t->ctx, hipEventRecord(t->ev[2], st));
+    RansacArgs r = ransac_args(t, n, 1, p->ransac_iters, p->ransac_seed, p->ransac_thresh_rad, p->polar_ratio,
+                               p->boundary_margin, t->d_pts, t->d_next);
+    if (n > 0) {
+        hipError_t e = launch_ransac(r, true, st);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac kernels");
+    } else {
+        VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal, 0, 2 * sizeof(int), st));
+    }
+    VIO_HIP(t->ctx, hipEventRecord(t->ev[3], st));
+    // CreateFeatureMask: discs of radius (int)min_dist around every kept point
+    VIO_HIP(t->ctx, hipMemsetAsync(t->d_disc, 0, sizeof(uint32_t) * t->disc_words * t->H, st));
+    const int radius = (int)p->min_dist;
+    if (radius != t->halfw_r) {
+        std::vector<int> hw = circle_half_widths(radius);
+        if ((rc = dalloc(t, &t->d_halfw, sizeof(int) * (radius + 1)))) return rc;
+        VIO_HIP(t->ctx, hipMemcpy(t->d_halfw, hw.data(), sizeof(int) * (radius + 1), hipMemcpyHostToDevice));
+        t->halfw_r = radius;
+    }
+    VIO_HIP(t->ctx, hipMemcpyAsync(t->d_scal + 5, &t->n_pts, sizeof(int), hipMemcpyHostToDevice, st));
+    if (n > 0 && radius > 0) {
+        DiscArgs d{t->d_next, t->d_kept, nullptr, t->d_scal + 5, t->d_disc, t->disc_words, t->W, t->H, radius,
+                   t->d_halfw};
+        hipError_t e = launch_disc_mask(d, n, st);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "disc_mask_kernel");
+    }
+    if ((rc = enqueue_gftt(t, t->lvl[1][0], t->lp[0], nullptr, 0, p->max_corners, p->quality, p->min_dist, true,
+                           p->boundary_margin, p->polar_ratio)))
+        return rc;
+    VIO_HIP(t->ctx, hipEventRecord(t->ev[4], st));
+    t->ran = true;
+    return VIO_OK;
+}
+
+int erp_tracker_sync(erp_tracker* t) {
+    if (!t) return VIO_EINVAL;
+    VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    return VIO_OK;
+}
+
+int erp_tracker_download(erp_tracker* t, float* next, uint8_t* status, uint8_t* kept, float* corners, int* n_corners) {
+    if (!t) return VIO_EINVAL;
+    VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    const int n = t->n_pts;
+    if (n && next) VIO_HIP(t->ctx, hipMemcpy(next, t->d_next, sizeof(float) * 2 * n, hipMemcpyDeviceToHost));
+    if (n && status) VIO_HIP(t->ctx, hipMemcpy(status, t->d_status, n, hipMemcpyDeviceToHost));
+    if (n && kept) VIO_HIP(t->ctx, hipMemcpy(kept, t->d_kept, n, hipMemcpyDeviceToHost));
+    if (n_corners) {
+        int nc = 0;
+        int rc = read_corners(t, corners, &nc);
+        if (rc) return rc;
+        *n_corners = nc;
+    }
+    return VIO_OK;
+}
+
+int erp_tracker_stage_ms(erp_tracker* t, double* pyr_ms, double* lk_ms, double* ransac_ms, double* gftt_ms,
+                         double* total_ms) {
+    if (!t || !t->ran) return VIO_EINVAL;
+    VIO_HIP(t->ctx, hipEventSynchronize(t->ev[4]));
+    float a = 0, b = 0, c = 0, d = 0, e = 0;
+    VIO_HIP(t->ctx, hipEventElapsedTime(&a, t->ev[0], t->ev[1]));
+    VIO_HIP(t->ctx, hipEventElapsedTime(&b, t->ev[1], t->ev[2]));
+    VIO_HIP(t->ctx, hipEventElapsedTime(&c, t->ev[2], t->ev[3]));
+    VIO_HIP(t->ctx, hipEventElapsedTime(&d, t->ev[3], t->ev[4]));
+    VIO_HIP(t->ctx, hipEventElapsedTime(&e, t->ev[0], t->ev[4]));
+    if (pyr_ms) *pyr_ms = a;
+    if (lk_ms) *lk_ms = b;
+    if (ransac_ms) *ransac_ms = c;
+    if (gftt_ms) *gftt_ms = d;
+    if (total_ms) *total_ms = e;
+    return VIO_OK;
+}
+
+int erp_klt_track(vio_ctx* ctx, const uint8_t* prev, const uint8_t* curr, int W, int H, int stride, const float* pts,
+                  int n, float* next, uint8_t* status, float* err, const erp_klt_params* params) {
+    if (!ctx || !prev || !curr || n < 0 || (n > 0 && (!pts || !next || !status))) return VIO_EINVAL;
+    int rc = check_klt(ctx, params);
+    if (rc) return rc;
+    erp_tracker* t = nullptr;
+    if ((rc = erp_tracker_create(ctx, W, H, std::max(n, 1), 0, &t))) return rc;
+    if (!(rc = upload_frame(t, 0, prev, stride)) && !(rc = upload_frame(t, 1, curr, stride)) &&
+        !(rc = erp_tracker_set_points(t, pts, n)) && !(rc = enqueue_lk(t, params, n))) {
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) rc = hip_fail(ctx, e, "erp_klt_track");
+        else if (n) {
+            if (hipMemcpy(next, t->d_next, sizeof(float) * 2 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(status, t->d_status, n, hipMemcpyDeviceToHost) != hipSuccess ||
+                (err && hipMemcpy(err, t->d_err, sizeof(float) * n, hipMemcpyDeviceToHost) != hipSuccess))
+                rc = hip_fail(ctx, hipErrorUnknown, "erp_klt_track download");
+        }
+    }
+    erp_tracker_destroy(t);
+    return rc;
+}
+
+int erp_gftt(vio_ctx* ctx, const uint8_t* img, const uint8_t* mask, int W, int H, int stride, int max_corners,
+             double quality, double min_dist, float* out_xy, int* n_out) {
+    if (!ctx || !img || !n_out || W < 3 || H < 3 || quality <= 0 || min_dist < 0 || max_corners < 0) return VIO_EINVAL;
+    if (max_corners == 0) max_corners = W * H;  // "no limit"
+    erp_tracker* t = nullptr;
+    int rc = erp_tracker_create(ctx, W, H, 1, max_corners, &t);
+    if (rc) return rc;
+    uint8_t* dmask = nullptr;
+    if (!(rc = upload_frame(t, 1, img, stride))) {
+        if (mask) {
+            if (!(rc = dalloc(t, &dmask, (size_t)t->lp[0] * H))) {
+                hipError_t e = hipMemcpy2DAsync(dmask, t->lp[0], mask, stride, W, H, hipMemcpyHostToDevice, ctx->stream);
+                if (e != hipSuccess) rc = hip_fail(ctx, e, "mask upload");
+            }
+        }
+        if (!rc) rc = enqueue_gftt(t, t->lvl[1][0], t->lp[0], dmask, t->lp[0], max_corners, quality, min_dist, false,
+                                   0, 0.f);
+        if (!rc) rc = read_corners(t, out_xy, n_out);
+        if (!rc) {
+            unsigned int nc = 0;
+            if (hipMemcpy(&nc, t->d_scal + 3, sizeof(nc), hipMemcpyDeviceToHost) == hipSuccess && nc > t->cand_cap) {
+                set_error(ctx, "GFTT candidate buffer overflow");
+                rc = VIO_ENOSYS;
+            }
+        }
+    }
+    erp_tracker_destroy(t);
+    return rc;
+}
+
+int erp_rot_ransac(vio_ctx* ctx, const float* p0, const float* p1, int n, int W, int H, const int32_t* samples,
+                   int iters, float thresh_rad, uint8_t* mask, int* n_in) {
+    if (!ctx || n < 0 || !mask || !n_in || iters < 0 || (n >= 3 && iters > 0 && !samples) || (n > 0 && (!p0 || !p1)))
+        return VIO_EINVAL;
+    if (n < 3) {  // FeatureTracker.cpp:130-134 / :258-260
+        for (int i = 0; i < n; ++i) mask[i] = 1;
+        *n_in = n;
+        return VIO_OK;
+    }
+    for (int i = 0; i < 3 * iters; ++i)
+        if (samples[i] < 0 || samples[i] >= n) { set_error(ctx, "RANSAC sample index out of range"); return VIO_EINVAL; }
+    erp_tracker* t = nullptr;
+    int rc = erp_tracker_create(ctx, std::max(W, 8), std::max(H, 8), n, 0, &t);
+    if (rc) return rc;
+    t->W = W; t->H = H;
+    float* d_p1 = nullptr;
+    if (!(rc = ensure_iters(t, std::max(iters, 1))) && !(rc = dalloc(t, &d_p1, sizeof(float) * 2 * n))) {
+        hipStream_t st = ctx->stream;
+        if (hipMemcpyAsync(t->d_pts, p0, sizeof(float) * 2 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(d_p1, p1, sizeof(float) * 2 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+            (iters && hipMemcpyAsync(t->d_samples, samples, sizeof(int32_t) * 3 * iters, hipMemcpyHostToDevice, st) !=
+                          hipSuccess)) {
+            rc = hip_fail(ctx, hipErrorUnknown, "ransac upload");
+        } else {
+            RansacArgs r = ransac_args(t, n, 0, iters, 0, thresh_rad, 0.f, 0, t->d_pts, d_p1);
+            hipError_t e = launch_ransac(r, false, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) rc = hip_fail(ctx, e, "ransac kernels");
+            else if (hipMemcpy(mask, t->d_kept, n, hipMemcpyDeviceToHost) != hipSuccess ||
+                     hipMemcpy(n_in, t->d_scal + 1, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+                rc = hip_fail(ctx, hipErrorUnknown, "ransac download");
+        }
+    }
+    erp_tracker_destroy(t);
+    return rc;
+}
+
+}  // extern "C"

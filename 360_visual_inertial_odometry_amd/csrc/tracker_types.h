@@ -1,0 +1,95 @@
+// tracker_types.h — kernel argument blocks of the ERP tracker (tracker.hip), shared with the host
+// side (tracker_host.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vio360 {
+
+constexpr int TRK_MAX_LEVELS = 8;
+
+struct PyrLevelPair {  // one pyramid level of both frames (same geometry)
+    uint8_t* p0;
+    uint8_t* p1;
+    int w, h, pitch;
+};
+
+struct LkLevel {
+    const uint8_t* prev;
+    const uint8_t* curr;
+    int w, h, pitch;
+};
+
+struct LkArgs {
+    LkLevel lv[TRK_MAX_LEVELS];
+    int levels;  // top level index (maxLevel after buildOpticalFlowPyramid's size check)
+    const float* pts;
+    float* next;
+    uint8_t* status;
+    float* err;
+    int n, win, max_iters;
+    float min_eig;
+    double eps2;
+};
+
+struct RansacArgs {
+    const float* p0;       // [n][2] previous points
+    const float* p1;       // [n][2] tracked points
+    const uint8_t* status; // [n] (mode 1)
+    int n, W, H, mode;     // mode 0: every point enters RANSAC; 1: status/polar/boundary filter first
+    float polar_ratio;
+    int margin;
+    int* gidx;             // [n] compacted -> input index
+    int* n_good;           // device scalar
+    float* b0;             // [n][3] bearings of the compacted points
+    float* b1;
+    int32_t* samples;      // [iters][3]
+    int iters;
+    uint32_t seed;
+    float thresh;
+    int* count;            // [iters]
+    uint8_t* kept;         // [n] output mask in input order
+    int* n_in;             // device scalar
+};
+
+struct GfArgs {
+    const uint8_t* img;
+    int W, H, pitch;
+    // mask: explicit u8 (mask != null), else analytic region + optional disc bitmask
+    const uint8_t* mask;
+    int mask_pitch;
+    int top_rows, bottom_start, margin;
+    const uint32_t* disc_bits;
+    int disc_words;  // 32-bit words per row
+    double quality, min_dist;
+    int max_corners;
+    uint32_t* max_ord;              // device scalar (ordered-int max of the masked eig map)
+    unsigned long long* cand;       // [cand_cap]
+    unsigned long long* cand_sorted;
+    unsigned int* n_cand;           // device scalar
+    unsigned int cand_cap;
+    int cell, gw, gh;
+    uint32_t* grid_global;          // non-null when the selection grid does not fit LDS
+    float* corners;                 // [max_corners][2]
+    int* n_out;                     // device scalar
+};
+
+struct DiscArgs {
+    const float* pts;       // [n][2]
+    const uint8_t* kept;    // [n] or null (every point)
+    const int* src_index;   // null: point k = pts[k]
+    const int* n_pts_dev;   // device scalar: number of points
+    uint32_t* bits;
+    int words, W, H, radius;
+    const int* halfw;       // [radius+1]
+};
+
+hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int frames, hipStream_t st);
+hipError_t launch_lk(const LkArgs& a, hipStream_t st);
+hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st);
+hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st);
+hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st);
+size_t gftt_sort_tmp_bytes(unsigned int cap);
+hipError_t gftt_select_set_lds(size_t bytes);
+
+}  // namespace vio360

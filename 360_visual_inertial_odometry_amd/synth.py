@@ -356,3 +356,88 @@ def make_global(K=1000, L=50000, k_per=10, seed=SEED + 5, W=ERP_W, H=ERP_H):
         "lm_true": P_true, "obs_kf": np.array(obs_kf, np.int32), "obs_lm": np.array(obs_lm, np.int32),
         "obs_uv": np.array(obs_uv, np.float32),
     }
+
+
+# --------------------------------------------------------------------------------------------
+# Config 1: ERP frames of a procedural environment: seeded multi-octave 3-D value
+# noise sampled along every ERP ray.  A pure camera rotation gives an analytic flow field.
+def _value_noise_tables(seed):
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(256).astype(np.int64)
+    vals = rng.random(256).astype(np.float32)
+    return np.concatenate([perm, perm]), vals
+
+
+def erp_rays(W, H):
+    """Unit bearings of the pixel centres of a W x H ERP image (Camera::PixelToBearing convention:
+    X-right, Y-down, Z-forward; u = W(0.5 + lon/2pi), v = H(0.5 - lat/pi)), shape (H, W, 3)."""
+    u = (np.arange(W, dtype=np.float64) + 0.5) / W
+    v = (np.arange(H, dtype=np.float64) + 0.5) / H
+    lon = (u - 0.5) * 2 * np.pi
+    lat = -(v - 0.5) * np.pi
+    cl = np.cos(lat)[:, None]
+    return np.stack([cl * np.sin(lon)[None, :], np.broadcast_to(-np.sin(lat)[:, None], (H, W)),
+                     cl * np.cos(lon)[None, :]], -1)
+
+
+def render_erp(W, H, R_wc=None, seed=1, octaves=6, base_freq=None, rows_per_chunk=64):
+    """u8 ERP image of the value-noise environment seen by a camera with rotation R_wc.  The base
+    frequency scales with the width so the per-pixel texture (and the LK minEig test) is the same
+    at every resolution."""
+    if base_freq is None:
+        base_freq = 12.0 * W / 960.0
+    perm, vals = _value_noise_tables(seed)
+    R = np.eye(3) if R_wc is None else np.asarray(R_wc, np.float64)
+    img = np.empty((H, W), np.uint8)
+    rays_all = erp_rays(W, H)
+    for y0 in range(0, H, rows_per_chunk):
+        d = rays_all[y0:y0 + rows_per_chunk] @ R.T  # world directions
+        acc = np.zeros(d.shape[:2], np.float64)
+        amp, tot = 1.0, 0.0
+        for o in range(octaves):
+            p = d * (base_freq * (2.0 ** o)) + 17.0 * (o + 1)
+            i0 = np.floor(p).astype(np.int64)
+            f = p - i0
+            f = f * f * (3 - 2 * f)  # smoothstep
+            n = 0.0
+            for dz in (0, 1):
+                for dy in (0, 1):
+                    for dx in (0, 1):
+                        h = perm[(perm[(perm[(i0[..., 0] + dx) & 255] + i0[..., 1] + dy) & 255] + i0[..., 2] + dz) & 255]
+                        wgt = (f[..., 0] if dx else 1 - f[..., 0]) * (f[..., 1] if dy else 1 - f[..., 1]) * \
+                              (f[..., 2] if dz else 1 - f[..., 2])
+                        n = n + wgt * vals[h]
+            acc += amp * n
+            tot += amp
+            amp *= 0.55
+        img[y0:y0 + rows_per_chunk] = np.clip(acc / tot * 255.0 * 1.6 - 80.0, 0, 255).astype(np.uint8)
+    return img
+
+
+def rot_yaw_pitch(yaw_deg, pitch_deg):
+    """Camera rotation: yaw about camera Y (down axis), then pitch about camera X."""
+    a, b = math.radians(yaw_deg), math.radians(pitch_deg)
+    Ry = np.array([[math.cos(a), 0, math.sin(a)], [0, 1, 0], [-math.sin(a), 0, math.cos(a)]])
+    Rx = np.array([[1, 0, 0], [0, math.cos(b), -math.sin(b)], [0, math.sin(b), math.cos(b)]])
+    return Ry @ Rx
+
+
+def erp_flow_truth(pts, W, H, R_21):
+    """Analytic position in frame 2 of frame-1 pixels under a pure rotation: d2 = R_21 d1."""
+    pts = np.asarray(pts, np.float64)
+    lon = (pts[:, 0] / W - 0.5) * 2 * np.pi
+    lat = -(pts[:, 1] / H - 0.5) * np.pi
+    d = np.stack([np.cos(lat) * np.sin(lon), -np.sin(lat), np.cos(lat) * np.cos(lon)], -1) @ np.asarray(R_21).T
+    u = W * (0.5 + np.arctan2(d[:, 0], d[:, 2]) / (2 * np.pi))
+    v = H * (0.5 - (-np.arcsin(np.clip(d[:, 1], -1, 1))) / np.pi)
+    return np.stack([u, v], -1)
+
+
+def config1(W=3840, H=1920, yaw_deg=1.5, pitch_deg=0.5, seed=1):
+    """Two-frame ERP KLT pair: frame 2 = same scene, camera yawed/pitched (pure rotation).
+    Returns (img1, img2, R_21) with R_21 mapping frame-1 camera bearings to frame-2 bearings."""
+    R1 = np.eye(3)
+    R2 = rot_yaw_pitch(yaw_deg, pitch_deg)  # R_wc of frame 2
+    img1 = render_erp(W, H, R1, seed=seed)
+    img2 = render_erp(W, H, R2, seed=seed)
+    return img1, img2, R2.T @ R1

@@ -69,6 +69,79 @@ def cpu_baseline(vio, synth, lm_iters, seconds):
                       f"{busy:.1f} s of solve time"}
 
 
+def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
+    """Config 1: two-frame ERP KLT pair at 3840x1920, 300 corners.  One step = the
+    device pipeline erp_tracker_run on frames resident in HBM: pyramids of both frames, LK of the
+    300 points, status/polar/boundary filter + 1000-hypothesis rotation RANSAC, GFTT re-detection
+    on frame 2 masked by the kept points."""
+    W, H = 3840, 1920
+    a, b, _ = synth.config1(W, H)
+    mask = np.zeros((H, W), np.uint8)
+    mask[int(np.float32(H) * np.float32(0.15)):int(np.float32(H) * np.float32(0.85)), 20:W - 20] = 255
+    pts = ctx.gftt(a, mask, 300, float(np.float32(0.01)), 30.0)
+    prm = vio.default_tracker_params(max_corners=300, seed=1)
+    t = vio.Tracker(ctx, W, H, max_points=512, max_corners=512)
+    t.upload(0, a)
+    t.upload(1, b)
+    t.set_points(pts)
+    for _ in range(warmup):
+        t.run(prm)
+    t.sync()
+    stage = {k: 0.0 for k in ("pyramids", "lk", "ransac", "gftt", "total")}
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        t.run(prm)
+        t.sync()
+        for k, v in t.stage_ms().items():
+            stage[k] += v / steps
+    wall = (time.perf_counter() - t0) / steps
+    res = t.download()
+    t.close()
+    mpx = W * H / 1e6
+    alg_bytes = 2.0 * W * H  # SURVEY §8d: each u8 frame read once
+    out = {
+        "metric": "ERP-KLT Mpx/s (config 1: 3840x1920 pair, 300 corners)",
+        "value": mpx / wall,
+        "unit": "Mpx/s",
+        "ms_per_step": wall * 1e3,
+        "device_ms_per_step": stage["total"],
+        "stage_ms": stage,
+        "tracked": int(res["status"].sum()),
+        "kept": int(res["kept"].sum()),
+        "new_corners": int(len(res["corners"])),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": alg_bytes / (stage["total"] * 1e-3) / 1e9,
+            "peak": 8000.0,
+            "unit": "GB/s",
+            "frac": alg_bytes / (stage["total"] * 1e-3) / 8.0e12,
+            "traffic": None,
+            "note": "algorithmic 2 B/px (both u8 frames read once) over the whole pipeline's device time",
+        },
+        "cpu_baseline": None,
+    }
+    if want_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        kp = vio.default_klt_params()
+        n, busy = 0, 0.0
+        while busy < cpu_seconds or n < 1:
+            ts = time.perf_counter()
+            nxt, st, _ = oracle_lib.klt_track(a, b, pts, kp)
+            vr = nxt[:, 1] / np.float32(H)
+            good = np.nonzero((st == 1) & (vr >= 0.15) & (vr <= 0.85) & (nxt[:, 0] >= 20) & (nxt[:, 0] <= W - 20))[0]
+            s = vio.ransac_samples(1, len(good), 1000)
+            km, _ = oracle_lib.rot_ransac(pts[good], nxt[good], W, H, s, vio.ransac_threshold())
+            m2 = mask.copy()
+            oracle_lib.gftt(b, m2, 300, float(np.float32(0.01)), 30.0)
+            busy += time.perf_counter() - ts
+            n += 1
+        out["cpu_baseline"] = {"value": n * mpx / busy, "unit": "Mpx/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} config-1 frame pairs through oracle/tracker_oracle.c (pyramids+LK+RANSAC+GFTT), "
+                                         f"{busy:.1f} s"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,6 +151,8 @@ def main():
     ap.add_argument("--lm-iters", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-klt", action="store_true")
+    ap.add_argument("--klt-steps", type=int, default=20)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -144,6 +219,8 @@ def main():
         single_kms, _ = one.kernel_ms()
         one.close()
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(vio, synth, args.lm_iters, args.cpu_seconds)
+        klt = None if args.no_klt else klt_bench(vio, synth, ctx, args.klt_steps, 3, args.cpu_seconds,
+                                                 not args.no_cpu_baseline and world == 1)
         single_ips = args.lm_iters / single_wall
         out = {
             "metric": "sliding-window BA iters/sec (10KF x 500pts)",
@@ -185,6 +262,7 @@ def main():
                 "vs_cpu": (single_ips / cpu["value"]) if cpu else None,
             },
             "cpu_baseline": cpu,
+            "erp_klt": klt,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -202,34 +202,58 @@ int erp_klt_track(vio_ctx* ctx, const uint8_t* prev, const uint8_t* curr, int W,
 int erp_gftt(vio_ctx* ctx, const uint8_t* img, const uint8_t* mask, int W, int H, int stride,
              int max_corners, double quality, double min_dist, float* out_xy, int* n_out);
 
-/* rotation-only RANSAC on ERP bearings with an injected sample stream (iters*3 indices) */
+/* rotation-only RANSAC on ERP bearings with an injected sample stream (iters*3 indices, each
+   triple distinct, as FeatureTracker.cpp:280-288 draws them).  mask[n] = best hypothesis' inliers
+   (all ones when no hypothesis has an inlier), *n_in = its inlier count. */
 int erp_rot_ransac(vio_ctx* ctx, const float* p0, const float* p1, int n, int W, int H,
                    const int32_t* samples, int iters, float thresh_rad, uint8_t* mask, int* n_in);
 
-/* whole FeatureTracker::TrackFeatures numeric path for one frame pair, device-resident:
-   pyramids of both frames + LK + RANSAC + GFTT re-detection (see erp_tracker_* below). */
+/* the reference's RANSAC sample stream made deterministic: std::mt19937(seed) +
+   std::uniform_int_distribution<>(0, n-1), three distinct indices per iteration
+   (FeatureTracker.cpp:273-288; the reference seeds from std::random_device).  Host-only helper. */
+int erp_ransac_samples(uint32_t seed, int n, int iters, int32_t* out);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Device-resident frame pipeline = the numeric part of FeatureTracker::TrackFeatures
+   (FeatureTracker.cpp:61-206) for one frame pair, all on the GPU with no host round trip:
+     pyramids of both frames -> pyramidal LK of the previous frame's points -> status / polar /
+     boundary filter (:117-126) -> rotation RANSAC on the survivors with the in-pipeline sample
+     stream of erp_ransac_samples(ransac_seed, n_good, ransac_iters) (:130-134) -> GFTT
+     re-detection on the current frame masked by polar ∧ boundary ∧ discs of radius
+     (int)min_dist around the kept points (CreateFeatureMask :386-402, DetectNewFeatures :208-226).
+   The host-side feature bookkeeping between those steps in the reference (RemoveClusteredFeatures,
+   Frame::LimitFeaturesPerGrid, feature ids) is the adapter's job; the in-pipeline
+   disc mask is built from every kept point. */
 typedef struct erp_tracker erp_tracker;
 int erp_tracker_create(vio_ctx* ctx, int W, int H, int max_points, int max_corners, erp_tracker** out);
-/* upload a frame into slot 0 (prev) or 1 (curr) */
+/* copy a host frame into slot 0 (prev) or 1 (curr); erp_tracker_device_frame gives the device
+   buffer of a slot (pitch *pitch bytes) for producers that write frames on the device */
 int erp_tracker_upload(erp_tracker* t, int slot, const uint8_t* img, int stride);
+int erp_tracker_device_frame(erp_tracker* t, int slot, uint8_t** dev_ptr, int* pitch);
+/* swap slots 0 and 1 (the current frame becomes the previous one, m_prev_image = current) */
+int erp_tracker_swap(erp_tracker* t);
 typedef struct {
-    int32_t n_pts;            /* tracked points (input) */
-    int32_t ransac_iters;     /* 1000 */
-    float ransac_thresh_rad;  /* 2 deg */
-    int32_t max_corners;      /* GFTT re-detection cap */
-    double quality;           /* 0.01 */
-    double min_dist;          /* 30 */
-    int32_t boundary_margin;  /* 20 */
-    float polar_ratio;        /* 0.15 */
+    int32_t ransac_iters;     /* 1000 (FeatureTracker.cpp:36) */
+    float ransac_thresh_rad;  /* 2 deg (:37, 2.0f * M_PI / 180.0f) */
+    uint32_t ransac_seed;     /* seed of the in-pipeline mt19937 sample stream */
+    int32_t max_corners;      /* goodFeaturesToTrack maxCorners (feature_detection.max_features) */
+    double quality;           /* qualityLevel (0.01) */
+    double min_dist;          /* minDistance (30); disc radius (int)min_dist */
+    int32_t boundary_margin;  /* camera.boundary_margin (20) */
+    float polar_ratio;        /* 0.15 (Camera::CreatePolarMask / IsInPolarRegion default) */
 } erp_tracker_params;
-/* runs the device pipeline (async); pts/samples already uploaded by erp_tracker_set_points */
-int erp_tracker_set_points(erp_tracker* t, const float* pts, int n, const int32_t* samples, int iters);
+/* previous-frame points (pixel coordinates) to track */
+int erp_tracker_set_points(erp_tracker* t, const float* pts, int n);
+/* enqueue the whole pipeline on the context stream (asynchronous) */
 int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p);
 int erp_tracker_sync(erp_tracker* t);
-int erp_tracker_download(erp_tracker* t, float* next, uint8_t* status, uint8_t* inlier,
-                         float* corners, int* n_corners);
-int erp_tracker_kernel_ms(erp_tracker* t, double* pyr_ms, double* lk_ms, double* gftt_ms,
-                          double* ransac_ms);
+/* results of the last run: per input point next position, LK status and kept flag
+   (status ∧ !polar ∧ !boundary ∧ RANSAC inlier); the new corners (≤ max_corners float2) */
+int erp_tracker_download(erp_tracker* t, float* next, uint8_t* status, uint8_t* kept, float* corners,
+                         int* n_corners);
+/* device time (ms) of the pipeline stages of the last run */
+int erp_tracker_stage_ms(erp_tracker* t, double* pyr_ms, double* lk_ms, double* ransac_ms, double* gftt_ms,
+                         double* total_ms);
 void erp_tracker_destroy(erp_tracker* t);
 
 #ifdef __cplusplus

@@ -6,6 +6,8 @@ import ctypes as C
 import os
 import subprocess
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 _lib = None
@@ -32,3 +34,75 @@ def ba_solve(vio, prob):
     if rc != 0:
         raise RuntimeError(f"oracle_ba_solve rc={rc}")
     return O.result()
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def klt_track(prev, curr, pts, params):
+    L = load()
+    prev = np.ascontiguousarray(prev, np.uint8)
+    curr = np.ascontiguousarray(curr, np.uint8)
+    H, W = prev.shape
+    pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 2)
+    n = len(pts)
+    nxt = np.zeros((n, 2), np.float32)
+    st = np.zeros(n, np.uint8)
+    err = np.zeros(n, np.float32)
+    rc = L.oracle_klt_track(_p(prev), _p(curr), W, H, W, _p(pts), n, _p(nxt), _p(st), _p(err), C.byref(params))
+    assert rc == 0
+    return nxt, st, err
+
+
+def gftt(img, mask, max_corners, quality, min_dist):
+    L = load()
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    cap = max_corners if max_corners > 0 else W * H
+    out = np.zeros((cap, 2), np.float32)
+    n = C.c_int()
+    rc = L.oracle_gftt(_p(img), _p(m) if m is not None else None, W, H, W, int(max_corners), C.c_double(quality),
+                       C.c_double(min_dist), _p(out), C.byref(n))
+    assert rc == 0
+    return out[: n.value].copy()
+
+
+def rot_ransac(p0, p1, W, H, samples, thresh):
+    L = load()
+    p0 = np.ascontiguousarray(p0, np.float32).reshape(-1, 2)
+    p1 = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    samples = np.ascontiguousarray(samples, np.int32).reshape(-1)
+    n = len(p0)
+    mask = np.zeros(n, np.uint8)
+    nin = C.c_int()
+    rc = L.oracle_rot_ransac(_p(p0), _p(p1), n, W, H, _p(samples), len(samples) // 3, C.c_float(thresh), _p(mask),
+                             C.byref(nin))
+    assert rc == 0
+    return mask, nin.value
+
+
+def min_eig_map(img):
+    L = load()
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    eig = np.zeros((H, W), np.float32)
+    L.oracle_min_eig_map(_p(img), W, H, W, _p(eig))
+    return eig
+
+
+def pyr_down(img):
+    L = load()
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape
+    out = np.zeros(((H + 1) // 2, (W + 1) // 2), np.uint8)
+    L.oracle_pyr_down(_p(img), W, H, W, _p(out), out.shape[1])
+    return out
+
+
+def pixel_to_bearing(u, v, W, H):
+    L = load()
+    b = np.zeros(3, np.float32)
+    L.oracle_pixel_to_bearing(C.c_float(u), C.c_float(v), W, H, _p(b))
+    return b

@@ -41,7 +41,7 @@ STRUCTS = {
     "vio_ba_summary": ("VioBaSummary", ["success", "num_bad_lm", "initial_cost", "fixed_cost"]),
     "vio_ba_output": ("VioBaOutput", ["T_wb", "lm_xyz", "obs_outlier", "summary"]),
     "erp_klt_params": ("ErpKltParams", ["win", "max_level", "epsilon", "min_eig_threshold"]),
-    "erp_tracker_params": ("ErpTrackerParams", ["n_pts", "ransac_thresh_rad", "quality", "min_dist",
+    "erp_tracker_params": ("ErpTrackerParams", ["ransac_iters", "ransac_seed", "quality", "min_dist",
                                                 "boundary_margin", "polar_ratio"]),
 }
 

@@ -1,0 +1,179 @@
+"""GPU parity of the HIP ERP tracker (libvio360.so via the C-ABI) against the CPU oracle.
+
+The HIP kernels implement the oracle's integer / float definitions literally (exact int64 LK sums,
+-ffp-contract=off), so the bar is BITWISE: tracked positions, status, RANSAC masks, corner lists.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+W, H = 960, 480
+
+
+@pytest.fixture(scope="module")
+def pair(synth):
+    return synth.config1(W, H)
+
+
+def region_mask(W, H, margin=20, polar=0.15):
+    m = np.zeros((H, W), np.uint8)
+    m[int(np.float32(H) * np.float32(polar)):int(np.float32(H) * (np.float32(1.0) - np.float32(polar))),
+      margin:W - margin] = 255
+    return m
+
+
+def test_klt_bitwise(vio, gpu_ctx, pair):
+    a, b, _ = pair
+    pts = oracle_lib.gftt(a, region_mask(W, H), 300, float(np.float32(0.01)), 30.0)
+    # add hard cases: image corners, outside the image, the polar rows
+    extra = np.array([[0, 0], [959.9, 479.9], [-30, 100], [1000, 20], [480, 5], [3.5, 240.25], [955.2, 300.7]],
+                     np.float32)
+    pts = np.concatenate([pts, extra])
+    prm = vio.default_klt_params()
+    g = gpu_ctx.klt_track(a, b, pts, prm)
+    o = oracle_lib.klt_track(a, b, pts, prm)
+    assert np.array_equal(g[1], o[1])
+    assert np.array_equal(g[0], o[0])
+    assert np.array_equal(g[2][o[1] == 1], o[2][o[1] == 1])
+
+
+def test_klt_params_and_levels(vio, gpu_ctx, pair):
+    a, b, _ = pair
+    pts = oracle_lib.gftt(a, None, 100, 0.01, 20.0)
+    for win, lv, it in [(15, 2, 10), (21, 0, 30), (9, 4, 5)]:
+        prm = vio.abi.ErpKltParams(win, lv, it, 0.01, 1e-4, 0)
+        g = gpu_ctx.klt_track(a, b, pts, prm)
+        o = oracle_lib.klt_track(a, b, pts, prm)
+        assert np.array_equal(g[1], o[1]) and np.array_equal(g[0], o[0]), (win, lv, it)
+    g = gpu_ctx.klt_track(a, b, np.zeros((0, 2), np.float32))
+    assert len(g[0]) == 0
+
+
+def test_gftt_bitwise(vio, gpu_ctx, pair):
+    a = pair[1]
+    q = float(np.float32(0.01))
+    m = region_mask(W, H)
+    m[200:260, 300:420] = 0
+    for mask, maxc, md in [(m, 300, 30.0), (None, 1000, 10.0), (m, 0, 5.0), (None, 50, 0.0), (m, 2000, 1.0)]:
+        g = gpu_ctx.gftt(a, mask, maxc, q, md)
+        o = oracle_lib.gftt(a, mask, maxc, q, md)
+        assert np.array_equal(g, o), (maxc, md, len(g), len(o))
+
+
+def test_gftt_odd_sizes(vio, gpu_ctx, synth):
+    rng = np.random.default_rng(0)
+    for (h, w) in [(37, 53), (129, 257), (64, 65)]:
+        img = synth.render_erp(w, h)
+        img = np.clip(img.astype(int) + rng.integers(-20, 20, img.shape), 0, 255).astype(np.uint8)
+        g = gpu_ctx.gftt(img, None, 0, 0.01, 3.0)
+        o = oracle_lib.gftt(img, None, 0, 0.01, 3.0)
+        assert np.array_equal(g, o), (h, w)
+
+
+def test_rot_ransac_bitwise(vio, gpu_ctx):
+    from test_tracker_oracle import planted_rotation
+    thr = vio.ransac_threshold()
+    for seed, frac, n in [(5, 0.2, 300), (9, 0.6, 120), (1, 0.0, 50), (3, 0.3, 1500)]:
+        p0, p1, inl = planted_rotation(n=n, outlier_frac=frac, seed=seed)
+        s = vio.ransac_samples(seed, len(p0), 1000)
+        g = gpu_ctx.rot_ransac(p0, p1, W, H, s, thr)
+        o = oracle_lib.rot_ransac(p0, p1, W, H, s, thr)
+        assert np.array_equal(g[0], o[0]) and g[1] == o[1]
+    m, k = gpu_ctx.rot_ransac(np.zeros((2, 2)), np.zeros((2, 2)), W, H, np.zeros(0, np.int32), thr)
+    assert m.tolist() == [1, 1] and k == 2
+
+
+def cv_circle_fill(mask, cx, cy, r):
+    """OpenCV drawing.cpp Circle(fill=1), LINE_8: the midpoint loop painting its spans."""
+    h, w = mask.shape
+    err, dx, dy, plus, minus = 0, r, 0, 1, (r << 1) - 1
+    while dx >= dy:
+        for (yy, xl, xr) in ((cy - dy, cx - dx, cx + dx), (cy + dy, cx - dx, cx + dx),
+                             (cy - dx, cx - dy, cx + dy), (cy + dx, cx - dy, cx + dy)):
+            if 0 <= yy < h:
+                mask[yy, max(xl, 0):min(xr, w - 1) + 1] = 0
+        dy += 1
+        err += plus
+        plus += 2
+        msk = (err <= 0) - 1
+        err -= minus & msk
+        dx += msk
+        minus -= msk & 2
+
+
+def pipeline_oracle(vio, prev, curr, pts, prm, klt):
+    """TrackFeatures' numeric path composed from the oracle pieces."""
+    H, W = prev.shape
+    nxt, st, _ = oracle_lib.klt_track(prev, curr, pts, klt)
+    vr = nxt[:, 1] / np.float32(H)
+    polar = (vr < np.float32(prm.polar_ratio)) | (vr > np.float32(1.0) - np.float32(prm.polar_ratio))
+    m = np.float32(prm.boundary_margin)
+    nearb = (nxt[:, 0] < m) | (nxt[:, 0] > np.float32(W) - m) | (nxt[:, 1] < m) | (nxt[:, 1] > np.float32(H) - m)
+    good = np.nonzero((st == 1) & ~polar & ~nearb)[0]
+    kept = np.zeros(len(pts), np.uint8)
+    if len(good) >= 3:
+        s = vio.ransac_samples(prm.ransac_seed, len(good), prm.ransac_iters)
+        mk, _ = oracle_lib.rot_ransac(pts[good], nxt[good], W, H, s, prm.ransac_thresh_rad)
+        kept[good] = mk
+    else:
+        kept[good] = 1
+    mask = region_mask(W, H, prm.boundary_margin, prm.polar_ratio)
+    r = int(prm.min_dist)
+    for i in np.nonzero(kept)[0]:
+        cv_circle_fill(mask, int(np.rint(nxt[i, 0])), int(np.rint(nxt[i, 1])), r)
+    corners = oracle_lib.gftt(curr, mask, prm.max_corners, prm.quality, prm.min_dist)
+    return nxt, st, kept, corners
+
+
+def test_pipeline_bitwise(vio, gpu_ctx, pair):
+    a, b, _ = pair
+    pts0 = oracle_lib.gftt(a, region_mask(W, H), 300, float(np.float32(0.01)), 30.0)
+    rng = np.random.default_rng(2)
+    bad = np.stack([rng.uniform(30, 930, 20), rng.uniform(80, 400, 20)], -1).astype(np.float32)
+    pts = np.concatenate([pts0, bad])  # weak points: some fail LK / become RANSAC outliers
+    prm = vio.default_tracker_params(max_corners=300, seed=77)
+    klt = vio.default_klt_params()
+    t = vio.Tracker(gpu_ctx, W, H, max_points=1024, max_corners=1024)
+    t.upload(0, a)
+    t.upload(1, b)
+    t.set_points(pts)
+    t.run(prm, klt)
+    res = t.download()
+    st_ms = t.stage_ms()
+    t.close()
+    nxt, st, kept, corners = pipeline_oracle(vio, a, b, pts, prm, klt)
+    assert np.array_equal(res["status"], st)
+    assert np.array_equal(res["next"], nxt)
+    assert np.array_equal(res["kept"], kept)
+    assert kept.sum() > 200
+    assert np.array_equal(res["corners"], corners)
+    assert st_ms["total"] > 0
+
+
+def test_pipeline_full_size_config1(vio, gpu_ctx, synth):
+    """Config 1 at its BASELINE size (3840x1920, 300 corners): LK against the analytic flow, the
+    pipeline against the oracle composition."""
+    a, b, R21 = synth.config1()
+    Wf, Hf = 3840, 1920
+    pts = oracle_lib.gftt(a, region_mask(Wf, Hf), 300, float(np.float32(0.01)), 30.0)
+    assert len(pts) == 300
+    prm = vio.default_tracker_params(max_corners=300, seed=1)
+    klt = vio.default_klt_params()
+    t = vio.Tracker(gpu_ctx, Wf, Hf, max_points=512, max_corners=512)
+    t.upload(0, a)
+    t.upload(1, b)
+    t.set_points(pts)
+    t.run(prm, klt)
+    res = t.download()
+    t.close()
+    truth = synth.erp_flow_truth(pts, Wf, Hf, R21)
+    ok = res["status"] == 1
+    assert ok.mean() > 0.95
+    e = np.linalg.norm(res["next"] - truth, axis=1)[ok]
+    assert np.median(e) < 0.05
+    nxt, st, kept, corners = pipeline_oracle(vio, a, b, pts, prm, klt)
+    assert np.array_equal(res["next"], nxt) and np.array_equal(res["kept"], kept)
+    assert np.array_equal(res["corners"], corners)
