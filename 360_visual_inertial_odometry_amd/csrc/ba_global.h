@@ -1,0 +1,76 @@
+// ba_global.h — device argument block and launchers of the global-BA path (ba_global.hip), driven
+// by the host LM loop in ba_global_host.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vio360 {
+
+struct GbaArgs {
+    int K, L, N;
+    int P;            // free poses (pose blocks of the reduced system)
+    int nf, nfp;      // reduced size 6P and its 64-padded size
+    double cols, rows, huber, chi2_thr;
+    double Lw[4], info[4];
+    // inputs (landmark-sorted observations)
+    const double* pose_raw;   // [K][24] raw R_init t_init R_cb t_cb
+    const int* pose_f;        // [K] f-offset (6 * block) or -1
+    const int* pose_of_block; // [P] keyframe of pose block p
+    const uint8_t* lm_var;    // [L]
+    const uint8_t* lm_marg;   // [L]
+    const int* lm_ptr;        // [L+1]
+    const int* obs_kf;        // [N]
+    const int* obs_lm;        // [N]
+    const float* obs_uv;      // [N][2]
+    const int* kf_ptr;        // [K+1]
+    const int* kf_obs;        // [N]
+    // Schur contributions sorted by destination block (pa >= pb)
+    long long n_dest;
+    const int* dest_a;        // [n_dest]
+    const int* dest_b;
+    const int* dest_ptr;      // [n_dest+1]
+    const int* contrib_a;     // [n_contrib] observation indices
+    const int* contrib_b;
+    // state
+    double* pinit;            // [K][24]
+    double* pc;               // [K][36]
+    double* x_pose;           // [K][6]
+    double* x_lm;             // [L][3]
+    double* c_pose;
+    double* c_lm;
+    double* r;                // [2][N]
+    double* jp;               // [12][N]
+    double* jl;               // [6][N]
+    double* V;                // [6][L]
+    double* gl;               // [3][L]
+    double* sl;               // [3][L]
+    double* Vi;               // [6][L]
+    double* yl;               // [3][L]
+    double* U;                // [K][27]
+    double* gf;               // [nfp]
+    double* colsq_f;
+    double* sf;
+    double* Df;
+    double* bf;               // rhs (consumed by the forward substitution)
+    double* yv;               // forward result
+    double* xf;               // reduced-system solution
+    double* Wo;               // [N][18]
+    double* Yo;               // [N][18]
+    double* S;                // [nfp][nfp]
+    double* Linv;             // [nfp/64][64][64]
+};
+
+hipError_t gba_launch_setup(const GbaArgs& A, hipStream_t s);
+// mode 0 cost of active blocks, 1 + Jacobians, 2 cost of the constant blocks; out[0] = cost
+hipError_t gba_launch_eval(const GbaArgs& A, const double* xp, const double* xl, int mode, double* partial,
+                           double* out, hipStream_t s);
+hipError_t gba_launch_linearise(const GbaArgs& A, int first, double* partial, double* out_gmax, hipStream_t s);
+hipError_t gba_launch_step_prep(const GbaArgs& A, double radius, double* partial, double* out_bad, hipStream_t s);
+hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s);
+hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s);
+hipError_t gba_launch_backsub(const GbaArgs& A, double* partial, double* out_nonfinite, hipStream_t s);
+hipError_t gba_launch_model(const GbaArgs& A, double* partial, double* out3, hipStream_t s);
+hipError_t gba_launch_post(const GbaArgs& A, double* chi2, uint8_t* outl, uint8_t* bad, double* partial, double* out3,
+                           hipStream_t s);
+
+}  // namespace vio360

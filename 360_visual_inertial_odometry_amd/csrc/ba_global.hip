@@ -1,0 +1,734 @@
+// ba_global.hip — global bundle adjustment (config 5: 1000 KF x 50k landmarks) on MI355X.
+//
+// Same maths and Ceres-2.0 LM semantics as the windowed solver (ba_kernel.hip), for problems whose
+// reduced camera system no longer fits one workgroup (RunBA / RunFullBA over hundreds of keyframes,
+// src/optimization/Optimizer.cpp:304-491).  The LM control stays on the host (ba_global_host.cpp,
+// scalars only); every O(N_obs) / O(L) / O(n^2..n^3) step is a kernel here:
+//   gba_eval_kernel        BAFactor::Evaluate + Huber/Corrector, one lane per observation
+//   gba_lin_lm_kernel      per-landmark V = Jl^T Jl, g_l, Jacobi scale (schur_eliminator_impl.h)
+//   gba_lin_pose_kernel    per-pose U = Jp^T Jp, g_p (one wavefront per pose, shuffle reductions)
+//   gba_step_lm_kernel     V~ = sVs + D^2 and its inverse (3x3 LLT), per landmark
+//   gba_step_obs_kernel    W = (s Jp)^T (s Jl), Y = W V~^-1 per observation
+//   gba_schur_kernel       S = diag(sUs + D^2) - sum Y W^T, one wavefront per 6x6 destination block,
+//                          contributions pre-sorted by destination (deterministic, no atomics)
+//   chol_* kernels         blocked right-looking Cholesky of S (64x64 tiles): diagonal POTRF + inverse
+//                          in LDS, TRSM and the trailing SYRK/GEMM on v_mfma_f64_16x16x4_f64
+//   trsv kernels           blocked forward / backward substitution with the diagonal inverses
+//   gba_backsub_kernel     y_l = V~^-1 (g~_l - W^T y_p)
+//   gba_model_kernel       model cost change, step / parameter norms, candidate = x + s*(-y)
+// Reductions write per-block partials reduced in a fixed order: results are run-to-run bitwise stable.
+#include <float.h>
+#include <hip/hip_runtime.h>
+
+#include "ba_factor_dev.h"
+#include "ba_global.h"
+#include "lie_dev.h"
+
+namespace vio360 {
+
+constexpr int GT = 256;  // threads per block of the element-wise kernels
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    return v;
+}
+// block reduction (GT threads) of up to 4 values: lane 0 of the block returns them
+template <int NV>
+__device__ __forceinline__ void block_reduce_store(double* v, double* out, bool is_max) {
+    __shared__ double red[GT / 64][NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] = is_max ? wave_max_d(v[q]) : wave_sum_d(v[q]);
+    if ((threadIdx.x & 63) == 0)
+        for (int q = 0; q < NV; ++q) red[threadIdx.x >> 6][q] = v[q];
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int q = 0; q < NV; ++q) {
+            double r = red[0][q];
+            for (int w = 1; w < GT / 64; ++w) r = is_max ? fmax(r, red[w][q]) : r + red[w][q];
+            out[q] = r;
+        }
+}
+
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(GT) gba_setup_kernel(GbaArgs A) {
+    int k = blockIdx.x * GT + threadIdx.x;
+    if (k >= A.K) return;
+    const double* pr = A.pose_raw + 24 * k;
+    double* pi = A.pinit + 24 * k;
+    polar3(pr, pi);
+    for (int i = 0; i < 3; ++i) pi[9 + i] = pr[9 + i];
+    polar3(pr + 12, pi + 12);
+    for (int i = 0; i < 3; ++i) pi[21 + i] = pr[21 + i];
+}
+
+__global__ void __launch_bounds__(GT) gba_pose_cache_kernel(GbaArgs A, const double* xp) {
+    int k = blockIdx.x * GT + threadIdx.x;
+    if (k >= A.K) return;
+    pose_cache_one(A.pinit + 24 * k, xp + 6 * k, A.pc + 36 * k);
+}
+
+// cost (and Jacobians) at (pose cache, xl).  mode: 0 = active blocks, cost only; 1 = active blocks
+// with Jacobians; 2 = the fixed (all-constant) blocks, cost only.  partial[blockIdx] = sum.
+__global__ void __launch_bounds__(GT) gba_eval_kernel(GbaArgs A, const double* xl, int mode, double* partial) {
+    const int N = A.N;
+    int o = blockIdx.x * GT + threadIdx.x;
+    double cost = 0.0;
+    if (o < N) {
+        int k = A.obs_kf[o], l = A.obs_lm[o];
+        bool active = A.pose_f[k] >= 0 || A.lm_var[l];
+        if ((mode == 2) != active) {
+            const double* pc = A.pc + 36 * k;
+            double Pw[3] = {xl[3 * l], xl[3 * l + 1], xl[3 * l + 2]};
+            double r[2], Jp[12], Jl[6];
+            bool jz;
+            factor_eval(pc, A.pose_raw + 24 * k + 12, Pw, (double)A.obs_uv[2 * o], (double)A.obs_uv[2 * o + 1], A.cols,
+                        A.rows, A.Lw, false, false, mode == 1, r, Jp, Jl, jz);
+            double cst, sc;
+            huber(A.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
+            cost = cst;
+            if (mode == 1) {
+                A.r[o] = r[0] * sc;
+                A.r[N + o] = r[1] * sc;
+#pragma unroll
+                for (int i = 0; i < 12; ++i) A.jp[(size_t)i * N + o] = jz ? 0.0 : Jp[i] * sc;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) A.jl[(size_t)i * N + o] = jz ? 0.0 : Jl[i] * sc;
+            }
+        }
+    }
+    double v[1] = {cost};
+    block_reduce_store<1>(v, partial + blockIdx.x, false);
+}
+
+// fixed-order sum (or max) of n partials into out[0] — one block
+__global__ void __launch_bounds__(GT) gba_reduce_kernel(const double* partial, int n, double* out, int is_max) {
+    double acc = is_max ? 0.0 : 0.0;
+    for (int i = threadIdx.x; i < n; i += GT) acc = is_max ? fmax(acc, partial[i]) : acc + partial[i];
+    double v[1] = {acc};
+    block_reduce_store<1>(v, out, is_max != 0);
+}
+
+// per landmark: V (6 packed), g_l (3), s_l at the first linearisation; partial = max |g_l|
+__global__ void __launch_bounds__(GT) gba_lin_lm_kernel(GbaArgs A, int first, double* partial) {
+    const int N = A.N, L = A.L;
+    int l = blockIdx.x * GT + threadIdx.x;
+    double gm = 0.0;
+    if (l < L && A.lm_var[l]) {
+        double v[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+        for (int o = A.lm_ptr[l]; o < A.lm_ptr[l + 1]; ++o) {
+            double a0 = A.jl[o], a1 = A.jl[(size_t)N + o], a2 = A.jl[2 * (size_t)N + o];
+            double b0 = A.jl[3 * (size_t)N + o], b1 = A.jl[4 * (size_t)N + o], b2 = A.jl[5 * (size_t)N + o];
+            double ra = A.r[o], rb = A.r[N + o];
+            v[0] += a0 * a0 + b0 * b0; v[1] += a0 * a1 + b0 * b1; v[2] += a0 * a2 + b0 * b2;
+            v[3] += a1 * a1 + b1 * b1; v[4] += a1 * a2 + b1 * b2; v[5] += a2 * a2 + b2 * b2;
+            g[0] += a0 * ra + b0 * rb; g[1] += a1 * ra + b1 * rb; g[2] += a2 * ra + b2 * rb;
+        }
+        for (int i = 0; i < 6; ++i) A.V[(size_t)i * L + l] = v[i];
+        for (int i = 0; i < 3; ++i) A.gl[(size_t)i * L + l] = g[i];
+        gm = fmax(fabs(g[0]), fmax(fabs(g[1]), fabs(g[2])));
+        if (first) {
+            A.sl[l] = 1.0 / (1.0 + sqrt(v[0]));
+            A.sl[(size_t)L + l] = 1.0 / (1.0 + sqrt(v[3]));
+            A.sl[2 * (size_t)L + l] = 1.0 / (1.0 + sqrt(v[5]));
+        }
+    }
+    double vv[1] = {gm};
+    block_reduce_store<1>(vv, partial + blockIdx.x, true);
+}
+
+// per pose (one wavefront): U (21 packed upper) and g_p (6) into A.U[27k]; f-space gradient,
+// column norms, Jacobi scale; partial[blockIdx] = max |g_p|
+__global__ void __launch_bounds__(GT) gba_lin_pose_kernel(GbaArgs A, int first, double* partial) {
+    const int N = A.N;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int k = blockIdx.x * (GT / 64) + wid;
+    double gm = 0.0;
+    if (k < A.K && A.pose_f[k] >= 0) {
+        double acc[27];
+#pragma unroll
+        for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+        for (int q = A.kf_ptr[k] + lane; q < A.kf_ptr[k + 1]; q += 64) {
+            int o = A.kf_obs[q];
+            double a[6], b[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { a[i] = A.jp[(size_t)i * N + o]; b[i] = A.jp[(size_t)(6 + i) * N + o]; }
+            double ra = A.r[o], rb = A.r[N + o];
+            int idx = 0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int j = i; j < 6; ++j) acc[idx++] += a[i] * a[j] + b[i] * b[j];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) acc[21 + i] += a[i] * ra + b[i] * rb;
+        }
+#pragma unroll
+        for (int i = 0; i < 27; ++i) acc[i] = wave_sum_d(acc[i]);
+        if (lane < 27) {
+            double mine = 0.0;
+#pragma unroll
+            for (int i = 0; i < 27; ++i) mine = lane == i ? acc[i] : mine;
+            A.U[27 * k + lane] = mine;
+        }
+        const int pf = A.pose_f[k];
+        if (lane < 6) {
+            double g = 0.0, cs = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                g = lane == i ? acc[21 + i] : g;
+                int di = i * 6 - (i * (i - 1)) / 2;
+                cs = lane == i ? acc[di] : cs;
+            }
+            A.gf[pf + lane] = g;
+            A.colsq_f[pf + lane] = cs;
+            if (first) A.sf[pf + lane] = 1.0 / (1.0 + sqrt(cs));
+        }
+        for (int i = 0; i < 6; ++i) gm = fmax(gm, fabs(acc[21 + i]));
+    }
+    __shared__ double red[GT / 64];
+    if (lane == 0) red[wid] = gm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r = red[0];
+        for (int w = 1; w < GT / 64; ++w) r = fmax(r, red[w]);
+        partial[blockIdx.x] = r;
+    }
+}
+
+// V~ = s V s + D^2 (D^2 = clamp(diag(s V s))/radius), inverse by LLT; bad -> partial = 1
+__global__ void __launch_bounds__(GT) gba_step_lm_kernel(GbaArgs A, double radius, double* partial) {
+    const int L = A.L;
+    const double dmin = 1e-6, dmax = 1e32;
+    int l = blockIdx.x * GT + threadIdx.x;
+    double bad = 0.0;
+    if (l < L && A.lm_var[l]) {
+        double s0 = A.sl[l], s1 = A.sl[(size_t)L + l], s2 = A.sl[2 * (size_t)L + l];
+        double v[6];
+        for (int i = 0; i < 6; ++i) v[i] = A.V[(size_t)i * L + l];
+        double a00 = v[0] * s0 * s0, a01 = v[1] * s0 * s1, a02 = v[2] * s0 * s2;
+        double a11 = v[3] * s1 * s1, a12 = v[4] * s1 * s2, a22 = v[5] * s2 * s2;
+        a00 += fmin(fmax(a00, dmin), dmax) / radius;
+        a11 += fmin(fmax(a11, dmin), dmax) / radius;
+        a22 += fmin(fmax(a22, dmin), dmax) / radius;
+        if (!(a00 > 0.0)) bad = 1.0;
+        double l00 = sqrt(a00), l10 = a01 / l00, l20 = a02 / l00;
+        double t11 = a11 - l10 * l10;
+        if (!(t11 > 0.0)) bad = 1.0;
+        double l11 = sqrt(t11), l21 = (a12 - l20 * l10) / l11;
+        double t22 = a22 - l20 * l20 - l21 * l21;
+        if (!(t22 > 0.0)) bad = 1.0;
+        double l22 = sqrt(t22);
+        double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+        double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22;
+        double i20 = -(l20 * i00 + l21 * i10) * i22;
+        A.Vi[l] = i00 * i00 + i10 * i10 + i20 * i20;
+        A.Vi[(size_t)L + l] = i10 * i11 + i20 * i21;
+        A.Vi[2 * (size_t)L + l] = i20 * i22;
+        A.Vi[3 * (size_t)L + l] = i11 * i11 + i21 * i21;
+        A.Vi[4 * (size_t)L + l] = i21 * i22;
+        A.Vi[5 * (size_t)L + l] = i22 * i22;
+    }
+    double v1[1] = {bad};
+    block_reduce_store<1>(v1, partial + blockIdx.x, true);
+}
+
+// f-space LM diagonal and rhs, padding rows of the reduced system
+__global__ void __launch_bounds__(GT) gba_step_f_kernel(GbaArgs A, double radius) {
+    int f = blockIdx.x * GT + threadIdx.x;
+    if (f >= A.nfp) return;
+    if (f < A.nf) {
+        double d = A.colsq_f[f] * A.sf[f] * A.sf[f];
+        d = fmin(fmax(d, 1e-6), 1e32);
+        A.Df[f] = sqrt(d / radius);
+        A.bf[f] = A.sf[f] * A.gf[f];
+    } else {
+        A.Df[f] = 0.0;
+        A.bf[f] = 0.0;
+    }
+}
+
+// per observation: W = (s_p Jp)^T (s_l Jl) (6x3, row-major) and Y = W V~^-1
+__global__ void __launch_bounds__(GT) gba_step_obs_kernel(GbaArgs A) {
+    const int N = A.N, L = A.L;
+    int o = blockIdx.x * GT + threadIdx.x;
+    if (o >= N) return;
+    int k = A.obs_kf[o], l = A.obs_lm[o];
+    int pf = A.pose_f[k];
+    if (pf < 0 || !A.lm_var[l]) return;
+    double s0 = A.sl[l], s1 = A.sl[(size_t)L + l], s2 = A.sl[2 * (size_t)L + l];
+    double vi[6];
+    for (int i = 0; i < 6; ++i) vi[i] = A.Vi[(size_t)i * L + l];
+    double b0 = A.jl[o] * s0, b1 = A.jl[(size_t)N + o] * s1, b2 = A.jl[2 * (size_t)N + o] * s2;
+    double d0 = A.jl[3 * (size_t)N + o] * s0, d1 = A.jl[4 * (size_t)N + o] * s1, d2 = A.jl[5 * (size_t)N + o] * s2;
+    double* W = A.Wo + 18 * (size_t)o;
+    double* Y = A.Yo + 18 * (size_t)o;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double sp = A.sf[pf + i];
+        double a = A.jp[(size_t)i * N + o] * sp, e = A.jp[(size_t)(6 + i) * N + o] * sp;
+        double W0 = a * b0 + e * d0, W1 = a * b1 + e * d1, W2 = a * b2 + e * d2;
+        W[3 * i] = W0; W[3 * i + 1] = W1; W[3 * i + 2] = W2;
+        Y[3 * i] = W0 * vi[0] + W1 * vi[1] + W2 * vi[2];
+        Y[3 * i + 1] = W0 * vi[1] + W1 * vi[3] + W2 * vi[4];
+        Y[3 * i + 2] = W0 * vi[2] + W1 * vi[4] + W2 * vi[5];
+    }
+}
+
+// S lower triangle, one wavefront per 6x6 destination block (pa >= pb pose blocks):
+//   S[pa,pb] = [pa == pb] (s U s + D^2) - sum over co-observations Y_oa W_ob^T
+__global__ void __launch_bounds__(GT) gba_schur_kernel(GbaArgs A) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long d = (long long)blockIdx.x * (GT / 64) + wid;
+    if (d >= A.n_dest) return;
+    const int pa = A.dest_a[d], pb = A.dest_b[d];
+    if (lane >= 36) return;
+    const int i = lane / 6, j = lane % 6;
+    double acc = 0.0;
+    for (int c = A.dest_ptr[d]; c < A.dest_ptr[d + 1]; ++c) {
+        const double* Y = A.Yo + 18 * (size_t)A.contrib_a[c] + 3 * i;
+        const double* W = A.Wo + 18 * (size_t)A.contrib_b[c] + 3 * j;
+        acc += Y[0] * W[0] + Y[1] * W[1] + Y[2] * W[2];
+    }
+    const int fa = 6 * pa + i, fb = 6 * pb + j;
+    double v = -acc;
+    if (pa == pb) {
+        const int k = A.pose_of_block[pa];
+        int a = min(i, j), b = max(i, j);
+        int idx = a * 6 - (a * (a - 1)) / 2 + (b - a);
+        v += A.U[27 * k + idx] * A.sf[fa] * A.sf[fb];
+        if (i == j) v += A.Df[fa] * A.Df[fa];
+    }
+    A.S[(size_t)fa * A.nfp + fb] = v;
+}
+
+// padding rows/cols [nf, nfp) of S: identity
+__global__ void __launch_bounds__(GT) gba_pad_kernel(GbaArgs A) {
+    const int pad = A.nfp - A.nf;
+    int e = blockIdx.x * GT + threadIdx.x;
+    if (e >= pad * A.nfp) return;
+    int r = A.nf + e / A.nfp, c = e % A.nfp;
+    A.S[(size_t)r * A.nfp + c] = (r == c) ? 1.0 : 0.0;
+}
+
+// rhs: b_p -= sum_{o in obs(p)} Y_o g~_l(o)   (one wavefront per pose)
+__global__ void __launch_bounds__(GT) gba_rhs_kernel(GbaArgs A) {
+    const int L = A.L;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int k = blockIdx.x * (GT / 64) + wid;
+    if (k >= A.K || A.pose_f[k] < 0) return;
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int q = A.kf_ptr[k] + lane; q < A.kf_ptr[k + 1]; q += 64) {
+        int o = A.kf_obs[q], l = A.obs_lm[o];
+        if (!A.lm_var[l]) continue;
+        double g0 = A.gl[l] * A.sl[l], g1 = A.gl[(size_t)L + l] * A.sl[(size_t)L + l];
+        double g2 = A.gl[2 * (size_t)L + l] * A.sl[2 * (size_t)L + l];
+        const double* Y = A.Yo + 18 * (size_t)o;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc[i] += Y[3 * i] * g0 + Y[3 * i + 1] * g1 + Y[3 * i + 2] * g2;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) acc[i] = wave_sum_d(acc[i]);
+    if (lane < 6) {
+        double mine = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) mine = lane == i ? acc[i] : mine;
+        A.bf[A.pose_f[k] + lane] -= mine;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Blocked Cholesky, NB = 64.  Lower triangle of S (row-major, leading dimension n).
+constexpr int NB = 64;
+using d4 = __attribute__((ext_vector_type(4))) double;
+
+// diagonal block: in-LDS right-looking Cholesky + lower-triangular inverse (for TRSM / TRSV)
+__global__ void __launch_bounds__(256) chol_diag_kernel(double* S, int n, int k, double* Linv, int* fail) {
+    __shared__ double T[NB][NB + 1];
+    __shared__ double Iv[NB][NB + 1];
+    __shared__ int bad;
+    double* blk = S + (size_t)k * NB * n + (size_t)k * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += 256) {
+        int r = e / NB, c = e % NB;
+        T[r][c] = c <= r ? blk[(size_t)r * n + c] : 0.0;
+    }
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    for (int j = 0; j < NB; ++j) {
+        double d = T[j][j];
+        if (!(d > 0.0)) { if (threadIdx.x == 0) bad = 1; }
+        __syncthreads();
+        if (bad) break;
+        double sd = sqrt(d);
+        // column j below the diagonal, then the trailing update
+        for (int r = j + 1 + threadIdx.x; r < NB; r += 256) T[r][j] /= sd;
+        __syncthreads();
+        if (threadIdx.x == 0) T[j][j] = sd;
+        for (int e = threadIdx.x; e < (NB - j - 1) * (NB - j - 1); e += 256) {
+            int r = j + 1 + e / (NB - j - 1), c = j + 1 + e % (NB - j - 1);
+            if (c <= r) T[r][c] -= T[r][j] * T[c][j];
+        }
+        __syncthreads();
+    }
+    if (bad) {
+        if (threadIdx.x == 0) *fail = 1;
+        return;
+    }
+    // inverse of the lower-triangular T: column c solves T x = e_c (one thread per column)
+    for (int c = threadIdx.x; c < NB; c += 256) {
+        for (int r = 0; r < NB; ++r) {
+            double s = (r == c) ? 1.0 : 0.0;
+            for (int q = c; q < r; ++q) s -= T[r][q] * Iv[q][c];
+            Iv[r][c] = r < c ? 0.0 : s / T[r][r];
+        }
+    }
+    __syncthreads();
+    double* Li = Linv + (size_t)k * NB * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += 256) {
+        int r = e / NB, c = e % NB;
+        if (c <= r) blk[(size_t)r * n + c] = T[r][c];
+        Li[e] = Iv[r][c];
+    }
+}
+
+// 64x64x64 tile product on MFMA f64: acc(wave's 32x32) += A(64xK) * B(64xK)^T from LDS
+// wave w: rows 32*(w>>1) .. +32, cols 32*(w&1) .. +32 ; 2x2 MFMA 16x16 tiles
+__device__ __forceinline__ void mfma_tile_ABt(const double (*As)[NB + 1], const double (*Bs)[NB + 1], d4 acc[2][2],
+                                              int wid, int lane) {
+    const int r0 = 32 * (wid >> 1), c0 = 32 * (wid & 1);
+    const int li = lane & 15, lk = lane >> 4;
+    for (int kk = 0; kk < NB; kk += 4) {
+        double a[2], b[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            a[t] = As[r0 + 16 * t + li][kk + lk];   // A[i][k]
+            b[t] = Bs[c0 + 16 * t + li][kk + lk];   // B^T[k][j] = B[j][k]
+        }
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[ti][tj], 0, 0, 0);
+    }
+}
+
+// panel: A_ik <- A_ik * Linv_kk^T for every block row i > k
+__global__ void __launch_bounds__(256) chol_trsm_kernel(double* S, int n, int k, const double* Linv) {
+    __shared__ double As[NB][NB + 1];
+    __shared__ double Bs[NB][NB + 1];
+    const int i = k + 1 + blockIdx.x;
+    double* blk = S + (size_t)i * NB * n + (size_t)k * NB;
+    const double* Li = Linv + (size_t)k * NB * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += 256) {
+        int r = e / NB, c = e % NB;
+        As[r][c] = blk[(size_t)r * n + c];
+        Bs[r][c] = Li[e];
+    }
+    __syncthreads();
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    d4 acc[2][2];
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0, 0, 0, 0};
+    mfma_tile_ABt(As, Bs, acc, wid, lane);
+    const int r0 = 32 * (wid >> 1), c0 = 32 * (wid & 1);
+    for (int ti = 0; ti < 2; ++ti)
+        for (int tj = 0; tj < 2; ++tj)
+            for (int q = 0; q < 4; ++q) {
+                int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                blk[(size_t)r * n + c] = acc[ti][tj][q];
+            }
+}
+
+// trailing update: A_ij -= A_ik A_jk^T for k < j <= i (lower block triangle), one tile per block
+__global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k, int nblk) {
+    __shared__ double As[NB][NB + 1];
+    __shared__ double Bs[NB][NB + 1];
+    // blockIdx.x -> (i, j) with 0 <= jj <= ii < m, i = k+1+ii, j = k+1+jj
+    const long long t = blockIdx.x;
+    int ii = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+    while ((long long)(ii + 1) * (ii + 2) / 2 <= t) ++ii;
+    while ((long long)ii * (ii + 1) / 2 > t) --ii;
+    const int jj = (int)(t - (long long)ii * (ii + 1) / 2);
+    const int i = k + 1 + ii, j = k + 1 + jj;
+    const double* Aik = S + (size_t)i * NB * n + (size_t)k * NB;
+    const double* Ajk = S + (size_t)j * NB * n + (size_t)k * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += 256) {
+        int r = e / NB, c = e % NB;
+        As[r][c] = Aik[(size_t)r * n + c];
+        Bs[r][c] = Ajk[(size_t)r * n + c];
+    }
+    __syncthreads();
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    d4 acc[2][2];
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0, 0, 0, 0};
+    mfma_tile_ABt(As, Bs, acc, wid, lane);
+    double* C = S + (size_t)i * NB * n + (size_t)j * NB;
+    const int r0 = 32 * (wid >> 1), c0 = 32 * (wid & 1);
+    for (int ti = 0; ti < 2; ++ti)
+        for (int tj = 0; tj < 2; ++tj)
+            for (int q = 0; q < 4; ++q) {
+                int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                if (i != j || c <= r) C[(size_t)r * n + c] -= acc[ti][tj][q];
+            }
+}
+
+// forward substitution step k: y_k = Linv_kk b_k (every block recomputes it from the final b_k;
+// block 0 publishes it), b_i -= L_ik y_k for the rows below
+__global__ void __launch_bounds__(256) trsv_fwd_kernel(const double* S, int n, int k, const double* Linv, double* b,
+                                                       double* y) {
+    __shared__ double yk[NB];
+    const double* Li = Linv + (size_t)k * NB * NB;
+    if (threadIdx.x < NB) {
+        double s = 0.0;
+        for (int q = 0; q <= (int)threadIdx.x; ++q) s += Li[threadIdx.x * NB + q] * b[k * NB + q];
+        yk[threadIdx.x] = s;
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < NB) y[k * NB + threadIdx.x] = yk[threadIdx.x];
+    int r = (k + 1) * NB + blockIdx.x * 256 + threadIdx.x;
+    if (r < n) {
+        const double* row = S + (size_t)r * n + (size_t)k * NB;
+        double s = 0.0;
+        for (int q = 0; q < NB; ++q) s += row[q] * yk[q];
+        b[r] -= s;
+    }
+}
+
+// backward substitution step k (k = nblk-1 .. 0): x_k = Linv_kk^T y_k, y_j -= L_kj^T x_k for j < k
+__global__ void __launch_bounds__(256) trsv_bwd_kernel(const double* S, int n, int k, const double* Linv, double* y,
+                                                       double* x) {
+    __shared__ double xk[NB];
+    const double* Li = Linv + (size_t)k * NB * NB;
+    if (threadIdx.x < NB) {
+        double s = 0.0;
+        for (int q = threadIdx.x; q < NB; ++q) s += Li[q * NB + threadIdx.x] * y[k * NB + q];
+        xk[threadIdx.x] = s;
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < NB) x[k * NB + threadIdx.x] = xk[threadIdx.x];
+    int c = blockIdx.x * 256 + threadIdx.x;  // column c < k*NB of row-block k
+    if (c < k * NB) {
+        double s = 0.0;
+        for (int q = 0; q < NB; ++q) s += S[(size_t)(k * NB + q) * n + c] * xk[q];
+        y[c] -= s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// landmark back-substitution y_l = V~^-1 (g~_l - sum W^T y_p); partial = non-finite flag
+__global__ void __launch_bounds__(GT) gba_backsub_kernel(GbaArgs A, double* partial) {
+    const int L = A.L;
+    int l = blockIdx.x * GT + threadIdx.x;
+    double fin = 0.0;
+    if (l < L && A.lm_var[l]) {
+        double s[3] = {A.sl[l], A.sl[(size_t)L + l], A.sl[2 * (size_t)L + l]};
+        double rhs[3];
+        for (int c = 0; c < 3; ++c) rhs[c] = A.gl[(size_t)c * L + l] * s[c];
+        for (int o = A.lm_ptr[l]; o < A.lm_ptr[l + 1]; ++o) {
+            int pf = A.pose_f[A.obs_kf[o]];
+            if (pf < 0) continue;
+            const double* W = A.Wo + 18 * (size_t)o;
+            for (int c = 0; c < 3; ++c) {
+                double w = 0.0;
+                for (int i = 0; i < 6; ++i) w += W[3 * i + c] * A.xf[pf + i];
+                rhs[c] -= w;
+            }
+        }
+        double vi[6];
+        for (int i = 0; i < 6; ++i) vi[i] = A.Vi[(size_t)i * L + l];
+        double y0 = vi[0] * rhs[0] + vi[1] * rhs[1] + vi[2] * rhs[2];
+        double y1 = vi[1] * rhs[0] + vi[3] * rhs[1] + vi[4] * rhs[2];
+        double y2 = vi[2] * rhs[0] + vi[4] * rhs[1] + vi[5] * rhs[2];
+        A.yl[l] = y0; A.yl[(size_t)L + l] = y1; A.yl[2 * (size_t)L + l] = y2;
+        if (!isfinite(y0) || !isfinite(y1) || !isfinite(y2)) fin = 1.0;
+    }
+    int f = blockIdx.x * GT + threadIdx.x;
+    if (f < A.nf && !isfinite(A.xf[f])) fin = 1.0;
+    double v[1] = {fin};
+    block_reduce_store<1>(v, partial + blockIdx.x, true);
+}
+
+// per observation model change; candidate poses/points and step norms.
+// partial[3*block + {0,1,2}] = model change, |x - cand|^2, |cand|^2
+__global__ void __launch_bounds__(GT) gba_model_kernel(GbaArgs A, double* partial) {
+    const int N = A.N, L = A.L, K = A.K;
+    int t = blockIdx.x * GT + threadIdx.x;
+    double mc = 0.0, sn = 0.0, xn = 0.0;
+    if (t < N) {
+        int o = t;
+        int k = A.obs_kf[o], l = A.obs_lm[o];
+        int pf = A.pose_f[k];
+        bool lv = A.lm_var[l];
+        if (pf >= 0 || lv) {
+            double m0 = 0, m1 = 0;
+            if (pf >= 0)
+                for (int i = 0; i < 6; ++i) {
+                    double d = -A.xf[pf + i] * A.sf[pf + i];
+                    m0 += A.jp[(size_t)i * N + o] * d;
+                    m1 += A.jp[(size_t)(6 + i) * N + o] * d;
+                }
+            if (lv)
+                for (int c = 0; c < 3; ++c) {
+                    double d = -A.yl[(size_t)c * L + l] * A.sl[(size_t)c * L + l];
+                    m0 += A.jl[(size_t)c * N + o] * d;
+                    m1 += A.jl[(size_t)(3 + c) * N + o] * d;
+                }
+            mc -= m0 * (A.r[o] + m0 / 2.0) + m1 * (A.r[N + o] + m1 / 2.0);
+        }
+    }
+    if (t < 6 * K) {
+        int k = t / 6, i = t % 6;
+        int pf = A.pose_f[k];
+        double x = A.x_pose[t];
+        double c = pf >= 0 ? x + (-A.xf[pf + i] * A.sf[pf + i]) : x;
+        A.c_pose[t] = c;
+        if (pf >= 0) { double d = x - c; sn += d * d; xn += c * c; }
+    }
+    if (t < 3 * L) {
+        int l = t / 3, c = t % 3;
+        double x = A.x_lm[t];
+        double cnd = A.lm_var[l] ? x + (-A.yl[(size_t)c * L + l] * A.sl[(size_t)c * L + l]) : x;
+        A.c_lm[t] = cnd;
+        if (A.lm_var[l]) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
+    }
+    double v[3] = {mc, sn, xn};
+    __shared__ double out3[3];
+    block_reduce_store<3>(v, out3, false);
+    if (threadIdx.x == 0) {
+        partial[3 * blockIdx.x] = out3[0];
+        partial[3 * blockIdx.x + 1] = out3[1];
+        partial[3 * blockIdx.x + 2] = out3[2];
+    }
+}
+
+// fixed-order reduction of strided partials: out[q] = sum_i partial[stride*i + q]
+__global__ void __launch_bounds__(GT) gba_reduce3_kernel(const double* partial, int n, double* out) {
+    double a[3] = {0, 0, 0};
+    for (int i = threadIdx.x; i < n; i += GT)
+        for (int q = 0; q < 3; ++q) a[q] += partial[3 * i + q];
+    block_reduce_store<3>(a, out, false);
+}
+
+// chi^2 + outlier flags + bad landmarks at the final point (Optimizer.cpp:415-456, 888-928)
+__global__ void __launch_bounds__(GT) gba_post_kernel(GbaArgs A, double* chi2, uint8_t* outl, uint8_t* bad,
+                                                      double* partial) {
+    int l = blockIdx.x * GT + threadIdx.x;
+    double cin = 0, cout_ = 0, cbad = 0;
+    if (l < A.L) {
+        int li = 0, lo = 0;
+        for (int o = A.lm_ptr[l]; o < A.lm_ptr[l + 1]; ++o) {
+            int k = A.obs_kf[o];
+            double Pw[3] = {A.x_lm[3 * l], A.x_lm[3 * l + 1], A.x_lm[3 * l + 2]};
+            double ch = factor_chi2(A.pc + 36 * k, Pw, (double)A.obs_uv[2 * o], (double)A.obs_uv[2 * o + 1], A.cols,
+                                    A.rows, A.info, false, false);
+            bool is_out = ch > A.chi2_thr;
+            chi2[o] = ch;
+            outl[o] = is_out;
+            if (is_out) lo++; else li++;
+        }
+        bool b = !A.lm_marg[l] && li == 0 && lo >= 2;
+        bad[l] = b;
+        cin = li; cout_ = lo; cbad = b;
+    }
+    double v[3] = {cin, cout_, cbad};
+    __shared__ double out3[3];
+    block_reduce_store<3>(v, out3, false);
+    if (threadIdx.x == 0) {
+        partial[3 * blockIdx.x] = out3[0];
+        partial[3 * blockIdx.x + 1] = out3[1];
+        partial[3 * blockIdx.x + 2] = out3[2];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers (host-callable)
+static inline dim3 g1(long long n) { return dim3((unsigned)((n + GT - 1) / GT)); }
+
+hipError_t gba_launch_setup(const GbaArgs& A, hipStream_t s) {
+    hipLaunchKernelGGL(gba_setup_kernel, g1(A.K), dim3(GT), 0, s, A);
+    return hipGetLastError();
+}
+hipError_t gba_launch_eval(const GbaArgs& A, const double* xp, const double* xl, int mode, double* partial,
+                           double* out, hipStream_t s) {
+    hipLaunchKernelGGL(gba_pose_cache_kernel, g1(A.K), dim3(GT), 0, s, A, xp);
+    hipLaunchKernelGGL(gba_eval_kernel, g1(A.N), dim3(GT), 0, s, A, xl, mode, partial);
+    hipLaunchKernelGGL(gba_reduce_kernel, dim3(1), dim3(GT), 0, s, (const double*)partial, (int)g1(A.N).x, out, 0);
+    return hipGetLastError();
+}
+hipError_t gba_launch_linearise(const GbaArgs& A, int first, double* partial, double* out_gmax, hipStream_t s) {
+    const int nbl = (int)g1(A.L).x;
+    const int nbp = (A.K + GT / 64 - 1) / (GT / 64);
+    hipLaunchKernelGGL(gba_lin_lm_kernel, dim3(nbl), dim3(GT), 0, s, A, first, partial);
+    hipLaunchKernelGGL(gba_lin_pose_kernel, dim3(nbp), dim3(GT), 0, s, A, first, partial + nbl);
+    hipLaunchKernelGGL(gba_reduce_kernel, dim3(1), dim3(GT), 0, s, (const double*)partial, nbl + nbp, out_gmax, 1);
+    return hipGetLastError();
+}
+hipError_t gba_launch_step_prep(const GbaArgs& A, double radius, double* partial, double* out_bad, hipStream_t s) {
+    const int nbl = (int)g1(A.L).x;
+    hipLaunchKernelGGL(gba_step_lm_kernel, dim3(nbl), dim3(GT), 0, s, A, radius, partial);
+    hipLaunchKernelGGL(gba_reduce_kernel, dim3(1), dim3(GT), 0, s, (const double*)partial, nbl, out_bad, 1);
+    hipLaunchKernelGGL(gba_step_f_kernel, g1(A.nfp), dim3(GT), 0, s, A, radius);
+    hipLaunchKernelGGL(gba_step_obs_kernel, g1(A.N), dim3(GT), 0, s, A);
+    if (A.n_dest > 0)
+        hipLaunchKernelGGL(gba_schur_kernel, dim3((unsigned)((A.n_dest + GT / 64 - 1) / (GT / 64))), dim3(GT), 0, s, A);
+    if (A.nfp > A.nf)
+        hipLaunchKernelGGL(gba_pad_kernel, g1((long long)(A.nfp - A.nf) * A.nfp), dim3(GT), 0, s, A);
+    hipLaunchKernelGGL(gba_rhs_kernel, dim3((A.K + GT / 64 - 1) / (GT / 64)), dim3(GT), 0, s, A);
+    return hipGetLastError();
+}
+hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
+    const int n = A.nfp, nblk = n / NB;
+    for (int k = 0; k < nblk; ++k) {
+        hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, A.S, n, k, A.Linv, fail);
+        const int m = nblk - k - 1;
+        if (m > 0) {
+            hipLaunchKernelGGL(chol_trsm_kernel, dim3(m), dim3(256), 0, s, A.S, n, k, (const double*)A.Linv);
+            hipLaunchKernelGGL(chol_syrk_kernel, dim3((unsigned)((long long)m * (m + 1) / 2)), dim3(256), 0, s, A.S, n,
+                               k, nblk);
+        }
+    }
+    return hipGetLastError();
+}
+hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {
+    const int n = A.nfp, nblk = n / NB;
+    for (int k = 0; k < nblk; ++k) {
+        int rows = n - (k + 1) * NB;
+        int nb = rows > 0 ? (rows + 255) / 256 : 1;
+        hipLaunchKernelGGL(trsv_fwd_kernel, dim3(nb), dim3(256), 0, s, (const double*)A.S, n, k,
+                           (const double*)A.Linv, A.bf, A.yv);
+    }
+    for (int k = nblk - 1; k >= 0; --k) {
+        int cols = k * NB;
+        int nb = cols > 0 ? (cols + 255) / 256 : 1;
+        hipLaunchKernelGGL(trsv_bwd_kernel, dim3(nb), dim3(256), 0, s, (const double*)A.S, n, k,
+                           (const double*)A.Linv, A.yv, A.xf);
+    }
+    return hipGetLastError();
+}
+hipError_t gba_launch_backsub(const GbaArgs& A, double* partial, double* out_nonfinite, hipStream_t s) {
+    const int nb = (int)g1(std::max(A.L, A.nf)).x;
+    hipLaunchKernelGGL(gba_backsub_kernel, dim3(nb), dim3(GT), 0, s, A, partial);
+    hipLaunchKernelGGL(gba_reduce_kernel, dim3(1), dim3(GT), 0, s, (const double*)partial, nb, out_nonfinite, 1);
+    return hipGetLastError();
+}
+hipError_t gba_launch_model(const GbaArgs& A, double* partial, double* out3, hipStream_t s) {
+    long long m = std::max((long long)A.N, std::max(6LL * A.K, 3LL * A.L));
+    const int nb = (int)g1(m).x;
+    hipLaunchKernelGGL(gba_model_kernel, dim3(nb), dim3(GT), 0, s, A, partial);
+    hipLaunchKernelGGL(gba_reduce3_kernel, dim3(1), dim3(GT), 0, s, (const double*)partial, nb, out3);
+    return hipGetLastError();
+}
+hipError_t gba_launch_post(const GbaArgs& A, double* chi2, uint8_t* outl, uint8_t* bad, double* partial, double* out3,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(gba_pose_cache_kernel, g1(A.K), dim3(GT), 0, s, A, (const double*)A.x_pose);
+    const int nb = (int)g1(A.L).x;
+    hipLaunchKernelGGL(gba_post_kernel, dim3(nb), dim3(GT), 0, s, A, chi2, outl, bad, partial);
+    hipLaunchKernelGGL(gba_reduce3_kernel, dim3(1), dim3(GT), 0, s, (const double*)partial, nb, out3);
+    return hipGetLastError();
+}
+
+}  // namespace vio360

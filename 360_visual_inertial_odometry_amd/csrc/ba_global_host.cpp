@@ -1,0 +1,360 @@
+// ba_global_host.cpp — host LM driver of the global-BA path (problems beyond one workgroup:
+// config 5, 1000 keyframes x 50k landmarks).  The control flow is Ceres 2.0's
+// TrustRegionMinimizer + LevenbergMarquardtStrategy exactly as restated in oracle/ba_oracle.c
+// (oracle_lm_minimize: trust_region_minimizer.cc:67-826, levenberg_marquardt_strategy.cc:66-160);
+// every array operation runs on the GPU (ba_global.hip) and only scalars come back.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "ba_global.h"
+#include "ba_types.h"
+#include "ctx.h"
+
+namespace vio360 {
+
+namespace {
+
+struct DevBufs {
+    std::vector<void*> ptrs;
+    vio_ctx* ctx;
+    ~DevBufs() {
+        for (void* p : ptrs) (void)hipFree(p);
+    }
+    template <class T>
+    int alloc(T** p, size_t n) {
+        void* q = nullptr;
+        if (hipMalloc(&q, std::max<size_t>(n * sizeof(T), 64)) != hipSuccess) {
+            set_error(ctx, "hipMalloc failed (global BA)");
+            return VIO_ENOMEM;
+        }
+        ptrs.push_back(q);
+        *p = (T*)q;
+        return VIO_OK;
+    }
+    template <class T>
+    int upload(T** p, const std::vector<T>& v) {
+        int rc = alloc(p, v.size());
+        if (rc) return rc;
+        if (!v.empty() && hipMemcpy((void*)*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) {
+            set_error(ctx, "hipMemcpy failed (global BA)");
+            return VIO_EDEVICE;
+        }
+        return VIO_OK;
+    }
+};
+
+#define GBA_CHECK(expr)                                            \
+    do {                                                           \
+        hipError_t _e = (expr);                                    \
+        if (_e != hipSuccess) return hip_fail(ctx, _e, #expr);     \
+    } while (0)
+
+}  // namespace
+
+bool global_ba_applicable(const vio_ba_problem& p) {
+    return (p.variant == VIO_BA_LOCAL || p.variant == VIO_BA_FULL) && p.num_kf > BA_KMAX;
+}
+
+int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
+    const int K = p.num_kf, L = p.num_lm, N = p.num_obs;
+    if (K <= 0 || L < 0 || N < 0 || !p.T_cb || !p.T_wb_init || !p.kf_const || (L && (!p.lm_const || !p.lm_xyz)) ||
+        (N && (!p.obs_kf || !p.obs_lm || !p.obs_uv))) {
+        set_error(ctx, "invalid global BA problem");
+        return VIO_EINVAL;
+    }
+    for (int o = 0; o < N; ++o)
+        if (p.obs_kf[o] < 0 || p.obs_kf[o] >= K || p.obs_lm[o] < 0 || p.obs_lm[o] >= L) {
+            set_error(ctx, "observation index out of range");
+            return VIO_EINVAL;
+        }
+    {
+        std::vector<int64_t> key(N);
+        for (int o = 0; o < N; ++o) key[o] = (int64_t)p.obs_lm[o] * K + p.obs_kf[o];
+        std::sort(key.begin(), key.end());
+        for (int o = 1; o < N; ++o)
+            if (key[o] == key[o - 1]) { set_error(ctx, "duplicate (keyframe, landmark) observation"); return VIO_EINVAL; }
+    }
+    (void)hipSetDevice(ctx->device);
+    hipStream_t st = ctx->stream;
+    // ---- reduced problem (Ceres RemoveFixedBlocks; points are the e-blocks) ----
+    std::vector<uint8_t> pose_used(K, 0), lm_used(L, 0), active(N, 0);
+    for (int o = 0; o < N; ++o) {
+        int k = p.obs_kf[o], l = p.obs_lm[o];
+        bool kv = !p.kf_const[k], lv = !p.lm_const[l];
+        if (kv) pose_used[k] = 1;
+        if (lv) lm_used[l] = 1;
+        active[o] = kv || lv;
+    }
+    std::vector<int> pose_f(K, -1), pose_of_block;
+    for (int k = 0; k < K; ++k)
+        if (pose_used[k]) { pose_f[k] = 6 * (int)pose_of_block.size(); pose_of_block.push_back(k); }
+    const int P = (int)pose_of_block.size();
+    const int nf = 6 * P;
+    const int nfp = std::max(64, (nf + 63) / 64 * 64);
+    int n_free = nf;
+    for (int l = 0; l < L; ++l) n_free += 3 * lm_used[l];
+    // landmark-sorted observations
+    std::vector<int> perm(N);
+    for (int o = 0; o < N; ++o) perm[o] = o;
+    std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return p.obs_lm[a] < p.obs_lm[b]; });
+    std::vector<int> lm_ptr(L + 1, 0), okf(N), olm(N), kf_ptr(K + 1, 0), kf_obs(N);
+    std::vector<float> ouv(2 * (size_t)N);
+    for (int o = 0; o < N; ++o) lm_ptr[p.obs_lm[o] + 1]++;
+    for (int l = 0; l < L; ++l) lm_ptr[l + 1] += lm_ptr[l];
+    for (int q = 0; q < N; ++q) {
+        int o = perm[q];
+        okf[q] = p.obs_kf[o]; olm[q] = p.obs_lm[o];
+        ouv[2 * q] = p.obs_uv[2 * o]; ouv[2 * q + 1] = p.obs_uv[2 * o + 1];
+        kf_ptr[okf[q] + 1]++;
+    }
+    for (int k = 0; k < K; ++k) kf_ptr[k + 1] += kf_ptr[k];
+    {
+        std::vector<int> fill(K, 0);
+        for (int q = 0; q < N; ++q) kf_obs[kf_ptr[okf[q]] + fill[okf[q]]++] = q;
+    }
+    // Schur contributions by destination block (pa >= pb), landmark order inside a destination
+    const long long n_dest = (long long)P * (P + 1) / 2;
+    std::vector<int> dest_cnt(n_dest + 1, 0);
+    auto dest_of = [](int a, int b) { return (long long)a * (a + 1) / 2 + b; };
+    for (int l = 0; l < L; ++l) {
+        if (!lm_used[l]) continue;
+        for (int qa = lm_ptr[l]; qa < lm_ptr[l + 1]; ++qa) {
+            int fa = pose_f[okf[qa]];
+            if (fa < 0) continue;
+            for (int qb = lm_ptr[l]; qb < lm_ptr[l + 1]; ++qb) {
+                int fb = pose_f[okf[qb]];
+                if (fb < 0 || fb > fa) continue;
+                dest_cnt[dest_of(fa / 6, fb / 6) + 1]++;
+            }
+        }
+    }
+    for (long long d = 0; d < n_dest; ++d) dest_cnt[d + 1] += dest_cnt[d];
+    const long long n_contrib = dest_cnt[n_dest];
+    if (n_contrib > INT32_MAX) { set_error(ctx, "too many Schur contributions"); return VIO_ENOSYS; }
+    std::vector<int> ca(n_contrib), cb(n_contrib), dfill(dest_cnt.begin(), dest_cnt.end() - 1);
+    for (int l = 0; l < L; ++l) {
+        if (!lm_used[l]) continue;
+        for (int qa = lm_ptr[l]; qa < lm_ptr[l + 1]; ++qa) {
+            int fa = pose_f[okf[qa]];
+            if (fa < 0) continue;
+            for (int qb = lm_ptr[l]; qb < lm_ptr[l + 1]; ++qb) {
+                int fb = pose_f[okf[qb]];
+                if (fb < 0 || fb > fa) continue;
+                int pos = dfill[dest_of(fa / 6, fb / 6)]++;
+                ca[pos] = qa; cb[pos] = qb;
+            }
+        }
+    }
+    std::vector<int> dest_a(n_dest), dest_b(n_dest);
+    for (int a = 0; a < P; ++a)
+        for (int b = 0; b <= a; ++b) { dest_a[dest_of(a, b)] = a; dest_b[dest_of(a, b)] = b; }
+    std::vector<double> pose_raw(24 * (size_t)K), xl0(3 * (size_t)L);
+    for (int k = 0; k < K; ++k) {
+        std::memcpy(&pose_raw[24 * k], p.T_wb_init[k].R, 9 * sizeof(double));
+        std::memcpy(&pose_raw[24 * k + 9], p.T_wb_init[k].t, 3 * sizeof(double));
+        std::memcpy(&pose_raw[24 * k + 12], p.T_cb[k].R, 9 * sizeof(double));
+        std::memcpy(&pose_raw[24 * k + 21], p.T_cb[k].t, 3 * sizeof(double));
+    }
+    std::memcpy(xl0.data(), p.lm_xyz, sizeof(double) * 3 * L);
+    std::vector<uint8_t> lm_marg(L, 0);
+    for (int l = 0; l < L; ++l) lm_marg[l] = p.lm_marg ? (p.lm_marg[l] != 0) : 0;
+
+    // ---- device state ----
+    DevBufs B;
+    B.ctx = ctx;
+    GbaArgs A;
+    std::memset(&A, 0, sizeof A);
+    A.K = K; A.L = L; A.N = N; A.P = P; A.nf = nf; A.nfp = nfp;
+    A.cols = p.cols; A.rows = p.rows; A.huber = p.huber_delta; A.chi2_thr = p.chi2_threshold;
+    for (int i = 0; i < 4; ++i) A.info[i] = p.info[i];
+    A.Lw[0] = 1; A.Lw[1] = 0; A.Lw[2] = 0; A.Lw[3] = 1;
+    if (p.info[0] > 0) {
+        double l00 = std::sqrt(p.info[0]), l10 = p.info[2] / l00, t = p.info[3] - l10 * l10;
+        if (t > 0) { A.Lw[0] = l00; A.Lw[2] = l10; A.Lw[3] = std::sqrt(t); }
+    }
+    int rc;
+    const double* c_pose_raw; const int *c_pose_f, *c_pob, *c_lm_ptr, *c_okf, *c_olm, *c_kf_ptr, *c_kf_obs;
+    const int *c_da, *c_db, *c_dp, *c_ca, *c_cb; const uint8_t *c_lv, *c_lmarg; const float* c_uv;
+    std::vector<int> dptr(dest_cnt.begin(), dest_cnt.end());
+    if ((rc = B.upload((double**)&c_pose_raw, pose_raw)) || (rc = B.upload((int**)&c_pose_f, pose_f)) ||
+        (rc = B.upload((int**)&c_pob, pose_of_block)) || (rc = B.upload((uint8_t**)&c_lv, lm_used)) ||
+        (rc = B.upload((uint8_t**)&c_lmarg, lm_marg)) || (rc = B.upload((int**)&c_lm_ptr, lm_ptr)) ||
+        (rc = B.upload((int**)&c_okf, okf)) || (rc = B.upload((int**)&c_olm, olm)) ||
+        (rc = B.upload((float**)&c_uv, ouv)) || (rc = B.upload((int**)&c_kf_ptr, kf_ptr)) ||
+        (rc = B.upload((int**)&c_kf_obs, kf_obs)) || (rc = B.upload((int**)&c_da, dest_a)) ||
+        (rc = B.upload((int**)&c_db, dest_b)) || (rc = B.upload((int**)&c_dp, dptr)) ||
+        (rc = B.upload((int**)&c_ca, ca)) || (rc = B.upload((int**)&c_cb, cb)))
+        return rc;
+    A.pose_raw = c_pose_raw; A.pose_f = c_pose_f; A.pose_of_block = c_pob; A.lm_var = c_lv; A.lm_marg = c_lmarg;
+    A.lm_ptr = c_lm_ptr; A.obs_kf = c_okf; A.obs_lm = c_olm; A.obs_uv = c_uv; A.kf_ptr = c_kf_ptr; A.kf_obs = c_kf_obs;
+    A.n_dest = n_dest; A.dest_a = c_da; A.dest_b = c_db; A.dest_ptr = c_dp; A.contrib_a = c_ca; A.contrib_b = c_cb;
+    const size_t Ns = std::max(N, 1), Ls = std::max(L, 1);
+    if ((rc = B.alloc(&A.pinit, 24 * (size_t)K)) || (rc = B.alloc(&A.pc, 36 * (size_t)K)) ||
+        (rc = B.alloc(&A.x_pose, 6 * (size_t)K)) || (rc = B.alloc(&A.x_lm, 3 * Ls)) ||
+        (rc = B.alloc(&A.c_pose, 6 * (size_t)K)) || (rc = B.alloc(&A.c_lm, 3 * Ls)) ||
+        (rc = B.alloc(&A.r, 2 * Ns)) || (rc = B.alloc(&A.jp, 12 * Ns)) || (rc = B.alloc(&A.jl, 6 * Ns)) ||
+        (rc = B.alloc(&A.V, 6 * Ls)) || (rc = B.alloc(&A.gl, 3 * Ls)) || (rc = B.alloc(&A.sl, 3 * Ls)) ||
+        (rc = B.alloc(&A.Vi, 6 * Ls)) || (rc = B.alloc(&A.yl, 3 * Ls)) || (rc = B.alloc(&A.U, 27 * (size_t)K)) ||
+        (rc = B.alloc(&A.gf, nfp)) || (rc = B.alloc(&A.colsq_f, nfp)) || (rc = B.alloc(&A.sf, nfp)) ||
+        (rc = B.alloc(&A.Df, nfp)) || (rc = B.alloc(&A.bf, nfp)) || (rc = B.alloc(&A.yv, nfp)) ||
+        (rc = B.alloc(&A.xf, nfp)) || (rc = B.alloc(&A.Wo, 18 * Ns)) || (rc = B.alloc(&A.Yo, 18 * Ns)) ||
+        (rc = B.alloc(&A.S, (size_t)nfp * nfp)) || (rc = B.alloc(&A.Linv, (size_t)nfp * 64)))
+        return rc;
+    const size_t nblk_max = (std::max<size_t>({Ns, Ls, 6 * (size_t)K, (size_t)nfp}) + 255) / 256 + 8;
+    double* partial;
+    double* scal;  // [0] cost [1] gmax [2] bad [3] nonfinite [4..6] model/step/xnorm [7] cand cost [8..10] post
+    int* dfail;
+    uint8_t *d_outl, *d_bad;
+    double* d_chi2;
+    if ((rc = B.alloc(&partial, 3 * nblk_max + 3 * (size_t)K)) || (rc = B.alloc(&scal, 16)) ||
+        (rc = B.alloc(&dfail, 4)) || (rc = B.alloc(&d_outl, Ns)) || (rc = B.alloc(&d_bad, Ls)) ||
+        (rc = B.alloc(&d_chi2, Ns)))
+        return rc;
+    GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));
+    GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0.data(), sizeof(double) * 3 * L, hipMemcpyHostToDevice, st));
+    GBA_CHECK(gba_launch_setup(A, st));
+
+    auto read = [&](double* h, int off, int n) -> int {
+        GBA_CHECK(hipMemcpyAsync(h, scal + off, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+        GBA_CHECK(hipStreamSynchronize(st));
+        return VIO_OK;
+    };
+    // ---- fixed cost (program.cc:305-390) ----
+    double h[16];
+    GBA_CHECK(gba_launch_eval(A, A.x_pose, A.x_lm, 2, partial, scal + 0, st));
+    if ((rc = read(h, 0, 1))) return rc;
+    const double fixed_cost = h[0];
+
+    // ---- LM (oracle_lm_minimize) ----
+    const int max_iter = p.max_iterations;
+    const bool fixed = p.fixed_iterations != 0;
+    int termination = VIO_TERM_NO_CONVERGENCE, iterations = 0, nsucc = 0, nunsucc = 0;
+    double initial_cost, final_cost;
+    if (n_free == 0) {
+        termination = VIO_TERM_CONVERGENCE;
+        initial_cost = final_cost = fixed_cost;
+    } else {
+        double radius = 1e4, decrease = 2.0, x_norm = -1.0, min_cost = DBL_MAX;
+        int consecutive_invalid = 0;
+        GBA_CHECK(gba_launch_eval(A, A.x_pose, A.x_lm, 1, partial, scal + 0, st));
+        GBA_CHECK(gba_launch_linearise(A, 1, partial, scal + 1, st));
+        if ((rc = read(h, 0, 2))) return rc;
+        double x_cost = h[0], gmax = h[1];
+        initial_cost = x_cost + fixed_cost;
+        double step_eval_current = x_cost, iter_cost = x_cost + fixed_cost;
+        final_cost = initial_cost;
+        int iteration = 0;
+        bool step_ok = true;
+        double model_change = 0, cand_cost = 0;
+        for (;;) {
+            if (step_ok) {
+                nsucc++;
+                if (x_cost < min_cost) min_cost = x_cost;
+            } else {
+                nunsucc++;
+            }
+            iterations++;
+            final_cost = std::min(final_cost, iter_cost);
+            if (iteration >= max_iter) { termination = VIO_TERM_NO_CONVERGENCE; break; }
+            if (!fixed && step_ok && gmax <= 1e-10) { termination = VIO_TERM_CONVERGENCE; break; }
+            if (!fixed && radius <= 1e-32) { termination = VIO_TERM_CONVERGENCE; break; }
+            iteration++;
+            // ComputeTrustRegionStep + candidate cost, one batch of kernels, one readback
+            GBA_CHECK(hipMemsetAsync(dfail, 0, sizeof(int), st));
+            GBA_CHECK(gba_launch_step_prep(A, radius, partial, scal + 2, st));
+            GBA_CHECK(gba_launch_cholesky(A, dfail, st));
+            GBA_CHECK(gba_launch_solve(A, st));
+            GBA_CHECK(gba_launch_backsub(A, partial, scal + 3, st));
+            GBA_CHECK(gba_launch_model(A, partial, scal + 4, st));
+            GBA_CHECK(gba_launch_eval(A, A.c_pose, A.c_lm, 0, partial, scal + 7, st));
+            int hfail = 0;
+            GBA_CHECK(hipMemcpyAsync(&hfail, dfail, sizeof(int), hipMemcpyDeviceToHost, st));
+            if ((rc = read(h, 0, 8))) return rc;
+            bool valid = h[2] == 0.0 && hfail == 0 && h[3] == 0.0;
+            model_change = h[4];
+            if (valid) valid = model_change > 0.0;
+            if (!valid) {
+                if (++consecutive_invalid >= 5) { termination = VIO_TERM_FAILURE; break; }
+                radius /= decrease;
+                decrease *= 2.0;
+                step_ok = false;
+                iter_cost = x_cost + fixed_cost;
+                continue;
+            }
+            consecutive_invalid = 0;
+            cand_cost = h[7];
+            const double step_norm = std::sqrt(h[5]);
+            if (!fixed && step_norm <= 1e-8 * (x_norm + 1e-8)) { termination = VIO_TERM_CONVERGENCE; break; }
+            if (!fixed && std::fabs(x_cost - cand_cost) <= 1e-6 * x_cost) { termination = VIO_TERM_CONVERGENCE; break; }
+            const double rel = (step_eval_current - cand_cost) / model_change;
+            if (rel > 1e-3) {
+                GBA_CHECK(hipMemcpyAsync(A.x_pose, A.c_pose, sizeof(double) * 6 * K, hipMemcpyDeviceToDevice, st));
+                GBA_CHECK(hipMemcpyAsync(A.x_lm, A.c_lm, sizeof(double) * 3 * L, hipMemcpyDeviceToDevice, st));
+                x_norm = std::sqrt(h[6]);
+                GBA_CHECK(gba_launch_eval(A, A.x_pose, A.x_lm, 1, partial, scal + 0, st));
+                GBA_CHECK(gba_launch_linearise(A, 0, partial, scal + 1, st));
+                if ((rc = read(h, 0, 2))) return rc;
+                x_cost = h[0];
+                gmax = h[1];
+                step_ok = true;
+                radius = std::min(1e16, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3)));
+                decrease = 2.0;
+                step_eval_current = cand_cost;
+                iter_cost = x_cost + fixed_cost;
+            } else {
+                step_ok = false;
+                iter_cost = cand_cost + fixed_cost;
+                radius /= decrease;
+                decrease *= 2.0;
+            }
+        }
+        if (termination == VIO_TERM_FAILURE) {  // Ceres leaves the user's parameters untouched
+            GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));
+            GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0.data(), sizeof(double) * 3 * L, hipMemcpyHostToDevice, st));
+        }
+    }
+    // ---- chi^2 / outliers / bad landmarks, outputs ----
+    GBA_CHECK(gba_launch_post(A, d_chi2, d_outl, d_bad, partial, scal + 8, st));
+    if ((rc = read(h, 8, 3))) return rc;
+    std::vector<double> pc(36 * (size_t)K), xl(3 * Ls), chi2(Ns);
+    std::vector<uint8_t> outl(Ns), bad(Ls);
+    GBA_CHECK(hipMemcpy(pc.data(), A.pc, sizeof(double) * 36 * K, hipMemcpyDeviceToHost));
+    GBA_CHECK(hipMemcpy(xl.data(), A.x_lm, sizeof(double) * 3 * Ls, hipMemcpyDeviceToHost));
+    GBA_CHECK(hipMemcpy(chi2.data(), d_chi2, sizeof(double) * Ns, hipMemcpyDeviceToHost));
+    GBA_CHECK(hipMemcpy(outl.data(), d_outl, Ns, hipMemcpyDeviceToHost));
+    GBA_CHECK(hipMemcpy(bad.data(), d_bad, Ls, hipMemcpyDeviceToHost));
+    if (out->T_wb)
+        for (int k = 0; k < K; ++k) {
+            std::memcpy(out->T_wb[k].R, &pc[36 * k], 9 * sizeof(double));
+            std::memcpy(out->T_wb[k].t, &pc[36 * k + 9], 3 * sizeof(double));
+        }
+    if (out->lm_xyz) std::memcpy(out->lm_xyz, xl.data(), sizeof(double) * 3 * L);
+    for (int q = 0; q < N; ++q) {
+        if (out->obs_chi2) out->obs_chi2[perm[q]] = chi2[q];
+        if (out->obs_outlier) out->obs_outlier[perm[q]] = outl[q];
+    }
+    if (out->lm_bad) std::memcpy(out->lm_bad, bad.data(), L);
+    if (out->summary) {
+        vio_ba_summary& s = *out->summary;
+        std::memset(&s, 0, sizeof s);
+        s.success = termination != VIO_TERM_FAILURE;
+        s.termination = termination;
+        s.iterations = iterations;
+        s.num_successful_steps = nsucc;
+        s.num_unsuccessful_steps = nunsucc;
+        s.num_inliers = (int)h[8];
+        s.num_outliers = (int)h[9];
+        s.num_bad_lm = (int)h[10];
+        s.initial_cost = initial_cost;
+        s.final_cost = final_cost;
+        s.fixed_cost = fixed_cost;
+    }
+    return VIO_OK;
+}
+
+}  // namespace vio360

@@ -19,6 +19,8 @@
 namespace vio360 {
 
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream);
+bool global_ba_applicable(const vio_ba_problem& p);
+int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out);
 size_t ba_ws_extra_doubles();
 
 void set_error(vio_ctx* ctx, const std::string& msg) {
@@ -510,6 +512,18 @@ void vio_ba_batch_destroy(vio_ba_batch* b) {
 
 int vio_ba_solve_batched(vio_ctx* ctx, const vio_ba_problem* probs, vio_ba_output* outs, int n) {
     if (!ctx || !probs || !outs || n <= 0) return VIO_EINVAL;
+    // problems beyond one workgroup's reduced system (K > 16: RunBA over hundreds of keyframes,
+    // config 5) take the multi-kernel global path, one problem at a time
+    bool any_global = false;
+    for (int i = 0; i < n; ++i) any_global |= global_ba_applicable(probs[i]);
+    if (any_global) {
+        for (int i = 0; i < n; ++i) {
+            int rc = global_ba_applicable(probs[i]) ? global_ba_solve(ctx, probs[i], &outs[i])
+                                                    : vio_ba_solve_batched(ctx, &probs[i], &outs[i], 1);
+            if (rc != VIO_OK) return rc;
+        }
+        return VIO_OK;
+    }
     vio_ba_batch* b = nullptr;
     int rc = vio_ba_batch_create(ctx, probs, n, &b);
     if (rc != VIO_OK) return rc;

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ba_types.h"
+#include "ba_factor_dev.h"
 #include "lie_dev.h"
 
 namespace vio360 {
@@ -94,126 +95,6 @@ __device__ __forceinline__ double block_max(double v, double* red) {
 #pragma unroll
     for (int w = 0; w < BA_THREADS / 64; ++w) r = fmax(r, red[w]);
     return r;
-}
-
-// ------------------------------------------------------------------------------------------
-// HuberLoss(delta) (loss_function.cc:48-62) -> cost, residual scale, Jacobian scale.
-// rho'' <= 0 everywhere for Huber, so the Corrector reduces to sqrt(rho') scaling (corrector.cc:82-86).
-__device__ __forceinline__ void huber(double delta, double sq, double& cost, double& scale) {
-    double b = delta * delta;
-    if (sq > b) {
-        double r = sqrt(sq);
-        cost = 0.5 * (2.0 * delta * r - b);
-        scale = sqrt(fmax(DBL_MIN, delta / r));
-    } else {
-        cost = 0.5 * sq;
-        scale = 1.0;
-    }
-}
-
-// BAFactor::Evaluate / PnPFactor::Evaluate (Factors.cpp:33-210, 327-542) given the pose cache.
-// returns 0 = ok, 1 = evaluation failure (PnP with |Pc| < 1e-10)
-__device__ __forceinline__ int factor_eval(const double* pc, const double* Rcb_raw, const double* Pw, double uo,
-                                           double vo, double cols, double rows, const double* Lw, bool outlier,
-                                           bool is_pnp, bool want_jac, double* r, double* Jp, double* Jl,
-                                           bool& jzero) {
-    jzero = true;
-    if (outlier) {
-        r[0] = 640.0; r[1] = 480.0;
-        return 0;
-    }
-    const double* Rbw = pc + 12;
-    const double* tbw = pc + 21;
-    const double* Rcw = pc + 24;
-    const double* tcw = pc + 33;
-    double Pc[3];
-    m3vec(Rcw, Pw, Pc);
-    Pc[0] += tcw[0]; Pc[1] += tcw[1]; Pc[2] += tcw[2];
-    double x = Pc[0], y = Pc[1], z = Pc[2];
-    double L = nrm3(Pc);
-    if (L < 1e-10) {
-        if (is_pnp) return 1;
-        r[0] = 640.0; r[1] = 360.0;
-        return 0;
-    }
-    const double inv2pi = 1.0 / (2.0 * M_PI);
-    double theta = atan2(x, z);
-    double phi = -asin(y / L);
-    double u = cols * (0.5 + theta / (2.0 * M_PI));
-    double v = rows * (0.5 - phi / M_PI);
-    double du = uo - u, dv = vo - v;
-    if (du > cols / 2.0) du -= cols;
-    else if (du < -cols / 2.0) du += cols;
-    if (fabs(du) > 100.0 || fabs(dv) > 100.0) {
-        r[0] = 100.0; r[1] = 100.0;
-        return 0;
-    }
-    r[0] = Lw[0] * du;
-    r[1] = Lw[2] * du + Lw[3] * dv;
-    if (!want_jac) return 0;
-    double xz2 = x * x + z * z, L2 = L * L;
-    if (xz2 < 1e-10 || L2 < 1e-10) return 0;
-    jzero = false;
-    double xzn = sqrt(xz2);
-    double Jc[6];
-    Jc[0] = -cols * inv2pi * z / xz2;
-    Jc[1] = 0.0;
-    Jc[2] = cols * inv2pi * x / xz2;
-    Jc[3] = rows / M_PI * (x * y) / (L2 * xzn);
-    Jc[4] = -rows / M_PI * xzn / L2;
-    Jc[5] = rows / M_PI * (y * z) / (L2 * xzn);
-    double Jw[6];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        Jw[j] = Lw[0] * Jc[j];
-        Jw[3 + j] = Lw[2] * Jc[j] + Lw[3] * Jc[3 + j];
-    }
-    // pose: [ -R_cb_raw | R_cb_raw [Pb]x ]   (Factors.cpp:500-522)
-    double Pb[3];
-    m3vec(Rbw, Pw, Pb);
-    Pb[0] += tbw[0]; Pb[1] += tbw[1]; Pb[2] += tbw[2];
-    double A[6];  // Jw * R_cb_raw (2x3)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-            A[3 * i + j] = Jw[3 * i] * Rcb_raw[j] + Jw[3 * i + 1] * Rcb_raw[3 + j] + Jw[3 * i + 2] * Rcb_raw[6 + j];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const double* a = A + 3 * i;
-        Jp[6 * i + 0] = -a[0];
-        Jp[6 * i + 1] = -a[1];
-        Jp[6 * i + 2] = -a[2];
-        // a * hat(Pb): [a1*Pb2 - a2*Pb1... ] row vector times skew
-        Jp[6 * i + 3] = a[1] * Pb[2] - a[2] * Pb[1];
-        Jp[6 * i + 4] = a[2] * Pb[0] - a[0] * Pb[2];
-        Jp[6 * i + 5] = a[0] * Pb[1] - a[1] * Pb[0];
-        // point: Jw * R_cb_raw * R_bw   (Factors.cpp:525-534)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) Jl[3 * i + j] = a[0] * Rbw[j] + a[1] * Rbw[3 + j] + a[2] * Rbw[6 + j];
-    }
-    return 0;
-}
-
-// compute_chi_square (Factors.cpp:212-265, 544-612), unweighted e^T Info e
-__device__ __forceinline__ double factor_chi2(const double* pc, const double* Pw, double uo, double vo, double cols,
-                                              double rows, const double* info, bool outlier, bool is_pnp) {
-    if (outlier && !is_pnp) return 0.0;
-    const double* Rcw = pc + 24;
-    const double* tcw = pc + 33;
-    double Pc[3];
-    m3vec(Rcw, Pw, Pc);
-    Pc[0] += tcw[0]; Pc[1] += tcw[1]; Pc[2] += tcw[2];
-    double L = nrm3(Pc);
-    if (L < 1e-10) return is_pnp ? DBL_MAX : 1000.0;
-    double theta = atan2(Pc[0], Pc[2]);
-    double phi = -asin(Pc[1] / L);
-    double u = cols * (0.5 + theta / (2.0 * M_PI));
-    double v = rows * (0.5 - phi / M_PI);
-    double du = uo - u, dv = vo - v;
-    if (du > cols / 2.0) du -= cols;
-    else if (du < -cols / 2.0) du += cols;
-    return du * (info[0] * du + info[1] * dv) + dv * (info[2] * du + info[3] * dv);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -404,29 +285,7 @@ struct WinCtx {
 // pose cache for the parameter set at (xp): T_wb = SE3(T_init) * exp(delta), etc.
 __device__ void pose_cache(BaShared& sh, const WinCtx& c, const double* xp) {
     int K = c.w->K;
-    for (int k = threadIdx.x; k < K; k += BA_THREADS) {
-        double dR[9], dt[3], xi[6];
-        for (int i = 0; i < 6; ++i) xi[i] = xp[6 * k + i];
-        se3_exp(xi, dR, dt);
-        const double* Ri = sh.pinit[k];
-        const double* ti = sh.pinit[k] + 9;
-        const double* Rc = sh.pinit[k] + 12;
-        const double* tc = sh.pinit[k] + 21;
-        double* pc = sh.pc[k];
-        double Rwb[9], twb[3], Rbw[9], tbw[3], Rcw[9], tcw[3];
-        m3mul(Ri, dR, Rwb);
-        m3vec(Ri, dt, twb);
-        for (int i = 0; i < 3; ++i) twb[i] += ti[i];
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) Rbw[3 * i + j] = Rwb[3 * j + i];
-        m3vec(Rbw, twb, tbw);
-        for (int i = 0; i < 3; ++i) tbw[i] = -tbw[i];
-        m3mul(Rc, Rbw, Rcw);
-        m3vec(Rc, tbw, tcw);
-        for (int i = 0; i < 3; ++i) tcw[i] += tc[i];
-        for (int i = 0; i < 9; ++i) { pc[i] = Rwb[i]; pc[12 + i] = Rbw[i]; pc[24 + i] = Rcw[i]; }
-        for (int i = 0; i < 3; ++i) { pc[9 + i] = twb[i]; pc[21 + i] = tbw[i]; pc[33 + i] = tcw[i]; }
-    }
+    for (int k = threadIdx.x; k < K; k += BA_THREADS) pose_cache_one(sh.pinit[k], xp + 6 * k, sh.pc[k]);
 }
 
 // Evaluate cost (and the Jacobian when want_jac) at the point (xp, xl, xv, xb).

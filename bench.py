@@ -41,10 +41,26 @@ def ba_flops_per_iter(prob):
     return float(f)
 
 
+def shard_seeds(seed0, rank, windows):
+    """Window partition of the weak-scaling job: rank r owns windows [r*W, (r+1)*W) of the global
+    sequence (seed = seed0 + global window index); no window is shared, no data crosses ranks."""
+    return [seed0 + rank * windows + i for i in range(windows)]
+
+
+def reduce_max(x, dist, device):
+    """Max of a per-rank scalar over all ranks (the slowest rank defines the job time)."""
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def make_shard(vio, synth, rank, windows, lm_iters):
     probs = []
-    for i in range(windows):
-        w = synth.config3(synth.SEED + rank * windows + i)
+    for seed in shard_seeds(synth.SEED, rank, windows):
+        w = synth.config3(seed)
         probs.append(vio.BaProblem(w, variant=vio.VIO_BA_VI, max_iterations=lm_iters, fixed_iterations=1))
     return probs
 
@@ -189,10 +205,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kms, kcount = batch.kernel_ms()
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = reduce_max(elapsed, dist, f"cuda:{local_rank}")
     # sanity: every window actually ran its iterations
     res = batch.download()
     assert all(r["iterations"] == args.lm_iters + 1 and r["final_cost"] < r["initial_cost"] for r in res)

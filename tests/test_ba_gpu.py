@@ -133,7 +133,7 @@ def test_edge_cases(vio, synth, gpu_ctx):
     with pytest.raises(vio.VioError):
         gpu_ctx.ba_solve([vio.BaProblem(bad)])
     with pytest.raises(vio.VioError):
-        gpu_ctx.ba_solve([vio.BaProblem(synth.make_window(K=17, L=10, seed=1))])
+        gpu_ctx.ba_solve([vio.BaProblem(synth.make_window(K=12, L=10, seed=1, imu=True), variant=vio.VIO_BA_VI)])
 
 
 def test_config4_full_size_properties(vio, synth, gpu_ctx):
@@ -149,3 +149,42 @@ def test_config4_full_size_properties(vio, synth, gpu_ctx):
         assert e1 < e0
     for i in (0, 97, 255):
         assert_parity(oracle_lib.ba_solve(vio, probs[i]), res[i], probs[i].c.chi2_threshold)
+
+
+@pytest.mark.parametrize("variant", ["full", "local"])
+def test_global_ba_parity(vio, synth, gpu_ctx, variant):
+    """K > 16 takes the multi-kernel global path (dense Schur + MFMA Cholesky): same parity bar."""
+    w = synth.make_global(K=120, L=6000, k_per=10, seed=31)
+    if variant == "local":
+        rng = np.random.default_rng(4)
+        marg = (rng.random(len(w["lm_xyz"])) < 0.1).astype(np.uint8)
+        w = dict(w, lm_const=marg, lm_marg=marg)
+    p = vio.BaProblem(w, variant=vio.VIO_BA_FULL if variant == "full" else vio.VIO_BA_LOCAL)
+    o = oracle_lib.ba_solve(vio, p)
+    g = gpu_ctx.ba_solve([p])[0]
+    assert_parity(o, g, p.c.chi2_threshold)
+    g2 = gpu_ctx.ba_solve([p])[0]
+    assert np.array_equal(g["T_wb"], g2["T_wb"]) and np.array_equal(g["lm_xyz"], g2["lm_xyz"])
+
+
+def test_global_ba_fixed_iterations(vio, synth, gpu_ctx):
+    w = synth.make_global(K=64, L=3000, k_per=8, seed=8)
+    p = vio.BaProblem(w, variant=vio.VIO_BA_FULL, max_iterations=10, fixed_iterations=1)
+    o = oracle_lib.ba_solve(vio, p)
+    g = gpu_ctx.ba_solve([p])[0]
+    assert o["iterations"] == g["iterations"] == 11
+    assert_parity(o, g, p.c.chi2_threshold, iters_tol=0)
+
+
+def test_config5_full_size_properties(vio, synth, gpu_ctx):
+    """Config 5 (1000 KF x 50k landmarks, dense 5994^2 reduced system) at full size: converges,
+    improves on the ground truth, bitwise reproducible."""
+    w = synth.make_global()
+    p = vio.BaProblem(w, variant=vio.VIO_BA_FULL, max_iterations=15)
+    g = gpu_ctx.ba_solve([p])[0]
+    assert g["success"] == 1 and g["final_cost"] < 0.5 * g["initial_cost"]
+    e0 = np.abs(w["T_wb_init"][:, :3, 3] - w["T_wb_true"][:, :3, 3]).mean()
+    e1 = np.abs(g["T_wb"][:, :3, 3] - w["T_wb_true"][:, :3, 3]).mean()
+    assert e1 < 0.5 * e0
+    g2 = gpu_ctx.ba_solve([p])[0]
+    assert np.array_equal(g["T_wb"], g2["T_wb"]) and g["final_cost"] == g2["final_cost"]
