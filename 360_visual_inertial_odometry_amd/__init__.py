@@ -11,7 +11,8 @@ import numpy as np
 
 from . import abi
 from .abi import (VIO_BA_FULL, VIO_BA_LOCAL, VIO_BA_VI, VIO_PNP, BaOutput, BaProblem,  # noqa: F401
-                  ErpKltParams, ErpTrackerParams, default_klt_params, default_tracker_params)
+                  ErpFrontendParams, ErpKltParams, ErpTrackerParams, default_frontend_params,
+                  default_klt_params, default_tracker_params)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VIO360_LIB") or os.path.join(_HERE, "libvio360.so")
@@ -25,7 +26,8 @@ EXPORTS = [
     "erp_klt_track", "erp_gftt", "erp_rot_ransac", "erp_ransac_samples", "erp_tracker_create",
     "erp_tracker_upload", "erp_tracker_device_frame", "erp_tracker_swap", "erp_tracker_set_points",
     "erp_tracker_run", "erp_tracker_sync", "erp_tracker_download", "erp_tracker_stage_ms",
-    "erp_tracker_destroy",
+    "erp_tracker_destroy", "erp_frontend_create", "erp_frontend_track", "erp_frontend_features",
+    "erp_frontend_stats", "erp_frontend_destroy",
 ]
 
 
@@ -72,6 +74,11 @@ def lib():
     L.erp_tracker_download.argtypes = [vp, vp, vp, vp, vp, C.POINTER(C.c_int)]
     L.erp_tracker_stage_ms.argtypes = [vp] + [C.POINTER(C.c_double)] * 5
     L.erp_tracker_destroy.argtypes = [vp]
+    L.erp_frontend_create.argtypes = [vp, C.c_int, C.c_int, C.POINTER(abi.ErpFrontendParams), C.POINTER(C.c_void_p)]
+    L.erp_frontend_track.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_int)]
+    L.erp_frontend_features.argtypes = [vp, vp, vp, vp, vp, C.c_int]
+    L.erp_frontend_stats.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.erp_frontend_destroy.argtypes = [vp]
     _lib = L
     return L
 
@@ -227,6 +234,42 @@ class Tracker:
     def close(self):
         if self.h:
             lib().erp_tracker_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Frontend:
+    """erp_frontend_*: FeatureTracker::TrackFeatures (device numerics + the reference's bookkeeping)."""
+
+    def __init__(self, ctx, W, H, params=None):
+        self.ctx = ctx
+        h = C.c_void_p()
+        self.params = params or default_frontend_params()
+        ctx.check(lib().erp_frontend_create(ctx.h, W, H, C.byref(self.params), C.byref(h)), "erp_frontend_create")
+        self.h = h
+
+    def track(self, img):
+        img = _u8img(img)
+        n = C.c_int()
+        self.ctx.check(lib().erp_frontend_track(self.h, _p(img), img.shape[1], C.byref(n)), "erp_frontend_track")
+        ids = np.zeros(n.value, np.int32)
+        xy = np.zeros((n.value, 2), np.float32)
+        tc = np.zeros(n.value, np.int32)
+        age = np.zeros(n.value, np.int32)
+        self.ctx.check(lib().erp_frontend_features(self.h, _p(ids), _p(xy), _p(tc), _p(age), n.value),
+                       "erp_frontend_features")
+        nt, nd = C.c_int(), C.c_int()
+        lib().erp_frontend_stats(self.h, C.byref(nt), C.byref(nd))
+        return {"ids": ids, "xy": xy, "track_count": tc, "age": age, "num_tracked": nt.value, "num_detected": nd.value}
+
+    def close(self):
+        if self.h:
+            lib().erp_frontend_destroy(self.h)
             self.h = None
 
     def __del__(self):

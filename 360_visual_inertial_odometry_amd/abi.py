@@ -74,6 +74,19 @@ class ErpTrackerParams(C.Structure):
                 ("boundary_margin", C.c_int32), ("polar_ratio", C.c_float)]
 
 
+class ErpFrontendParams(C.Structure):
+    _fields_ = [("max_features", C.c_int32), ("min_distance", C.c_float), ("quality_level", C.c_float),
+                ("boundary_margin", C.c_int32), ("grid_cols", C.c_int32), ("grid_rows", C.c_int32),
+                ("max_features_per_grid", C.c_int32), ("remove_clustered", C.c_int32),
+                ("clustered_std_ratio", C.c_float), ("ransac_seed", C.c_uint32)]
+
+
+def default_frontend_params(seed=0):
+    """config/default_config.yaml values the tracker reads (feature_detection.*, camera.boundary_margin,
+    visualization.highlight_clustered_grid / clustered_std_ratio)."""
+    return ErpFrontendParams(1000, 30.0, 0.01, 20, 20, 10, 10, 1, 0.25, seed)
+
+
 def default_klt_params():
     """FeatureTracker's hard-coded LK settings (src/processing/FeatureTracker.cpp:33-35,240)."""
     return ErpKltParams(21, 3, 30, 0.01, 0.01, 0)

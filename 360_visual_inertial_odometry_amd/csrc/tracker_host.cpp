@@ -536,3 +536,260 @@ int erp_rot_ransac(vio_ctx* ctx, const float* p0, const float* p1, int n, int W,
 }
 
 }  // extern "C"
+
+// ============================================================================================
+// erp_frontend: FeatureTracker::TrackFeatures (FeatureTracker.cpp:61-206) = the device numeric
+// path + the reference's host bookkeeping, restated on plain structs instead of Frame / Feature.
+// ============================================================================================
+namespace {
+
+struct FeatureRec {
+    int32_t id;
+    float x, y;
+    int32_t track_count, age;
+};
+
+// Frame::AssignFeaturesToGrid + LimitFeaturesPerGrid (src/database/Frame.cpp:108-202)
+void assign_and_limit(std::vector<FeatureRec>& feats, int W, int H, int gc, int gr, int max_per) {
+    const float cw = (float)W / gc, ch = (float)H / gr;
+    std::vector<std::vector<int>> grid((size_t)gc * gr);
+    auto assign = [&]() {
+        for (auto& c : grid) c.clear();
+        for (size_t i = 0; i < feats.size(); ++i) {
+            float x = feats[i].x, y = feats[i].y;
+            if (x < 0 || x >= W || y < 0 || y >= H) continue;
+            int gx = std::min((int)(x / cw), gc - 1), gy = std::min((int)(y / ch), gr - 1);
+            grid[(size_t)gy * gc + gx].push_back((int)i);
+        }
+    };
+    assign();
+    for (auto& cell : grid) {
+        if (cell.size() <= (size_t)max_per) continue;
+        std::sort(cell.begin(), cell.end(),
+                  [&](int a, int b) { return feats[a].track_count > feats[b].track_count; });
+        cell.resize(max_per);
+    }
+    std::vector<char> keep(feats.size(), 0);
+    for (auto& cell : grid)
+        for (int i : cell) keep[i] = 1;
+    std::vector<FeatureRec> out;
+    for (size_t i = 0; i < feats.size(); ++i)
+        if (keep[i]) out.push_back(feats[i]);
+    feats.swap(out);
+}
+
+// FeatureTracker::RemoveClusteredFeatures (FeatureTracker.cpp:404-497), tracker grid 20 x 10
+void remove_clustered(std::vector<FeatureRec>& feats, int W, int H, float ratio) {
+    if (feats.size() < 4) return;
+    const int gc = 20, gr = 10;  // m_grid_cols / m_grid_rows (FeatureTracker.cpp:39-40)
+    const float cw = (float)W / gc, ch = (float)H / gr;
+    const float thr = std::sqrt(cw * cw + ch * ch) * ratio;
+    std::vector<std::vector<size_t>> cells((size_t)gc * gr);
+    auto cell_of = [&](const FeatureRec& f) {
+        int col = std::min((int)(f.x / cw), gc - 1), row = std::min((int)(f.y / ch), gr - 1);
+        return (size_t)row * gc + col;
+    };
+    for (size_t i = 0; i < feats.size(); ++i) cells[cell_of(feats[i])].push_back(i);
+    std::vector<char> clustered(cells.size(), 0);
+    for (size_t c = 0; c < cells.size(); ++c) {
+        if (cells[c].size() < 4) continue;
+        float mx = 0.f, my = 0.f;
+        for (size_t i : cells[c]) { mx += feats[i].x; my += feats[i].y; }
+        mx /= cells[c].size();
+        my /= cells[c].size();
+        float var = 0.f;
+        for (size_t i : cells[c]) {
+            float dx = feats[i].x - mx, dy = feats[i].y - my;
+            var += (dx * dx + dy * dy);
+        }
+        var /= cells[c].size();
+        if (std::sqrt(var) < thr) clustered[c] = 1;
+    }
+    std::vector<FeatureRec> out;
+    for (auto& f : feats)
+        if (!clustered[cell_of(f)]) out.push_back(f);
+    feats.swap(out);
+}
+
+}  // namespace
+
+struct erp_frontend {
+    erp_tracker* t = nullptr;
+    erp_frontend_params p{};
+    int W = 0, H = 0;
+    int frame = 0;
+    int32_t next_id = 0;
+    int num_tracked = 0, num_detected = 0;
+    std::vector<FeatureRec> feats;
+};
+
+namespace {
+
+// GFTT on slot 1 with the DetectNewFeatures mask: polar ∧ boundary ∧ (discs around `feats`)
+int frontend_detect(erp_frontend* f, std::vector<float>& corners) {
+    erp_tracker* t = f->t;
+    hipStream_t st = t->ctx->stream;
+    int rc;
+    const bool discs = !f->feats.empty();
+    if (discs) {
+        const int n = (int)f->feats.size();
+        if (n > t->max_points) { set_error(t->ctx, "too many features for the disc mask"); return VIO_ENOSYS; }
+        std::vector<float> xy(2 * (size_t)n);
+        for (int i = 0; i < n; ++i) { xy[2 * i] = f->feats[i].x; xy[2 * i + 1] = f->feats[i].y; }
+        VIO_HIP(t->ctx, hipMemcpyAsync(t->d_pts, xy.data(), sizeof(float) * 2 * n, hipMemcpyHostToDevice, st));
+        VIO_HIP(t->ctx, hipMemcpyAsync(t->d_scal + 5, &n, sizeof(int), hipMemcpyHostToDevice, st));
+        VIO_HIP(t->ctx, hipMemsetAsync(t->d_disc, 0, sizeof(uint32_t) * t->disc_words * t->H, st));
+        const int radius = (int)f->p.min_distance;
+        if (radius != t->halfw_r) {
+            std::vector<int> hw = circle_half_widths(radius);
+            if ((rc = dalloc(t, &t->d_halfw, sizeof(int) * (radius + 1)))) return rc;
+            VIO_HIP(t->ctx, hipMemcpy(t->d_halfw, hw.data(), sizeof(int) * (radius + 1), hipMemcpyHostToDevice));
+            t->halfw_r = radius;
+        }
+        DiscArgs d{t->d_pts, nullptr, nullptr, t->d_scal + 5, t->d_disc, t->disc_words, t->W, t->H, radius, t->d_halfw};
+        hipError_t e = launch_disc_mask(d, n, st);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "disc_mask_kernel");
+    }
+    if ((rc = enqueue_gftt(t, t->lvl[1][0], t->lp[0], nullptr, 0, f->p.max_features, (double)f->p.quality_level,
+                           (double)f->p.min_distance, discs, f->p.boundary_margin, 0.15f)))
+        return rc;
+    int n = 0;
+    corners.resize(2 * (size_t)std::max(f->p.max_features, 1));
+    if ((rc = read_corners(t, corners.data(), &n))) return rc;
+    corners.resize(2 * (size_t)n);
+    return VIO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int erp_frontend_create(vio_ctx* ctx, int W, int H, const erp_frontend_params* p, erp_frontend** out) {
+    if (!ctx || !p || !out || p->max_features <= 0 || p->grid_cols <= 0 || p->grid_rows <= 0 ||
+        p->max_features_per_grid <= 0 || p->min_distance < 0 || p->quality_level <= 0)
+        return VIO_EINVAL;
+    *out = nullptr;
+    erp_frontend* f = new erp_frontend();
+    f->p = *p;
+    f->W = W; f->H = H;
+    const int cap = std::max(4096, 2 * p->max_features + p->grid_cols * p->grid_rows * p->max_features_per_grid);
+    int rc = erp_tracker_create(ctx, W, H, cap, p->max_features, &f->t);
+    if (rc) { delete f; return rc; }
+    if ((rc = ensure_iters(f->t, 1000))) { erp_tracker_destroy(f->t); delete f; return rc; }
+    *out = f;
+    return VIO_OK;
+}
+
+void erp_frontend_destroy(erp_frontend* f) {
+    if (!f) return;
+    erp_tracker_destroy(f->t);
+    delete f;
+}
+
+int erp_frontend_track(erp_frontend* f, const uint8_t* img, int stride, int* n_features) {
+    if (!f || !img) return VIO_EINVAL;
+    erp_tracker* t = f->t;
+    vio_ctx* ctx = t->ctx;
+    hipStream_t st = ctx->stream;
+    int rc;
+    if ((rc = upload_frame(t, 1, img, stride))) return rc;
+    const erp_frontend_params& P = f->p;
+    if (f->frame == 0 || f->feats.empty()) {
+        // first frame (or nothing to track): detect only (:68-97)
+        f->feats.clear();
+        std::vector<float> c;
+        if ((rc = frontend_detect(f, c))) return rc;
+        for (size_t i = 0; i < c.size() / 2; ++i) f->feats.push_back({f->next_id++, c[2 * i], c[2 * i + 1], 0, 0});
+        f->num_tracked = 0;
+        f->num_detected = (int)(c.size() / 2);
+        assign_and_limit(f->feats, f->W, f->H, P.grid_cols, P.grid_rows, P.max_features_per_grid);
+    } else {
+        // TrackOpticalFlow (:228-251)
+        const int n = (int)f->feats.size();
+        if (n > t->max_points) { set_error(ctx, "too many features"); return VIO_ENOSYS; }
+        std::vector<float> prev(2 * (size_t)n), next(2 * (size_t)n);
+        std::vector<uint8_t> status(n);
+        for (int i = 0; i < n; ++i) { prev[2 * i] = f->feats[i].x; prev[2 * i + 1] = f->feats[i].y; }
+        if ((rc = erp_tracker_set_points(t, prev.data(), n))) return rc;
+        erp_klt_params kp{21, 3, 30, 0.01f, 0.01f, 0};  // FeatureTracker.cpp:33-35, 240
+        if ((rc = enqueue_lk(t, &kp, n))) return rc;
+        VIO_HIP(ctx, hipMemcpyAsync(next.data(), t->d_next, sizeof(float) * 2 * n, hipMemcpyDeviceToHost, st));
+        VIO_HIP(ctx, hipMemcpyAsync(status.data(), t->d_status, n, hipMemcpyDeviceToHost, st));
+        VIO_HIP(ctx, hipStreamSynchronize(st));
+        // status ∧ !IsInPolarRegion ∧ !IsNearBoundary (:117-126; Camera.cpp:120-139)
+        std::vector<int> good;
+        const float m = (float)P.boundary_margin;
+        for (int i = 0; i < n; ++i) {
+            float x = next[2 * i], y = next[2 * i + 1];
+            float vr = y / (float)f->H;
+            bool polar = vr < 0.15f || vr > (1.0f - 0.15f);
+            bool nearb = x < m || x > (float)f->W - m || y < m || y > (float)f->H - m;
+            if (status[i] && !polar && !nearb) good.push_back(i);
+        }
+        std::vector<uint8_t> inl(good.size(), 1);
+        if (good.size() >= 3) {  // RejectOutliersRotationRANSAC (:253-328)
+            const int ng = (int)good.size();
+            std::vector<int32_t> samples(3 * 1000);
+            erp_ransac_samples(P.ransac_seed + (uint32_t)f->frame, ng, 1000, samples.data());
+            std::vector<float> g0(2 * (size_t)ng), g1(2 * (size_t)ng);
+            for (int j = 0; j < ng; ++j) {
+                g0[2 * j] = prev[2 * good[j]]; g0[2 * j + 1] = prev[2 * good[j] + 1];
+                g1[2 * j] = next[2 * good[j]]; g1[2 * j + 1] = next[2 * good[j] + 1];
+            }
+            VIO_HIP(ctx, hipMemcpyAsync(t->d_pts, g0.data(), sizeof(float) * 2 * ng, hipMemcpyHostToDevice, st));
+            VIO_HIP(ctx, hipMemcpyAsync(t->d_next, g1.data(), sizeof(float) * 2 * ng, hipMemcpyHostToDevice, st));
+            VIO_HIP(ctx, hipMemcpyAsync(t->d_samples, samples.data(), sizeof(int32_t) * 3000, hipMemcpyHostToDevice, st));
+            const float thr = (float)(2.0f * M_PI / 180.0f);
+            RansacArgs r = ransac_args(t, ng, 0, 1000, 0, thr, 0.f, 0, t->d_pts, t->d_next);
+            hipError_t e = launch_ransac(r, false, st);
+            if (e != hipSuccess) return hip_fail(ctx, e, "ransac kernels");
+            VIO_HIP(ctx, hipMemcpyAsync(inl.data(), t->d_kept, ng, hipMemcpyDeviceToHost, st));
+            VIO_HIP(ctx, hipStreamSynchronize(st));
+        }
+        std::vector<FeatureRec> cur;
+        for (size_t j = 0; j < good.size(); ++j) {
+            if (!inl[j]) continue;
+            const FeatureRec& pf = f->feats[good[j]];
+            cur.push_back({pf.id, next[2 * good[j]], next[2 * good[j] + 1], pf.track_count + 1, pf.age + 1});
+        }
+        f->feats.swap(cur);
+        f->num_tracked = (int)f->feats.size();
+        if (P.remove_clustered) remove_clustered(f->feats, f->W, f->H, P.clustered_std_ratio);
+        assign_and_limit(f->feats, f->W, f->H, P.grid_cols, P.grid_rows, P.max_features_per_grid);
+        if ((int)f->feats.size() < P.max_features) {  // CreateFeatureMask + DetectNewFeatures (:176-199)
+            std::vector<float> c;
+            if ((rc = frontend_detect(f, c))) return rc;
+            for (size_t i = 0; i < c.size() / 2; ++i) f->feats.push_back({f->next_id++, c[2 * i], c[2 * i + 1], 0, 0});
+            f->num_detected = (int)(c.size() / 2);
+            assign_and_limit(f->feats, f->W, f->H, P.grid_cols, P.grid_rows, P.max_features_per_grid);
+        } else {
+            f->num_detected = 0;
+        }
+    }
+    erp_tracker_swap(t);  // m_prev_image = current (:202)
+    f->frame++;
+    if (n_features) *n_features = (int)f->feats.size();
+    return VIO_OK;
+}
+
+int erp_frontend_features(erp_frontend* f, int32_t* ids, float* xy, int32_t* track_count, int32_t* age, int cap) {
+    if (!f || cap < 0) return VIO_EINVAL;
+    int n = std::min(cap, (int)f->feats.size());
+    for (int i = 0; i < n; ++i) {
+        const FeatureRec& r = f->feats[i];
+        if (ids) ids[i] = r.id;
+        if (xy) { xy[2 * i] = r.x; xy[2 * i + 1] = r.y; }
+        if (track_count) track_count[i] = r.track_count;
+        if (age) age[i] = r.age;
+    }
+    return VIO_OK;
+}
+
+int erp_frontend_stats(erp_frontend* f, int* num_tracked, int* num_detected) {
+    if (!f) return VIO_EINVAL;
+    if (num_tracked) *num_tracked = f->num_tracked;
+    if (num_detected) *num_detected = f->num_detected;
+    return VIO_OK;
+}
+
+}  // extern "C"

@@ -158,6 +158,31 @@ def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
     return out
 
 
+def global_ba_bench(vio, synth, ctx, lm_iters):
+    """Config 5: global BA, 1000 KF x 50k landmarks, 500k observations, dense 5994^2 reduced camera
+    system (RunBA semantics, fix first).  Timed: one solve of exactly lm_iters LM iterations with
+    inputs uploaded once; value = LM iterations per second of that solve."""
+    w = synth.make_global()
+    p = vio.BaProblem(w, variant=vio.VIO_BA_FULL, max_iterations=lm_iters, fixed_iterations=1)
+    ctx.ba_solve([p])  # warm-up (allocations, code objects)
+    t0 = time.perf_counter()
+    r = ctx.ba_solve([p])[0]
+    wall = time.perf_counter() - t0
+    flops = ba_flops_per_iter(p)
+    return {
+        "metric": "global BA LM iterations/s (config 5: 1000 KF x 50k landmarks)",
+        "value": lm_iters / wall,
+        "unit": "LM-iterations/s",
+        "ms_per_iteration": wall / lm_iters * 1e3,
+        "note": "wall time of the whole vio_ba_solve call incl. problem packing/upload and the final "
+                "chi2 pass; fixed iterations",
+        "final_cost_ratio": r["final_cost"] / r["initial_cost"],
+        "roofline": {"bound": "mfma", "achieved": flops * lm_iters / wall / 1e12, "peak": FP64_PEAK / 1e12,
+                     "unit": "TFLOP/s", "frac": flops * lm_iters / wall / FP64_PEAK, "traffic": None,
+                     "flops_per_iteration": flops},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,6 +194,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-klt", action="store_true")
     ap.add_argument("--klt-steps", type=int, default=20)
+    ap.add_argument("--no-global", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -232,6 +258,7 @@ def main():
         single_kms, _ = one.kernel_ms()
         one.close()
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(vio, synth, args.lm_iters, args.cpu_seconds)
+        gba = None if args.no_global else global_ba_bench(vio, synth, ctx, args.lm_iters)
         klt = None if args.no_klt else klt_bench(vio, synth, ctx, args.klt_steps, 3, args.cpu_seconds,
                                                  not args.no_cpu_baseline and world == 1)
         single_ips = args.lm_iters / single_wall
@@ -276,6 +303,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "erp_klt": klt,
+            "global_ba": gba,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

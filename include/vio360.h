@@ -256,6 +256,34 @@ int erp_tracker_stage_ms(erp_tracker* t, double* pyr_ms, double* lk_ms, double* 
                          double* total_ms);
 void erp_tracker_destroy(erp_tracker* t);
 
+/* ------------------------------------------------------------------------------------------ */
+/* FeatureTracker::TrackFeatures as a whole (src/processing/FeatureTracker.cpp:61-206): the device
+   numeric path above plus the reference's host bookkeeping — feature ids (survivors keep theirs,
+   new detections take m_next_feature_id++ in GFTT order), track counts / ages,
+   RemoveClusteredFeatures (:404-497, gated by visualization.highlight_clustered_grid),
+   Frame::AssignFeaturesToGrid / LimitFeaturesPerGrid (src/database/Frame.cpp:108-202, std::sort by
+   track count) and CreateFeatureMask discs (:386-402).  One object per camera stream. */
+typedef struct erp_frontend erp_frontend;
+typedef struct {
+    int32_t max_features;         /* feature_detection.max_features (1000) */
+    float min_distance;           /* feature_detection.min_distance (30) */
+    float quality_level;          /* feature_detection.quality_level (0.01) */
+    int32_t boundary_margin;      /* camera.boundary_margin (20) */
+    int32_t grid_cols, grid_rows; /* Frame grid: feature_detection.grid_cols/rows (20, 10) */
+    int32_t max_features_per_grid;/* feature_detection.max_features_per_grid (10) */
+    int32_t remove_clustered;     /* visualization.highlight_clustered_grid (1) */
+    float clustered_std_ratio;    /* visualization.clustered_std_ratio (0.25 in the yaml) */
+    uint32_t ransac_seed;         /* frame f uses erp_ransac_samples(ransac_seed + f, ...) */
+} erp_frontend_params;
+int erp_frontend_create(vio_ctx* ctx, int W, int H, const erp_frontend_params* p, erp_frontend** out);
+/* process the next frame (u8 W x H); *n_features = features of this frame after the call */
+int erp_frontend_track(erp_frontend* f, const uint8_t* img, int stride, int* n_features);
+/* current frame's features in Frame order: id, pixel, track count, age (any pointer may be NULL) */
+int erp_frontend_features(erp_frontend* f, int32_t* ids, float* xy, int32_t* track_count, int32_t* age, int cap);
+/* GetTrackingStats (FeatureTracker.h): features after tracking, new detections of the last frame */
+int erp_frontend_stats(erp_frontend* f, int* num_tracked, int* num_detected);
+void erp_frontend_destroy(erp_frontend* f);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,3 +77,18 @@ def test_no_device_fails_loudly(vio):
         pytest.skip("GPU present")
     with pytest.raises(vio.VioError):
         vio.Context(0)
+
+
+def test_frontend_params_layout(vio, tmp_path):
+    src = tmp_path / "fe.c"
+    fields = ["max_features", "min_distance", "quality_level", "boundary_margin", "grid_cols", "grid_rows",
+              "max_features_per_grid", "remove_clustered", "clustered_std_ratio", "ransac_seed"]
+    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){",
+             'printf("%zu\\n", sizeof(erp_frontend_params));']
+    lines += [f'printf("%zu\\n", offsetof(erp_frontend_params, {f}));' for f in fields]
+    src.write_text("\n".join(lines + ["return 0;}"]))
+    subprocess.check_call(["gcc", "-o", str(tmp_path / "fe"), str(src)])
+    out = [int(x) for x in subprocess.check_output([str(tmp_path / "fe")]).split()]
+    cls = vio.abi.ErpFrontendParams
+    assert out[0] == C.sizeof(cls)
+    assert out[1:] == [getattr(cls, f).offset for f in fields]
