@@ -210,3 +210,27 @@ def test_ransac_recovers_planted_inliers(vio):
     # fewer than 3 points: all ones (FeatureTracker.cpp:130-134)
     m2, n2 = oracle_lib.rot_ransac(p0[:2], p1[:2], 960, 480, np.zeros(0, np.int32), vio.ransac_threshold())
     assert m2.tolist() == [1, 1] and n2 == 2
+
+
+def test_frontend_oracle_runs(vio, synth):
+    """The TrackFeatures bookkeeping restatement (tests/frontend_oracle.py) on its own: survivors keep
+    their ids and count up, new detections take fresh ids, the grid cap holds."""
+    from frontend_oracle import FrontendOracle
+    W, H = 960, 480
+    prm = vio.default_frontend_params(seed=3)
+    orc = FrontendOracle(vio, W, H, prm)
+    prev_ids, prev_tc = None, None
+    for f in range(3):
+        out = orc.track(synth.render_erp(W, H, synth.rot_yaw_pitch(1.2 * f, 0.3 * f)))
+        ids = out["ids"]
+        assert len(set(ids.tolist())) == len(ids)
+        if prev_ids is not None:
+            kept = np.isin(ids, prev_ids)
+            assert kept.sum() > 100
+            before = dict(zip(prev_ids.tolist(), prev_tc.tolist()))
+            assert all(tc == before[i] + 1 for i, tc in zip(ids[kept].tolist(), out["track_count"][kept].tolist()))
+            assert np.all(ids[~kept] > prev_ids.max()) and np.all(out["track_count"][~kept] == 0)
+        prev_ids, prev_tc = ids, out["track_count"]
+        cells = (np.minimum((out["xy"][:, 1] / np.float32(48)).astype(int), 9) * 20 +
+                 np.minimum((out["xy"][:, 0] / np.float32(48)).astype(int), 19))
+        assert np.bincount(cells).max() <= prm.max_features_per_grid
