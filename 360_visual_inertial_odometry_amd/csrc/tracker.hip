@@ -716,7 +716,9 @@ __global__ void __launch_bounds__(256) gftt_cand_kernel(GfArgs G) {
 // One workgroup.  Accepted corners live in a grid of cell = round(min_dist) with <= 3 per cell.
 constexpr int GS_THREADS = 256;
 constexpr int GS_SLOTS = 3;
-__global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G) {
+__global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const unsigned long long* keys,
+                                                                  const unsigned int* n_keys, unsigned int cap,
+                                                                  int fast) {
     extern __shared__ uint32_t grid_lds[];
     __shared__ int s_good[GS_THREADS];
     __shared__ int s_acc;
@@ -726,7 +728,7 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G) {
     for (int e = threadIdx.x; e < ncell * GS_SLOTS; e += GS_THREADS) grid[e] = 0xffffffffu;
     if (threadIdx.x == 0) { s_acc = 0; s_stop = 0; }
     __syncthreads();
-    const unsigned int total = min(*G.n_cand, G.cand_cap);
+    const unsigned int total = min(*n_keys, cap);
     const int cell = G.cell;
     const double md2 = G.min_dist * G.min_dist;
     auto conflicts = [&](int x, int y, int slot_lane_only) -> bool {
@@ -747,7 +749,7 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G) {
         unsigned int ci = c0 + threadIdx.x;
         int good = 0;
         if (ci < total) {
-            unsigned int idx = (unsigned int)(G.cand_sorted[ci] & 0xffffffffu);
+            unsigned int idx = (unsigned int)(keys[ci] & 0xffffffffu);
             good = !conflicts((int)(idx % G.W), (int)(idx / G.W), 0);
         }
         s_good[threadIdx.x] = good;
@@ -758,7 +760,7 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G) {
             const int nb = min((unsigned int)GS_THREADS, total - c0);
             for (int j = 0; j < nb; ++j) {
                 if (!s_good[j]) continue;
-                unsigned int idx = (unsigned int)(G.cand_sorted[c0 + j] & 0xffffffffu);
+                unsigned int idx = (unsigned int)(keys[c0 + j] & 0xffffffffu);
                 int x = (int)(idx % G.W), y = (int)(idx / G.W);
                 int xc = x / cell, yc = y / cell;
                 // 9 cells x 3 slots = 27 lanes
@@ -794,7 +796,55 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G) {
         __syncthreads();
         if (s_stop) break;
     }
-    if (threadIdx.x == 0) *G.n_out = s_acc;
+    if (threadIdx.x == 0) {
+        *G.n_out = s_acc;
+        // the top-K subset ran dry before max_corners: the exact pass over every candidate must decide
+        if (fast) *G.incomplete = (!s_stop && G.cut[1] == 0) ? 1 : 0;
+    }
+}
+
+// histogram of candidate responses (bucket = float bits >> 20), grid-stride over the candidates
+__global__ void __launch_bounds__(256) gftt_hist_kernel(GfArgs G) {
+    __shared__ unsigned int h[GF_BUCKETS];
+    for (int b = threadIdx.x; b < GF_BUCKETS; b += 256) h[b] = 0;
+    __syncthreads();
+    const unsigned int n = min(*G.n_cand, G.cand_cap);
+    for (unsigned int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+        atomicAdd(&h[(unsigned int)(G.cand[i] >> 52)], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < GF_BUCKETS; b += 256)
+        if (h[b]) atomicAdd(&G.hist[b], h[b]);
+}
+
+// cut bucket: the highest buckets holding >= topk_target candidates (never more than topk_cap)
+__global__ void __launch_bounds__(64) gftt_cut_kernel(GfArgs G) {
+    if (threadIdx.x != 0) return;
+    unsigned int cum = 0;
+    int cut = GF_BUCKETS;  // buckets >= cut form the top set (GF_BUCKETS: empty set)
+    for (int b = GF_BUCKETS - 1; b >= 0; --b) {
+        unsigned int c = G.hist[b];
+        if (c == 0) { cut = b; continue; }
+        if (cum + c > G.topk_cap) break;  // this bucket would overflow the top-K buffer
+        cum += c;
+        cut = b;
+        if (cum >= G.topk_target) break;
+    }
+    unsigned int below = 0;
+    for (int q = 0; q < cut && q < GF_BUCKETS; ++q) below += G.hist[q];
+    G.cut[0] = cut;
+    G.cut[1] = below == 0 ? 1 : 0;  // every candidate is in the top set
+}
+
+__global__ void __launch_bounds__(256) gftt_topk_compact_kernel(GfArgs G) {
+    const unsigned int n = min(*G.n_cand, G.cand_cap);
+    const unsigned int cut = (unsigned int)G.cut[0];
+    for (unsigned int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        unsigned long long k = G.cand[i];
+        if ((unsigned int)(k >> 52) >= cut) {
+            unsigned int pos = atomicAdd(G.n_top, 1u);
+            if (pos < G.topk_cap) G.topk[pos] = k;
+        }
+    }
 }
 
 // rasterise the discs of CreateFeatureMask (cv::circle filled, LINE_8; half-widths precomputed
@@ -847,18 +897,38 @@ hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st) {
     hipLaunchKernelGGL(disc_mask_kernel, dim3(max_pts), dim3(128), 0, st, d);
     return hipGetLastError();
 }
-hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {
-    dim3 blk(256);
+static hipError_t gftt_candidates(const GfArgs& g, hipStream_t st) {
     dim3 grd((g.W + GF_BX - 1) / GF_BX, (g.H + GF_BY - 1) / GF_BY);
-    hipLaunchKernelGGL(gftt_max_kernel, grd, blk, 0, st, g);
-    hipLaunchKernelGGL(gftt_cand_kernel, grd, blk, 0, st, g);
-    // sort all cand_cap slots (unused slots hold 0 and sort to the end)
+    hipLaunchKernelGGL(gftt_max_kernel, grd, dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gftt_cand_kernel, grd, dim3(256), 0, st, g);
+    return hipGetLastError();
+}
+static size_t gftt_select_lds(const GfArgs& g) {
+    return g.grid_global ? 0 : (size_t)g.gw * g.gh * GS_SLOTS * sizeof(uint32_t);
+}
+// fast path: candidates -> histogram -> top-K compaction -> sort of topk_cap keys -> greedy
+hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {
+    hipError_t e = gftt_candidates(g, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(gftt_hist_kernel, dim3(256), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gftt_cut_kernel, dim3(1), dim3(64), 0, st, g);
+    hipLaunchKernelGGL(gftt_topk_compact_kernel, dim3(256), dim3(256), 0, st, g);
+    size_t tb = sort_tmp_bytes;
+    e = hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.topk, g.topk_sorted, (int)g.topk_cap, 0, 64, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(gftt_select_kernel, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
+                       (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
+    return hipGetLastError();
+}
+// exact fallback: sort every candidate slot (unused slots hold 0 and sort to the end) and redo the
+// greedy pass from the strongest candidate
+hipError_t launch_gftt_full(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {
     size_t tb = sort_tmp_bytes;
     hipError_t e = hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.cand, g.cand_sorted, (int)g.cand_cap,
                                                                0, 64, st);
     if (e != hipSuccess) return e;
-    size_t lds = g.grid_global ? 0 : (size_t)g.gw * g.gh * GS_SLOTS * sizeof(uint32_t);
-    hipLaunchKernelGGL(gftt_select_kernel, dim3(1), dim3(GS_THREADS), lds, st, g);
+    hipLaunchKernelGGL(gftt_select_kernel, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
+                       (const unsigned long long*)g.cand_sorted, (const unsigned int*)g.n_cand, g.cand_cap, 0);
     return hipGetLastError();
 }
 size_t gftt_sort_tmp_bytes(unsigned int cap) {

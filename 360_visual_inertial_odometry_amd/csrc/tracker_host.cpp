@@ -74,6 +74,11 @@ struct erp_tracker {
     int* d_halfw = nullptr;
     int halfw_r = -1;
     uint8_t* d_mask = nullptr;  // explicit mask (erp_gftt)
+    // GFTT top-K fast path
+    unsigned int* d_hist = nullptr;
+    unsigned long long *d_topk = nullptr, *d_topk_sorted = nullptr;
+    unsigned int topk_cap = 0;
+    GfArgs last_gf{};           // arguments of the last enqueued GFTT (exact fallback)
     hipEvent_t ev[6] = {};
     bool ran = false;
     std::vector<void*> allocs;
@@ -120,6 +125,10 @@ int ensure_gftt(erp_tracker* t, double min_dist) {
         if ((rc = dalloc(t, &t->d_cand_sorted, sizeof(unsigned long long) * t->cand_cap)) != VIO_OK) return rc;
         t->sort_tmp_bytes = gftt_sort_tmp_bytes(t->cand_cap);
         if ((rc = dalloc(t, (char**)&t->d_sort_tmp, t->sort_tmp_bytes)) != VIO_OK) return rc;
+        t->topk_cap = std::min<unsigned int>(65536u, t->cand_cap);
+        if ((rc = dalloc(t, &t->d_hist, sizeof(unsigned int) * GF_BUCKETS)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_topk, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_topk_sorted, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
     }
     if (min_dist >= 1) {
         int cell = (int)std::lrint(min_dist);
@@ -264,8 +273,21 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
         hipError_t e = gftt_select_set_lds(std::max<size_t>(lds, 4));
         if (e != hipSuccess) return hip_fail(t->ctx, e, "hipFuncSetAttribute(gftt_select)");
     }
+    g.hist = t->d_hist;
+    g.topk = t->d_topk;
+    g.topk_sorted = t->d_topk_sorted;
+    g.n_top = (unsigned int*)(t->d_scal + 6);
+    g.cut = t->d_scal + 7;
+    g.incomplete = t->d_scal + 9;
+    g.topk_cap = t->topk_cap;
+    g.topk_target = (unsigned int)std::min<size_t>(t->topk_cap, std::max<size_t>(4096, 16 * (size_t)max_corners));
+    // scalars [2] max_ord [3] n_cand [4] n_out [6] n_top [7..8] cut [9] incomplete
     VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal + 2, 0, 3 * sizeof(int), t->ctx->stream));
+    VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal + 6, 0, 4 * sizeof(int), t->ctx->stream));
+    VIO_HIP(t->ctx, hipMemsetAsync(t->d_hist, 0, sizeof(unsigned int) * GF_BUCKETS, t->ctx->stream));
+    VIO_HIP(t->ctx, hipMemsetAsync(t->d_topk, 0, sizeof(unsigned long long) * t->topk_cap, t->ctx->stream));
     VIO_HIP(t->ctx, hipMemsetAsync(t->d_cand, 0, sizeof(unsigned long long) * t->cand_cap, t->ctx->stream));
+    t->last_gf = g;
     hipError_t e = launch_gftt(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
     if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt kernels");
     return VIO_OK;
@@ -279,7 +301,14 @@ int upload_frame(erp_tracker* t, int slot, const uint8_t* img, int stride) {
 }
 
 int read_corners(erp_tracker* t, float* out_xy, int* n_out) {
-    int n = 0;
+    int n = 0, inc = 0;
+    VIO_HIP(t->ctx, hipMemcpyAsync(&inc, t->d_scal + 9, sizeof(int), hipMemcpyDeviceToHost, t->ctx->stream));
+    VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    if (inc) {  // the top-K subset did not decide: exact pass over every candidate
+        hipError_t e = launch_gftt_full(t->last_gf, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt exact fallback");
+        VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal + 9, 0, sizeof(int), t->ctx->stream));
+    }
     VIO_HIP(t->ctx, hipMemcpyAsync(&n, t->d_scal + 4, sizeof(int), hipMemcpyDeviceToHost, t->ctx->stream));
     VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
     if (n > 0 && out_xy)

@@ -72,7 +72,18 @@ struct GfArgs {
     uint32_t* grid_global;          // non-null when the selection grid does not fit LDS
     float* corners;                 // [max_corners][2]
     int* n_out;                     // device scalar
+    // top-K fast path: histogram of candidate responses, the strongest candidates compacted and
+    // sorted; `incomplete` is raised when the greedy pass needs candidates beyond them
+    unsigned int* hist;             // [GF_BUCKETS]
+    unsigned long long* topk;       // [topk_cap]
+    unsigned long long* topk_sorted;
+    unsigned int* n_top;            // device scalar
+    int* cut;                       // device scalar: [0] cut bucket [1] everything selected
+    unsigned int topk_cap, topk_target;
+    int* incomplete;                // device scalar
 };
+
+constexpr int GF_BUCKETS = 2048;    // float bits >> 20 of a positive response
 
 struct DiscArgs {
     const float* pts;       // [n][2]
@@ -88,7 +99,9 @@ hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int fra
 hipError_t launch_lk(const LkArgs& a, hipStream_t st);
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st);
 hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st);
+// fast path (top-K) and the exact fallback over every candidate (used when `incomplete` is raised)
 hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st);
+hipError_t launch_gftt_full(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st);
 size_t gftt_sort_tmp_bytes(unsigned int cap);
 hipError_t gftt_select_set_lds(size_t bytes);
 
