@@ -262,7 +262,9 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     g.cand = t->d_cand; g.cand_sorted = t->d_cand_sorted;
     g.n_cand = (unsigned int*)(t->d_scal + 3);
     g.cand_cap = t->cand_cap;
-    g.cell = min_dist >= 1 ? (int)std::lrint(min_dist) : 1;
+    // minDistance < 1: every candidate is accepted in order (featureselect.cpp), no grid needed — one
+    // cell covering the image keeps the selection kernel's conflict test trivially false
+    g.cell = min_dist >= 1 ? (int)std::lrint(min_dist) : std::max(t->W, t->H);
     g.gw = (t->W + g.cell - 1) / g.cell;
     g.gh = (t->H + g.cell - 1) / g.cell;
     size_t lds = (size_t)g.gw * g.gh * 3 * sizeof(uint32_t);
