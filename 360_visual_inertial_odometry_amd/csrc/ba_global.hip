@@ -346,52 +346,56 @@ __global__ void __launch_bounds__(GT) gba_rhs_kernel(GbaArgs A) {
 constexpr int NB = 64;
 using d4 = __attribute__((ext_vector_type(4))) double;
 
-// diagonal block: in-LDS right-looking Cholesky + lower-triangular inverse (for TRSM / TRSV)
+// diagonal block: in-LDS right-looking Cholesky + lower-triangular inverse (for TRSM / TRSV).
+// One barrier per column: the trailing update reads the unscaled column j (T[i][c] -= T[i][j] T[c][j] / d)
+// and the column is scaled after the barrier, which the next column's update never touches.
 __global__ void __launch_bounds__(256) chol_diag_kernel(double* S, int n, int k, double* Linv, int* fail) {
     __shared__ double T[NB][NB + 1];
     __shared__ double Iv[NB][NB + 1];
-    __shared__ int bad;
+    __shared__ double rdiag[NB];
     double* blk = S + (size_t)k * NB * n + (size_t)k * NB;
     for (int e = threadIdx.x; e < NB * NB; e += 256) {
-        int r = e / NB, c = e % NB;
+        int r = e >> 6, c = e & 63;
         T[r][c] = c <= r ? blk[(size_t)r * n + c] : 0.0;
     }
-    if (threadIdx.x == 0) bad = 0;
     __syncthreads();
+    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    bool ok = true;
     for (int j = 0; j < NB; ++j) {
-        double d = T[j][j];
-        if (!(d > 0.0)) { if (threadIdx.x == 0) bad = 1; }
-        __syncthreads();
-        if (bad) break;
-        double sd = sqrt(d);
-        // column j below the diagonal, then the trailing update
-        for (int r = j + 1 + threadIdx.x; r < NB; r += 256) T[r][j] /= sd;
-        __syncthreads();
-        if (threadIdx.x == 0) T[j][j] = sd;
-        for (int e = threadIdx.x; e < (NB - j - 1) * (NB - j - 1); e += 256) {
-            int r = j + 1 + e / (NB - j - 1), c = j + 1 + e % (NB - j - 1);
-            if (c <= r) T[r][c] -= T[r][j] * T[c][j];
+        const double d = T[j][j];  // uniform: every thread reads the same LDS word
+        if (!(d > 0.0)) { ok = false; break; }
+        const double id = 1.0 / d;
+        for (int i = j + 1 + ty; i < NB; i += 16) {
+            const double lij = T[i][j] * id;
+            for (int c = j + 1 + tx; c <= i; c += 16) T[i][c] -= lij * T[c][j];
         }
         __syncthreads();
+        const double sd = sqrt(d), isd = 1.0 / sd;
+        for (int i = j + 1 + threadIdx.x; i < NB; i += 256) T[i][j] *= isd;
+        if (threadIdx.x == 0) { T[j][j] = sd; rdiag[j] = isd; }
     }
-    if (bad) {
+    if (!ok) {
         if (threadIdx.x == 0) *fail = 1;
         return;
     }
-    // inverse of the lower-triangular T: column c solves T x = e_c (one thread per column)
-    for (int c = threadIdx.x; c < NB; c += 256) {
-        for (int r = 0; r < NB; ++r) {
-            double s = (r == c) ? 1.0 : 0.0;
-            for (int q = c; q < r; ++q) s -= T[r][q] * Iv[q][c];
-            Iv[r][c] = r < c ? 0.0 : s / T[r][r];
-        }
-    }
     __syncthreads();
+    // inverse X = T^-1 row by row: X[r][c] = (delta_rc - sum_{c<=q<r} T[r][q] X[q][c]) / T[r][r];
+    // thread = (column c, quarter p) splits the q-sum, two shuffles combine the quarters
+    const int c = threadIdx.x >> 2, p = threadIdx.x & 3;
+    for (int r = 0; r < NB; ++r) {
+        double s = 0.0;
+        if (c < r)
+            for (int q = c + p; q < r; q += 4) s += T[r][q] * Iv[q][c];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        if (p == 0) Iv[r][c] = c > r ? 0.0 : ((r == c ? 1.0 : 0.0) - s) * rdiag[r];
+        __syncthreads();
+    }
     double* Li = Linv + (size_t)k * NB * NB;
     for (int e = threadIdx.x; e < NB * NB; e += 256) {
-        int r = e / NB, c = e % NB;
-        if (c <= r) blk[(size_t)r * n + c] = T[r][c];
-        Li[e] = Iv[r][c];
+        int r = e >> 6, cc = e & 63;
+        if (cc <= r) blk[(size_t)r * n + cc] = T[r][cc];
+        Li[e] = Iv[r][cc];
     }
 }
 
@@ -477,7 +481,8 @@ __global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k,
 }
 
 // forward substitution step k: y_k = Linv_kk b_k (every block recomputes it from the final b_k;
-// block 0 publishes it), b_i -= L_ik y_k for the rows below
+// block 0 publishes it), then b_r -= L_rk y_k for the rows below: one wavefront per row, coalesced
+// 512-B row segment, shuffle reduction
 __global__ void __launch_bounds__(256) trsv_fwd_kernel(const double* S, int n, int k, const double* Linv, double* b,
                                                        double* y) {
     __shared__ double yk[NB];
@@ -489,19 +494,22 @@ __global__ void __launch_bounds__(256) trsv_fwd_kernel(const double* S, int n, i
     }
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x < NB) y[k * NB + threadIdx.x] = yk[threadIdx.x];
-    int r = (k + 1) * NB + blockIdx.x * 256 + threadIdx.x;
-    if (r < n) {
-        const double* row = S + (size_t)r * n + (size_t)k * NB;
-        double s = 0.0;
-        for (int q = 0; q < NB; ++q) s += row[q] * yk[q];
-        b[r] -= s;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const double ylane = yk[lane];
+    for (int r = (k + 1) * NB + blockIdx.x * 16 + wid; r < n && r < (k + 1) * NB + (blockIdx.x + 1) * 16; r += 4) {
+        double s = S[(size_t)r * n + (size_t)k * NB + lane] * ylane;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (lane == 0) b[r] -= s;
     }
 }
 
-// backward substitution step k (k = nblk-1 .. 0): x_k = Linv_kk^T y_k, y_j -= L_kj^T x_k for j < k
+// backward substitution step k (k = nblk-1 .. 0): x_k = Linv_kk^T y_k, y_c -= sum_q L[kNB+q][c] x_k[q]
+// for c < kNB: 64 columns per block, the q-sum split over 4 thread groups and combined in LDS
 __global__ void __launch_bounds__(256) trsv_bwd_kernel(const double* S, int n, int k, const double* Linv, double* y,
                                                        double* x) {
     __shared__ double xk[NB];
+    __shared__ double part[4][64];
     const double* Li = Linv + (size_t)k * NB * NB;
     if (threadIdx.x < NB) {
         double s = 0.0;
@@ -510,12 +518,14 @@ __global__ void __launch_bounds__(256) trsv_bwd_kernel(const double* S, int n, i
     }
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x < NB) x[k * NB + threadIdx.x] = xk[threadIdx.x];
-    int c = blockIdx.x * 256 + threadIdx.x;  // column c < k*NB of row-block k
-    if (c < k * NB) {
-        double s = 0.0;
-        for (int q = 0; q < NB; ++q) s += S[(size_t)(k * NB + q) * n + c] * xk[q];
-        y[c] -= s;
-    }
+    const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    double s = 0.0;
+    if (c < k * NB)
+        for (int q = g * 16; q < g * 16 + 16; ++q) s += S[(size_t)(k * NB + q) * n + c] * xk[q];
+    part[g][cl] = s;
+    __syncthreads();
+    if (g == 0 && c < k * NB) y[c] -= (part[0][cl] + part[1][cl]) + (part[2][cl] + part[3][cl]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -697,13 +707,13 @@ hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
     for (int k = 0; k < nblk; ++k) {
         int rows = n - (k + 1) * NB;
-        int nb = rows > 0 ? (rows + 255) / 256 : 1;
+        int nb = rows > 0 ? (rows + 15) / 16 : 1;
         hipLaunchKernelGGL(trsv_fwd_kernel, dim3(nb), dim3(256), 0, s, (const double*)A.S, n, k,
                            (const double*)A.Linv, A.bf, A.yv);
     }
     for (int k = nblk - 1; k >= 0; --k) {
         int cols = k * NB;
-        int nb = cols > 0 ? (cols + 255) / 256 : 1;
+        int nb = cols > 0 ? (cols + 63) / 64 : 1;
         hipLaunchKernelGGL(trsv_bwd_kernel, dim3(nb), dim3(256), 0, s, (const double*)A.S, n, k,
                            (const double*)A.Linv, A.yv, A.xf);
     }
