@@ -52,6 +52,7 @@ struct __align__(16) BaShared {
     unsigned long long prof_acc[16];
     unsigned long long prof_last;
     int prof_on;
+    int chol_bad;
 };
 
 // per-phase shader-clock accounting (diagnostic; enabled when BaPools::prof != nullptr)
@@ -562,51 +563,50 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     __syncthreads();
 }
 
-// right-looking Cholesky of S (nf x nf, LDS) then solve S y = b (y overwrites b).
-// Returns false (uniformly) when S is not positive definite.
+// Cholesky of S (nf x nf, LDS, nf <= 128) then solve S y = b (y overwrites b).
+// Left-looking and wave-synchronous: wave 0 alone computes column j for its rows i = lane, lane+64
+// (L[i][j] = (S[i][j] - sum_k L[i][k] L[j][k]) / L[j][j]) with no workgroup barrier per column;
+// the other waves wait at one barrier.  Returns false (uniformly) when S is not positive definite.
 __device__ bool cholesky_solve(BaShared& sh, int nf) {
     double* S = sh.S;
-    for (int j = 0; j < nf; ++j) {
-        double d2 = S[j * nf + j];
-        if (!(d2 > 0.0)) return false;  // uniform: every thread read the same value
-        double inv = 1.0 / d2;
-        // trailing update of the lower triangle (i >= k > j): thread (ty, tx) of a 16x16 grid
-        // walks rows j+1+ty+16a and columns j+1+tx+16b
-#ifdef CHOL_OLD
-        {
-            int m = nf - j - 1;
-            int cnt = m * (m + 1) / 2;
-            for (int e = threadIdx.x; e < cnt; e += BA_THREADS) {
-                int ii = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                while ((ii + 1) * (ii + 2) / 2 <= e) ++ii;
-                while (ii * (ii + 1) / 2 > e) --ii;
-                int kk = e - ii * (ii + 1) / 2;
-                int i = j + 1 + ii, k = j + 1 + kk;
-                S[i * nf + k] -= S[i * nf + j] * S[k * nf + j] * inv;
+    int& chol_bad = sh.chol_bad;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        int bad = 0;
+        for (int j = 0; j < nf && !bad; ++j) {
+            const double* Lj = S + j * nf;
+            double s0 = 0.0, s1 = 0.0;  // rows i0 = lane, i1 = lane + 64 (only i >= j matter)
+            const int i0 = lane, i1 = lane + 64;
+            const bool a0 = i0 >= j && i0 < nf, a1 = i1 >= j && i1 < nf;
+            if (a0) {
+                const double* Li = S + i0 * nf;
+                double p0 = 0.0, p1 = 0.0;
+                int k = 0;
+                for (; k + 1 < j; k += 2) { p0 += Li[k] * Lj[k]; p1 += Li[k + 1] * Lj[k + 1]; }
+                if (k < j) p0 += Li[k] * Lj[k];
+                s0 = Li[j] - (p0 + p1);
             }
-        }
-#else
-        {
-            const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
-            for (int i = j + 1 + ty; i < nf; i += 16) {
-                const double lij = S[i * nf + j] * inv;
-                for (int k = j + 1 + tx; k <= i; k += 16) S[i * nf + k] -= lij * S[k * nf + j];
+            if (a1) {
+                const double* Li = S + i1 * nf;
+                double p0 = 0.0, p1 = 0.0;
+                int k = 0;
+                for (; k + 1 < j; k += 2) { p0 += Li[k] * Lj[k]; p1 += Li[k + 1] * Lj[k + 1]; }
+                if (k < j) p0 += Li[k] * Lj[k];
+                s1 = Li[j] - (p0 + p1);
             }
+            const double d = j < 64 ? __shfl(s0, j, 64) : __shfl(s1, j - 64, 64);
+            if (!(d > 0.0)) { bad = 1; break; }
+            const double ld = sqrt(d), il = 1.0 / ld;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            if (a0) S[i0 * nf + j] = i0 == j ? ld : s0 * il;
+            if (a1) S[i1 * nf + j] = i1 == j ? ld : s1 * il;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-#endif
-        // scale column j-1 (not read by this step)
-        if (j > 0) {
-            double dprev = S[(j - 1) * nf + (j - 1)];
-            double sd = sqrt(dprev);
-            for (int i = j + threadIdx.x; i < nf; i += BA_THREADS) S[i * nf + (j - 1)] /= sd;
-        }
-        __syncthreads();
-        if (j > 0 && threadIdx.x == 0) S[(j - 1) * nf + (j - 1)] = sqrt(S[(j - 1) * nf + (j - 1)]);
-        __syncthreads();
+        if (lane == 0) chol_bad = bad;
     }
-    // last column
-    if (threadIdx.x == 0) S[(nf - 1) * nf + (nf - 1)] = sqrt(S[(nf - 1) * nf + (nf - 1)]);
     __syncthreads();
+    if (chol_bad) return false;
     // triangular solves by wave 0 (wave-synchronous); rows owned lane, lane+64
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
