@@ -138,7 +138,7 @@ int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
     w.nf = off;
     w.ni = w.nf - w.np;
     if (w.nf > BA_NF_MAX) { set_error(ctx, "reduced system larger than 96 parameters"); return VIO_ENOSYS; }
-    w.T = (w.np + 1 + 15) / 16;
+    w.T = (w.np + 15) / 16;
     if (w.T < 1) w.T = 1;
     w.npad = 16 * w.T;
     w.n_imu = 0;

@@ -35,10 +35,9 @@ struct LmState {
 };
 
 struct __align__(16) BaShared {
-    double S[BA_NF_MAX * BA_NF_MAX];
-    double At[BA_KC * BA_NF_MAX];
-    double Bt[BA_KC * BA_NF_MAX];
-    double gcol[BA_KC];
+    double S[BA_NF_MAX * (BA_NF_MAX + 1)];  // row stride nf|1 (odd: conflict-free column walks)
+    double stage[BA_STAGE];      // Schur panels At | Bt (k-major, see schur_gemm)
+    double gcol[BA_GCOL];
     double b[BA_NF_MAX], s_f[BA_NF_MAX], g_f[BA_NF_MAX], colsq_f[BA_NF_MAX], D_f[BA_NF_MAX];
     double U[BA_KMAX][27];
     double pc[BA_KMAX][36];      // Rwb(9) twb(3) Rbw(9) tbw(3) Rcw(9) tcw(3) at the point being evaluated
@@ -54,9 +53,10 @@ struct __align__(16) BaShared {
     int prof_on;
     int chol_bad;
 };
+static_assert(sizeof(BaShared) <= 160 * 1024, "BaShared exceeds the 160 KB LDS of a gfx950 CU");
 
 // per-phase shader-clock accounting (diagnostic; enabled when BaPools::prof != nullptr)
-enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST };
+enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST, PF_FILL };
 __device__ __forceinline__ void prof_mark(BaShared& sh, int slot) {
     if (sh.prof_on && threadIdx.x == 0) {
         unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -473,27 +473,66 @@ __device__ void linearise(BaShared& sh, const WinCtx& c, bool first) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Schur GEMM: S_pp -= Y W^T and b_p -= Y g over landmark chunks (Y = W~ V~^-1).
+// Schur GEMM: S_pp -= Y W^T and b_p -= Y g over landmark chunks (Y = W~ V~^-1), on
+// v_mfma_f64_16x16x4_f64.  Per chunk of LC landmarks the obs lanes scatter their 6x3 Y / W blocks into
+// k-major LDS panels At/Bt (k = 3*landmark + component, one row of npad pose columns per k; rows of
+// unobserved / constant poses stay zero); each wave then owns a fixed set of the lower-triangle
+// 16x16 output tiles (S is only read on and below the diagonal by the Cholesky) and accumulates them
+// across all chunks in registers; the rhs column runs on the VALU beside it.  Fixed per-lane k order
+// plus a fixed shuffle tree: bitwise reproducible.
+using d4 = __attribute__((ext_vector_type(4))) double;
+
+__host__ __device__ constexpr int schur_ks(int T) { return (T & 1) ? 16 * T : 16 * T + 16; }
+__host__ __device__ constexpr int schur_kc(int LC) { return (3 * LC + 3) & ~3; }
+__host__ __device__ constexpr int schur_lc(int T) {
+    int lc = 1;
+    while (2 * schur_kc(lc + 1) * schur_ks(T) <= BA_STAGE && schur_kc(lc + 1) <= BA_GCOL) ++lc;
+    return lc;
+}
+
 template <int T>
 __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
-    const int N = w.N, L = w.L;
-    const int npad = 16 * T;
-    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    const int N = w.N, L = w.L, np = w.np;
+    constexpr int KS = schur_ks(T);    // k-row stride (doubles): the 4 k-rows of a fragment hit both bank halves
+    constexpr int LC = schur_lc(T);    // landmarks per chunk
+    constexpr int KC = schur_kc(LC);   // k rows per chunk (multiple of 4)
+    constexpr int NT = T * (T + 1) / 2;
+    constexpr int TPW = (NT + 3) / 4;  // lower tiles per wave
+    constexpr int RPW = (T + 3) / 4;   // rhs row groups per wave
+    static_assert(2 * KC * KS <= BA_STAGE && KC <= BA_GCOL, "Schur staging exceeds LDS panel");
+    double* At = sh.stage;
+    double* Bt = sh.stage + KC * KS;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r16 = lane & 15, kk = lane >> 4;
     const double* jp = c.ws + c.L.jp;
     const double* jl = c.ws + c.L.jl;
     const double* Vi = c.ws + c.L.Vi;
     const double* gl = c.ws + c.L.gl;
     const double* sl = c.ws + c.L.s_l;
-    double acc[T][T];
+    int trow[TPW], tcol[TPW];
 #pragma unroll
-    for (int i = 0; i < T; ++i)
+    for (int m = 0; m < TPW; ++m) {
+        int t = wid + 4 * m, r = 0;
+        if (t >= NT) { trow[m] = -1; tcol[m] = 0; continue; }
+        while (t > r) { t -= r + 1; ++r; }
+        trow[m] = r; tcol[m] = t;
+    }
+    d4 acc[TPW];
 #pragma unroll
-        for (int j = 0; j < T; ++j) acc[i][j] = 0.0;
-    for (int l0 = 0; l0 < L; l0 += BA_LC) {
-        const int l1 = min(l0 + BA_LC, L);
-        // zero staging
-        for (int e = threadIdx.x; e < BA_KC * npad; e += BA_THREADS) { sh.At[e] = 0.0; sh.Bt[e] = 0.0; }
+    for (int m = 0; m < TPW; ++m) acc[m] = d4{0.0, 0.0, 0.0, 0.0};
+    double bacc[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) bacc[q] = 0.0;
+    for (int l0 = 0; l0 < L; l0 += LC) {
+        const int l1 = min(l0 + LC, L);
+        for (int e = threadIdx.x; e < 2 * KC * KS; e += BA_THREADS) sh.stage[e] = 0.0;
+        for (int e = threadIdx.x; e < KC; e += BA_THREADS) {
+            const int l = l0 + e / 3, cc = e % 3;
+            double v = 0.0;
+            if (l < l1 && c.lm_var[l]) v = gl[(int64_t)cc * L + l] * sl[(int64_t)cc * L + l];
+            sh.gcol[e] = v;
+        }
         __syncthreads();
         const int o0 = c.lm_ptr[l0], o1 = c.lm_ptr[l1];
         for (int o = o0 + threadIdx.x; o < o1; o += BA_THREADS) {
@@ -516,70 +555,77 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
                 double Y1 = W0 * vi[1] + W1 * vi[3] + W2 * vi[4];
                 double Y2 = W0 * vi[2] + W1 * vi[4] + W2 * vi[5];
                 int row = pf + i;
-                sh.At[(3 * j + 0) * npad + row] = Y0;
-                sh.At[(3 * j + 1) * npad + row] = Y1;
-                sh.At[(3 * j + 2) * npad + row] = Y2;
-                sh.Bt[(3 * j + 0) * npad + row] = W0;
-                sh.Bt[(3 * j + 1) * npad + row] = W1;
-                sh.Bt[(3 * j + 2) * npad + row] = W2;
-            }
-        }
-        // rhs column (index np in B): g~_l
-        for (int jj = threadIdx.x; jj < BA_LC; jj += BA_THREADS) {
-            int l = l0 + jj;
-            for (int cc = 0; cc < 3; ++cc) {
-                double v = 0.0;
-                if (l < l1 && c.lm_var[l]) v = gl[(int64_t)cc * L + l] * sl[(int64_t)cc * L + l];
-                sh.Bt[(3 * jj + cc) * npad + w.np] = v;
+                At[(3 * j + 0) * KS + row] = Y0;
+                At[(3 * j + 1) * KS + row] = Y1;
+                At[(3 * j + 2) * KS + row] = Y2;
+                Bt[(3 * j + 0) * KS + row] = W0;
+                Bt[(3 * j + 1) * KS + row] = W1;
+                Bt[(3 * j + 2) * KS + row] = W2;
             }
         }
         __syncthreads();
-        const int kc = 3 * (l1 - l0);
-        for (int cidx = 0; cidx < kc; ++cidx) {
-            double a[T], b[T];
+        prof_mark(sh, PF_FILL);
+        const int nsteps = (3 * (l1 - l0) + 3) >> 2;
+        for (int st = 0; st < nsteps; ++st) {
+            const int kr = (4 * st + kk) * KS;
 #pragma unroll
-            for (int i = 0; i < T; ++i) a[i] = sh.At[cidx * npad + ty * T + i];
+            for (int m = 0; m < TPW; ++m) {
+                if (trow[m] < 0) continue;
+                const double a = At[kr + 16 * trow[m] + r16];
+                const double b = Bt[kr + 16 * tcol[m] + r16];
+                acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[m], 0, 0, 0);
+            }
+            const double g = sh.gcol[4 * st + kk];
 #pragma unroll
-            for (int j = 0; j < T; ++j) b[j] = sh.Bt[cidx * npad + tx * T + j];
-#pragma unroll
-            for (int i = 0; i < T; ++i)
-#pragma unroll
-                for (int j = 0; j < T; ++j) acc[i][j] += a[i] * b[j];
+            for (int q = 0; q < RPW; ++q) {
+                const int rg = wid + 4 * q;
+                if (rg < T) bacc[q] += At[kr + 16 * rg + r16] * g;
+            }
         }
         __syncthreads();
+        prof_mark(sh, PF_GEMM);
     }
-    const int nf = w.nf;
+    const int ls = w.nf | 1;
 #pragma unroll
-    for (int i = 0; i < T; ++i) {
-        int row = ty * T + i;
-        if (row >= w.np) continue;
+    for (int m = 0; m < TPW; ++m) {
+        if (trow[m] < 0) continue;
+        const int col = 16 * tcol[m] + r16;
 #pragma unroll
-        for (int j = 0; j < T; ++j) {
-            int col = tx * T + j;
-            if (col < w.np) sh.S[row * nf + col] -= acc[i][j];
-            else if (col == w.np) sh.b[row] -= acc[i][j];
+        for (int r = 0; r < 4; ++r) {
+            const int row = 16 * trow[m] + 4 * r + kk;
+            if (row < np && col < np) sh.S[row * ls + col] -= acc[m][r];
         }
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        double v = bacc[q];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        const int row = 16 * (wid + 4 * q) + r16;
+        if (kk == 0 && wid + 4 * q < T && row < np) sh.b[row] -= v;
     }
     __syncthreads();
 }
 
-// Cholesky of S (nf x nf, LDS, nf <= 128) then solve S y = b (y overwrites b).
+// Cholesky of S (nf x nf, LDS, nf <= 128, row stride ls = nf|1) then solve S y = b (y overwrites b).
 // Left-looking and wave-synchronous: wave 0 alone computes column j for its rows i = lane, lane+64
 // (L[i][j] = (S[i][j] - sum_k L[i][k] L[j][k]) / L[j][j]) with no workgroup barrier per column;
-// the other waves wait at one barrier.  Returns false (uniformly) when S is not positive definite.
+// the other waves wait at one barrier.  The odd row stride makes the per-lane row walks hit 32
+// distinct bank pairs.  Returns false (uniformly) when S is not positive definite.
 __device__ bool cholesky_solve(BaShared& sh, int nf) {
     double* S = sh.S;
+    const int ls = nf | 1;
     int& chol_bad = sh.chol_bad;
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         int bad = 0;
         for (int j = 0; j < nf && !bad; ++j) {
-            const double* Lj = S + j * nf;
+            const double* Lj = S + j * ls;
             double s0 = 0.0, s1 = 0.0;  // rows i0 = lane, i1 = lane + 64 (only i >= j matter)
             const int i0 = lane, i1 = lane + 64;
             const bool a0 = i0 >= j && i0 < nf, a1 = i1 >= j && i1 < nf;
             if (a0) {
-                const double* Li = S + i0 * nf;
+                const double* Li = S + i0 * ls;
                 double p0 = 0.0, p1 = 0.0;
                 int k = 0;
                 for (; k + 1 < j; k += 2) { p0 += Li[k] * Lj[k]; p1 += Li[k + 1] * Lj[k + 1]; }
@@ -587,7 +633,7 @@ __device__ bool cholesky_solve(BaShared& sh, int nf) {
                 s0 = Li[j] - (p0 + p1);
             }
             if (a1) {
-                const double* Li = S + i1 * nf;
+                const double* Li = S + i1 * ls;
                 double p0 = 0.0, p1 = 0.0;
                 int k = 0;
                 for (; k + 1 < j; k += 2) { p0 += Li[k] * Lj[k]; p1 += Li[k + 1] * Lj[k + 1]; }
@@ -598,8 +644,8 @@ __device__ bool cholesky_solve(BaShared& sh, int nf) {
             if (!(d > 0.0)) { bad = 1; break; }
             const double ld = sqrt(d), il = 1.0 / ld;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            if (a0) S[i0 * nf + j] = i0 == j ? ld : s0 * il;
-            if (a1) S[i1 * nf + j] = i1 == j ? ld : s1 * il;
+            if (a0) S[i0 * ls + j] = i0 == j ? ld : s0 * il;
+            if (a1) S[i1 * ls + j] = i1 == j ? ld : s1 * il;
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
@@ -614,19 +660,19 @@ __device__ bool cholesky_solve(BaShared& sh, int nf) {
         double b1 = lane + 64 < nf ? sh.b[lane + 64] : 0.0;
         for (int j = 0; j < nf; ++j) {
             double bj = j < 64 ? __shfl(b0, j, 64) : __shfl(b1, j - 64, 64);
-            double yj = bj / S[j * nf + j];
+            double yj = bj / S[j * ls + j];
             if (lane == j) b0 = yj;
             if (lane + 64 == j) b1 = yj;
-            if (lane > j && lane < nf) b0 -= S[lane * nf + j] * yj;
-            if (lane + 64 > j && lane + 64 < nf) b1 -= S[(lane + 64) * nf + j] * yj;
+            if (lane > j && lane < nf) b0 -= S[lane * ls + j] * yj;
+            if (lane + 64 > j && lane + 64 < nf) b1 -= S[(lane + 64) * ls + j] * yj;
         }
         for (int j = nf - 1; j >= 0; --j) {
             double bj = j < 64 ? __shfl(b0, j, 64) : __shfl(b1, j - 64, 64);
-            double yj = bj / S[j * nf + j];
+            double yj = bj / S[j * ls + j];
             if (lane == j) b0 = yj;
             if (lane + 64 == j) b1 = yj;
-            if (lane < j) b0 -= S[j * nf + lane] * yj;
-            if (lane + 64 < j) b1 -= S[j * nf + lane + 64] * yj;
+            if (lane < j) b0 -= S[j * ls + lane] * yj;
+            if (lane + 64 < j) b1 -= S[j * ls + lane + 64] * yj;
         }
         if (lane < nf) sh.b[lane] = b0;
         if (lane + 64 < nf) sh.b[lane + 64] = b1;
@@ -638,7 +684,7 @@ __device__ bool cholesky_solve(BaShared& sh, int nf) {
 // One LM step computation (ComputeTrustRegionStep): returns validity uniformly via sh.st.valid.
 __device__ void compute_step(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
-    const int N = w.N, L = w.L, nf = w.nf;
+    const int N = w.N, L = w.L, nf = w.nf, ls = nf | 1;
     const double radius = sh.st.radius;
     const double dmin = 1e-6, dmax = 1e32;
     double* Vi = c.ws + c.L.Vi;
@@ -685,7 +731,7 @@ __device__ void compute_step(BaShared& sh, const WinCtx& c) {
         sh.D_f[f] = sqrt(d / radius);
         sh.b[f] = sh.s_f[f] * sh.g_f[f];
     }
-    for (int e = threadIdx.x; e < nf * nf; e += BA_THREADS) sh.S[e] = 0.0;
+    for (int e = threadIdx.x; e < nf * ls; e += BA_THREADS) sh.S[e] = 0.0;
     __syncthreads();
     for (int k = 0; k < w.K; ++k) {
         int pf = w.pose_f[k];
@@ -694,18 +740,18 @@ __device__ void compute_step(BaShared& sh, const WinCtx& c) {
             int i = e / 6, j = e % 6;
             int a = min(i, j), b = max(i, j);
             int idx = a * 6 - (a * (a - 1)) / 2 + (b - a);
-            sh.S[(pf + i) * nf + pf + j] = sh.U[k][idx] * sh.s_f[pf + i] * sh.s_f[pf + j];
+            sh.S[(pf + i) * ls + pf + j] = sh.U[k][idx] * sh.s_f[pf + i] * sh.s_f[pf + j];
         }
     }
     if (w.is_vi) {
         const int ni = w.ni, np = w.np;
         for (int e = threadIdx.x; e < ni * ni; e += BA_THREADS) {
             int p = e / ni, q = e % ni;
-            sh.S[(np + p) * nf + np + q] = c.Himu[e] * sh.s_f[np + p] * sh.s_f[np + q];
+            sh.S[(np + p) * ls + np + q] = c.Himu[e] * sh.s_f[np + p] * sh.s_f[np + q];
         }
     }
     __syncthreads();
-    for (int f = threadIdx.x; f < nf; f += BA_THREADS) sh.S[f * nf + f] += sh.D_f[f] * sh.D_f[f];
+    for (int f = threadIdx.x; f < nf; f += BA_THREADS) sh.S[f * ls + f] += sh.D_f[f] * sh.D_f[f];
     double anybad = block_max((double)bad, sh.redm);
     if (anybad > 0.0) {
         if (threadIdx.x == 0) sh.st.valid = 0;

@@ -60,7 +60,7 @@ def all_cases(vio, synth):
     return cases(vio, synth)
 
 
-def assert_parity_vi_converged(vio, w, o, g):
+def assert_parity_vi_converged(vio, w, o, g, **kw):
     """VI windows with the reference's IMU information (the rotation block of the preintegrated
     covariance is never propagated, IMUPreintegrator.cpp:240-274, so its sqrt-information is 1e4)
     are ill-conditioned near the optimum: a 1e-13 relative perturbation of the input moves the
@@ -71,7 +71,7 @@ def assert_parity_vi_converged(vio, w, o, g):
     within 1e-3 m / 1e-2 m / 1e-4 rel cost absolutely).  The fixed-iteration trajectory itself is
     compared at the tight bar (test_ba_parity_fixed_iterations)."""
     w2 = dict(w, lm_xyz=w["lm_xyz"] * (1 + 1e-13))
-    o2 = oracle_lib.ba_solve(vio, vio.BaProblem(w2, variant=vio.VIO_BA_VI))
+    o2 = oracle_lib.ba_solve(vio, vio.BaProblem(w2, variant=vio.VIO_BA_VI, **kw))
     dt_self = np.abs(o["T_wb"][:, :3, 3] - o2["T_wb"][:, :3, 3]).max()
     dl_self = np.abs(o["lm_xyz"] - o2["lm_xyz"]).max()
     dc_self = abs(o["final_cost"] - o2["final_cost"])
@@ -102,7 +102,7 @@ def test_ba_parity_reference_options(vio, gpu_ctx, all_cases, idx):
         assert g["final_cost"] < g["initial_cost"]
 
 
-@pytest.mark.parametrize("idx,iters", [(0, 10), (2, 10), (3, 10), (2, 30), (5, 40)])
+@pytest.mark.parametrize("idx,iters", [(0, 10), (2, 10), (3, 10), (2, 30), (5, 20)])
 def test_ba_parity_fixed_iterations(vio, gpu_ctx, all_cases, idx, iters):
     """Benchmark mode (exactly `iters` LM iterations, tolerances off) — the timed configuration, and
     long VI trajectories through accepted and rejected steps."""
@@ -114,6 +114,20 @@ def test_ba_parity_fixed_iterations(vio, gpu_ctx, all_cases, idx, iters):
     assert (o["num_successful_steps"], o["num_unsuccessful_steps"]) == \
         (g["num_successful_steps"], g["num_unsuccessful_steps"])
     assert_parity(o, g, p.c.chi2_threshold, iters_tol=0)
+
+
+def test_ba_vi_long_fixed_trajectory(vio, gpu_ctx, all_cases):
+    """40 fixed LM iterations on a VI window run past convergence, where accept / reject decisions
+    are made on roundoff-sized cost changes (the oracle's own 1e-13-perturbed run flips them too):
+    judged at the oracle self-sensitivity bar, with the iteration count exact."""
+    name, w, var = all_cases[5]
+    assert var == vio.VIO_BA_VI
+    kw = dict(max_iterations=40, fixed_iterations=1)
+    p = vio.BaProblem(w, variant=var, **kw)
+    o = oracle_lib.ba_solve(vio, p)
+    g = gpu_ctx.ba_solve([p])[0]
+    assert o["iterations"] == g["iterations"] == 41
+    assert_parity_vi_converged(vio, w, o, g, **kw)
 
 
 def test_batched_equals_single_bitwise(vio, synth, gpu_ctx):
@@ -176,12 +190,16 @@ def test_config4_full_size_properties(vio, synth, gpu_ctx):
     ws = synth.config4(256)
     probs = [vio.BaProblem(w, variant=vio.VIO_BA_VI) for w in ws]
     res = gpu_ctx.ba_solve(probs)
+    # the same windows started from the ground truth: the optimum of the noisy problem near the truth
+    tw = [dict(w, T_wb_init=w["T_wb_true"], lm_xyz=w["lm_true"], vel=w["vel_true"]) for w in ws]
+    tres = gpu_ctx.ba_solve([vio.BaProblem(w, variant=vio.VIO_BA_VI) for w in tw])
     gain = []
-    for w, g in zip(ws, res):
+    for w, g, t in zip(ws, res, tres):
         assert g["success"] == 1 and g["final_cost"] < 1e-2 * g["initial_cost"]
-        e0 = np.linalg.norm(w["lm_xyz"] - w["lm_true"], axis=1).mean()
-        e1 = np.linalg.norm(g["lm_xyz"] - w["lm_true"], axis=1).mean()
-        gain.append(e1 < e0)
+        assert g["final_cost"] <= t["final_cost"] * (1 + 1e-3)   # same basin as the truth start
+        e0 = np.linalg.norm(w["lm_xyz"] - t["lm_xyz"], axis=1).mean()
+        e1 = np.linalg.norm(g["lm_xyz"] - t["lm_xyz"], axis=1).mean()
+        gain.append(e1 < 0.1 * e0)
     assert np.mean(gain) > 0.9
     fixed = [vio.BaProblem(ws[i], variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1) for i in (0, 97, 255)]
     fres = gpu_ctx.ba_solve(fixed)
