@@ -52,6 +52,7 @@ struct __align__(16) BaShared {
     unsigned long long prof_last;
     int prof_on;
     int chol_bad;
+    int posef[BA_KMAX];          // copy of BaWin::pose_f (per-lane indexed in the Schur fill)
 };
 static_assert(sizeof(BaShared) <= 160 * 1024, "BaShared exceeds the 160 KB LDS of a gfx950 CU");
 
@@ -495,7 +496,7 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
     const int N = w.N, L = w.L, np = w.np;
     constexpr int KS = schur_ks(T);    // k-row stride (doubles): the 4 k-rows of a fragment hit both bank halves
-    constexpr int LC = schur_lc(T);    // landmarks per chunk
+    constexpr int LC = schur_lc(T) < 16 ? schur_lc(T) : 16;  // landmarks per chunk (16 fill slots)
     constexpr int KC = schur_kc(LC);   // k rows per chunk (multiple of 4)
     constexpr int NT = T * (T + 1) / 2;
     constexpr int TPW = (NT + 3) / 4;  // lower tiles per wave
@@ -524,48 +525,60 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     double bacc[RPW];
 #pragma unroll
     for (int q = 0; q < RPW; ++q) bacc[q] = 0.0;
+    const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
+    // fill lanes: (landmark slot jf, keyframe pf_k); each writes its pose's 6 rows x 3 k-rows every
+    // chunk (the value or zero), so only the padding rows / k-rows need zeroing, once.
+    const int jf = threadIdx.x >> 4, kf = threadIdx.x & 15;
+    const int pf = kf < w.K ? sh.posef[kf] : -1;
+    for (int e = threadIdx.x; e < 2 * KC * KS; e += BA_THREADS) sh.stage[e] = 0.0;
+    __syncthreads();
     for (int l0 = 0; l0 < L; l0 += LC) {
         const int l1 = min(l0 + LC, L);
-        for (int e = threadIdx.x; e < 2 * KC * KS; e += BA_THREADS) sh.stage[e] = 0.0;
         for (int e = threadIdx.x; e < KC; e += BA_THREADS) {
             const int l = l0 + e / 3, cc = e % 3;
             double v = 0.0;
             if (l < l1 && c.lm_var[l]) v = gl[(int64_t)cc * L + l] * sl[(int64_t)cc * L + l];
             sh.gcol[e] = v;
         }
-        __syncthreads();
-        const int o0 = c.lm_ptr[l0], o1 = c.lm_ptr[l1];
-        for (int o = o0 + threadIdx.x; o < o1; o += BA_THREADS) {
-            int l = c.obs_lm[o], k = c.obs_kf[o];
-            int pf = w.pose_f[k];
-            if (pf < 0 || !c.lm_var[l]) continue;
-            int j = l - l0;
-            double s0 = sl[l], s1 = sl[(int64_t)L + l], s2 = sl[2 * (int64_t)L + l];
-            double vi[6];
+        if (jf < LC && pf >= 0) {
+            const int l = l0 + jf;
+            const int o = (l < l1 && c.lm_var[l]) ? lk[16 * l + kf] : -1;
+            double Y[6][3], Wv[6][3];
+            if (o >= 0) {
+                double s0 = sl[l], s1 = sl[(int64_t)L + l], s2 = sl[2 * (int64_t)L + l];
+                double vi[6];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) vi[i] = Vi[(int64_t)i * L + l];
-            double b0 = jl[o] * s0, b1 = jl[(int64_t)N + o] * s1, b2 = jl[2 * (int64_t)N + o] * s2;
-            double d0 = jl[3 * (int64_t)N + o] * s0, d1 = jl[4 * (int64_t)N + o] * s1, d2 = jl[5 * (int64_t)N + o] * s2;
+                for (int i = 0; i < 6; ++i) vi[i] = Vi[(int64_t)i * L + l];
+                double b0 = jl[o] * s0, b1 = jl[(int64_t)N + o] * s1, b2 = jl[2 * (int64_t)N + o] * s2;
+                double d0 = jl[3 * (int64_t)N + o] * s0, d1 = jl[4 * (int64_t)N + o] * s1, d2 = jl[5 * (int64_t)N + o] * s2;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                double sp = sh.s_f[pf + i];
-                double a = jp[(int64_t)i * N + o] * sp, e = jp[(int64_t)(6 + i) * N + o] * sp;
-                double W0 = a * b0 + e * d0, W1 = a * b1 + e * d1, W2 = a * b2 + e * d2;
-                double Y0 = W0 * vi[0] + W1 * vi[1] + W2 * vi[2];
-                double Y1 = W0 * vi[1] + W1 * vi[3] + W2 * vi[4];
-                double Y2 = W0 * vi[2] + W1 * vi[4] + W2 * vi[5];
-                int row = pf + i;
-                At[(3 * j + 0) * KS + row] = Y0;
-                At[(3 * j + 1) * KS + row] = Y1;
-                At[(3 * j + 2) * KS + row] = Y2;
-                Bt[(3 * j + 0) * KS + row] = W0;
-                Bt[(3 * j + 1) * KS + row] = W1;
-                Bt[(3 * j + 2) * KS + row] = W2;
+                for (int i = 0; i < 6; ++i) {
+                    double sp = sh.s_f[pf + i];
+                    double a = jp[(int64_t)i * N + o] * sp, e = jp[(int64_t)(6 + i) * N + o] * sp;
+                    double W0 = a * b0 + e * d0, W1 = a * b1 + e * d1, W2 = a * b2 + e * d2;
+                    Wv[i][0] = W0; Wv[i][1] = W1; Wv[i][2] = W2;
+                    Y[i][0] = W0 * vi[0] + W1 * vi[1] + W2 * vi[2];
+                    Y[i][1] = W0 * vi[1] + W1 * vi[3] + W2 * vi[4];
+                    Y[i][2] = W0 * vi[2] + W1 * vi[4] + W2 * vi[5];
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+#pragma unroll
+                    for (int cc = 0; cc < 3; ++cc) { Y[i][cc] = 0.0; Wv[i][cc] = 0.0; }
             }
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    At[(3 * jf + cc) * KS + pf + i] = Y[i][cc];
+                    Bt[(3 * jf + cc) * KS + pf + i] = Wv[i][cc];
+                }
         }
         __syncthreads();
         prof_mark(sh, PF_FILL);
         const int nsteps = (3 * (l1 - l0) + 3) >> 2;
+#pragma unroll 2
         for (int st = 0; st < nsteps; ++st) {
             const int kr = (4 * st + kk) * KS;
 #pragma unroll
@@ -1130,6 +1143,13 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
         if (w.is_vi && k >= 1 && c.preint_valid[k]) imu_sqrt_info(c.preint[k], c.sqi + 81 * k);
     }
     for (int o = threadIdx.x; o < N; o += BA_THREADS) c.outlier[o] = 0;
+    for (int k = threadIdx.x; k < BA_KMAX; k += BA_THREADS) sh.posef[k] = k < K ? w.pose_f[k] : -1;
+    {   // (landmark, keyframe) -> observation table for the Schur fill (pairs are unique: host-checked)
+        int* lk = reinterpret_cast<int*>(c.ws + c.L.lk);
+        for (int e = threadIdx.x; e < 16 * L; e += BA_THREADS) lk[e] = -1;
+        __syncthreads();
+        for (int o = threadIdx.x; o < N; o += BA_THREADS) lk[16 * c.obs_lm[o] + c.obs_kf[o]] = o;
+    }
     init_params(sh, c, false);
 
     // ---- fixed cost: residual blocks whose parameters are all constant (program.cc:305-390)

@@ -69,6 +69,7 @@ struct BaWsLayout {
     int64_t c_pose, c_lm, c_vel, c_bias;       // candidate
     int64_t r, jp, jl;                         // obs SoA: r[2][N], jp[12][N], jl[6][N]
     int64_t V, gl, Vi, s_l, y_l;               // landmark: V[6][L], gl[3][L], Vi[6][L], s_l[3][L], y_l[3][L]
+    int64_t lk;                                // int32 [L][16]: observation of landmark l from keyframe k, or -1
     int64_t total;
 };
 
@@ -91,6 +92,7 @@ __host__ __device__ inline BaWsLayout ba_ws_layout(int K, int L, int N) {
     w.Vi = o; o += 6 * (int64_t)L;
     w.s_l = o; o += 3 * (int64_t)L;
     w.y_l = o; o += 3 * (int64_t)L;
+    w.lk = o; o += 8 * (int64_t)L;
     o = (o + 31) & ~(int64_t)31;
     w.total = o;
     return w;
