@@ -36,7 +36,7 @@ struct LmState {
 
 struct __align__(16) BaShared {
     double S[BA_NF_MAX * (BA_NF_MAX + 1)];  // row stride nf|1 (odd: conflict-free column walks)
-    double stage[BA_STAGE];      // Schur panels At | Bt (k-major, see schur_gemm)
+    double stage[BA_STAGE];      // with S: the Schur panels At | Bt (k-major, see schur_gemm)
     double gcol[BA_GCOL];
     double b[BA_NF_MAX], s_f[BA_NF_MAX], g_f[BA_NF_MAX], colsq_f[BA_NF_MAX], D_f[BA_NF_MAX];
     double U[BA_KMAX][27];
@@ -55,6 +55,8 @@ struct __align__(16) BaShared {
     int posef[BA_KMAX];          // copy of BaWin::pose_f (per-lane indexed in the Schur fill)
 };
 static_assert(sizeof(BaShared) <= 160 * 1024, "BaShared exceeds the 160 KB LDS of a gfx950 CU");
+static_assert(offsetof(BaShared, stage) == offsetof(BaShared, S) + sizeof(double) * BA_NF_MAX * (BA_NF_MAX + 1),
+              "Schur panels span S and stage contiguously");
 
 // per-phase shader-clock accounting (diagnostic; enabled when BaPools::prof != nullptr)
 enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST, PF_FILL };
@@ -474,36 +476,68 @@ __device__ void linearise(BaShared& sh, const WinCtx& c, bool first) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Reduced system before the Schur update (schur_eliminator_impl.h:179-377 E^T E-free part): zero,
+// Jacobi-scaled pose blocks U, IMU block, LM diagonal.  Also the panel area of schur_gemm is S
+// itself, so this runs after the landmark loop.
+__device__ void assemble_S(BaShared& sh, const WinCtx& c) {
+    const BaWin& w = *c.w;
+    const int nf = w.nf, ls = nf | 1;
+    for (int e = threadIdx.x; e < nf * ls; e += BA_THREADS) sh.S[e] = 0.0;
+    __syncthreads();
+    for (int e = threadIdx.x; e < 36 * w.K; e += BA_THREADS) {
+        const int k = e / 36, ij = e - 36 * k;
+        const int pf = sh.posef[k];
+        if (pf < 0) continue;
+        const int i = ij / 6, j = ij % 6;
+        const int a = min(i, j), b = max(i, j);
+        const int idx = a * 6 - (a * (a - 1)) / 2 + (b - a);
+        sh.S[(pf + i) * ls + pf + j] = sh.U[k][idx] * sh.s_f[pf + i] * sh.s_f[pf + j];
+    }
+    if (w.is_vi) {
+        const int ni = w.ni, np = w.np;
+        for (int e = threadIdx.x; e < ni * ni; e += BA_THREADS) {
+            int p = e / ni, q = e % ni;
+            sh.S[(np + p) * ls + np + q] = c.Himu[e] * sh.s_f[np + p] * sh.s_f[np + q];
+        }
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < nf; f += BA_THREADS) sh.S[f * ls + f] += sh.D_f[f] * sh.D_f[f];
+    __syncthreads();
+}
+
 // Schur GEMM: S_pp -= Y W^T and b_p -= Y g over landmark chunks (Y = W~ V~^-1), on
-// v_mfma_f64_16x16x4_f64.  Per chunk of LC landmarks the obs lanes scatter their 6x3 Y / W blocks into
-// k-major LDS panels At/Bt (k = 3*landmark + component, one row of npad pose columns per k; rows of
-// unobserved / constant poses stay zero); each wave then owns a fixed set of the lower-triangle
-// 16x16 output tiles (S is only read on and below the diagonal by the Cholesky) and accumulates them
-// across all chunks in registers; the rhs column runs on the VALU beside it.  Fixed per-lane k order
-// plus a fixed shuffle tree: bitwise reproducible.
+// v_mfma_f64_16x16x4_f64.  Per chunk of LC landmarks, fill lanes (landmark slot, keyframe) write
+// their pose's 6 rows of the k-major LDS panels At/Bt (k = 3*landmark + component; the value, or
+// zero when the keyframe does not see the landmark).  Each wave owns a fixed set of the
+// lower-triangle 16x16 output tiles (the Cholesky reads S on and below the diagonal only) and
+// accumulates them over all chunks in registers, the rhs column on the VALU beside it.  The panels
+// alias S (assembled afterwards), and the global loads of chunk c+1 (observation index one chunk
+// further ahead) are in flight while chunk c runs on the matrix cores.  Fixed per-lane k order and
+// a fixed shuffle tree: bitwise reproducible.
 using d4 = __attribute__((ext_vector_type(4))) double;
 
+constexpr int BA_PANEL = BA_NF_MAX * (BA_NF_MAX + 1) + BA_STAGE;  // S followed by stage
 __host__ __device__ constexpr int schur_ks(int T) { return (T & 1) ? 16 * T : 16 * T + 16; }
 __host__ __device__ constexpr int schur_kc(int LC) { return (3 * LC + 3) & ~3; }
 __host__ __device__ constexpr int schur_lc(int T) {
     int lc = 1;
-    while (2 * schur_kc(lc + 1) * schur_ks(T) <= BA_STAGE && schur_kc(lc + 1) <= BA_GCOL) ++lc;
+    while (2 * schur_kc(lc + 1) * schur_ks(T) <= BA_PANEL && schur_kc(lc + 1) <= BA_GCOL) ++lc;
     return lc;
 }
 
 template <int T>
 __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
-    const int N = w.N, L = w.L, np = w.np;
-    constexpr int KS = schur_ks(T);    // k-row stride (doubles): the 4 k-rows of a fragment hit both bank halves
-    constexpr int LC = schur_lc(T) < 16 ? schur_lc(T) : 16;  // landmarks per chunk (16 fill slots)
-    constexpr int KC = schur_kc(LC);   // k rows per chunk (multiple of 4)
+    const int N = w.N, L = w.L, K = w.K, np = w.np;
+    constexpr int KS = schur_ks(T);     // k-row stride (doubles): the 4 k-rows of a fragment hit both bank halves
+    constexpr int LCMAX = schur_lc(T);
     constexpr int NT = T * (T + 1) / 2;
-    constexpr int TPW = (NT + 3) / 4;  // lower tiles per wave
-    constexpr int RPW = (T + 3) / 4;   // rhs row groups per wave
-    static_assert(2 * KC * KS <= BA_STAGE && KC <= BA_GCOL, "Schur staging exceeds LDS panel");
-    double* At = sh.stage;
-    double* Bt = sh.stage + KC * KS;
+    constexpr int TPW = (NT + 3) / 4;   // lower tiles per wave
+    constexpr int RPW = (T + 3) / 4;    // rhs row groups per wave
+    const int LC = min(LCMAX, BA_THREADS / K);  // landmarks per chunk: one fill lane per (landmark, keyframe)
+    const int KC = schur_kc(LC);
+    double* At = sh.S;
+    double* Bt = sh.S + KC * KS;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r16 = lane & 15, kk = lane >> 4;
     const double* jp = c.ws + c.L.jp;
@@ -511,6 +545,7 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     const double* Vi = c.ws + c.L.Vi;
     const double* gl = c.ws + c.L.gl;
     const double* sl = c.ws + c.L.s_l;
+    const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
     int trow[TPW], tcol[TPW];
 #pragma unroll
     for (int m = 0; m < TPW; ++m) {
@@ -525,41 +560,57 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     double bacc[RPW];
 #pragma unroll
     for (int q = 0; q < RPW; ++q) bacc[q] = 0.0;
-    const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
-    // fill lanes: (landmark slot jf, keyframe pf_k); each writes its pose's 6 rows x 3 k-rows every
-    // chunk (the value or zero), so only the padding rows / k-rows need zeroing, once.
-    const int jf = threadIdx.x >> 4, kf = threadIdx.x & 15;
-    const int pf = kf < w.K ? sh.posef[kf] : -1;
-    for (int e = threadIdx.x; e < 2 * KC * KS; e += BA_THREADS) sh.stage[e] = 0.0;
+
+    const int jf = threadIdx.x / K, kf = threadIdx.x - jf * K;
+    const int pf = jf < LC ? sh.posef[kf] : -1;
+    // prefetch registers: observation of the chunk after next, data of the next chunk
+    int o_next = -1;
+    double pj[12], lj[6], sv[3], vv[6], gq = 0.0;
+    auto load_obs = [&](int l0n) -> int {
+        const int l = l0n + jf;
+        return (pf >= 0 && l < L) ? lk[16 * l + kf] : -1;
+    };
+    auto load_data = [&](int l0n, int o) {
+        const int l = l0n + jf;
+        if (o >= 0) {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) pj[i] = jp[(int64_t)i * N + o];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) lj[i] = jl[(int64_t)i * N + o];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) sv[i] = sl[(int64_t)i * L + l];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) vv[i] = Vi[(int64_t)i * L + l];
+        }
+        gq = 0.0;
+        if (threadIdx.x < KC) {
+            const int lg = l0n + threadIdx.x / 3, cg = threadIdx.x % 3;
+            if (lg < min(l0n + LC, L) && c.lm_var[lg]) gq = gl[(int64_t)cg * L + lg] * sl[(int64_t)cg * L + lg];
+        }
+    };
+    for (int e = threadIdx.x; e < 2 * KC * KS; e += BA_THREADS) sh.S[e] = 0.0;
+    int o_cur = load_obs(0);
+    load_data(0, o_cur);
+    o_next = load_obs(LC);
     __syncthreads();
     for (int l0 = 0; l0 < L; l0 += LC) {
         const int l1 = min(l0 + LC, L);
-        for (int e = threadIdx.x; e < KC; e += BA_THREADS) {
-            const int l = l0 + e / 3, cc = e % 3;
-            double v = 0.0;
-            if (l < l1 && c.lm_var[l]) v = gl[(int64_t)cc * L + l] * sl[(int64_t)cc * L + l];
-            sh.gcol[e] = v;
-        }
-        if (jf < LC && pf >= 0) {
-            const int l = l0 + jf;
-            const int o = (l < l1 && c.lm_var[l]) ? lk[16 * l + kf] : -1;
+        // ---- fill chunk [l0, l1) from the prefetch registers
+        if (threadIdx.x < KC) sh.gcol[threadIdx.x] = gq;
+        if (pf >= 0) {
             double Y[6][3], Wv[6][3];
-            if (o >= 0) {
-                double s0 = sl[l], s1 = sl[(int64_t)L + l], s2 = sl[2 * (int64_t)L + l];
-                double vi[6];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) vi[i] = Vi[(int64_t)i * L + l];
-                double b0 = jl[o] * s0, b1 = jl[(int64_t)N + o] * s1, b2 = jl[2 * (int64_t)N + o] * s2;
-                double d0 = jl[3 * (int64_t)N + o] * s0, d1 = jl[4 * (int64_t)N + o] * s1, d2 = jl[5 * (int64_t)N + o] * s2;
+            if (o_cur >= 0) {
+                const double b0 = lj[0] * sv[0], b1 = lj[1] * sv[1], b2 = lj[2] * sv[2];
+                const double d0 = lj[3] * sv[0], d1 = lj[4] * sv[1], d2 = lj[5] * sv[2];
 #pragma unroll
                 for (int i = 0; i < 6; ++i) {
-                    double sp = sh.s_f[pf + i];
-                    double a = jp[(int64_t)i * N + o] * sp, e = jp[(int64_t)(6 + i) * N + o] * sp;
-                    double W0 = a * b0 + e * d0, W1 = a * b1 + e * d1, W2 = a * b2 + e * d2;
+                    const double sp = sh.s_f[pf + i];
+                    const double a = pj[i] * sp, e = pj[6 + i] * sp;
+                    const double W0 = a * b0 + e * d0, W1 = a * b1 + e * d1, W2 = a * b2 + e * d2;
                     Wv[i][0] = W0; Wv[i][1] = W1; Wv[i][2] = W2;
-                    Y[i][0] = W0 * vi[0] + W1 * vi[1] + W2 * vi[2];
-                    Y[i][1] = W0 * vi[1] + W1 * vi[3] + W2 * vi[4];
-                    Y[i][2] = W0 * vi[2] + W1 * vi[4] + W2 * vi[5];
+                    Y[i][0] = W0 * vv[0] + W1 * vv[1] + W2 * vv[2];
+                    Y[i][1] = W0 * vv[1] + W1 * vv[3] + W2 * vv[4];
+                    Y[i][2] = W0 * vv[2] + W1 * vv[4] + W2 * vv[5];
                 }
             } else {
 #pragma unroll
@@ -577,8 +628,14 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
         }
         __syncthreads();
         prof_mark(sh, PF_FILL);
+        // ---- prefetch: data of the next chunk, observation index of the one after
+        o_cur = o_next;
+        if (l1 < L) {
+            load_data(l1, o_cur);
+            o_next = load_obs(l1 + LC);
+        }
+        // ---- MFMA over the chunk
         const int nsteps = (3 * (l1 - l0) + 3) >> 2;
-#pragma unroll 2
         for (int st = 0; st < nsteps; ++st) {
             const int kr = (4 * st + kk) * KS;
 #pragma unroll
@@ -598,6 +655,7 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
         __syncthreads();
         prof_mark(sh, PF_GEMM);
     }
+    assemble_S(sh, c);
     const int ls = w.nf | 1;
 #pragma unroll
     for (int m = 0; m < TPW; ++m) {
@@ -637,21 +695,29 @@ __device__ bool cholesky_solve(BaShared& sh, int nf) {
             double s0 = 0.0, s1 = 0.0;  // rows i0 = lane, i1 = lane + 64 (only i >= j matter)
             const int i0 = lane, i1 = lane + 64;
             const bool a0 = i0 >= j && i0 < nf, a1 = i1 >= j && i1 < nf;
+            // dot products of row prefixes: 8 independent partial sums per row keep 8+ LDS reads in
+            // flight per latency (the loop is latency-bound otherwise)
             if (a0) {
                 const double* Li = S + i0 * ls;
-                double p0 = 0.0, p1 = 0.0;
+                double p[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
                 int k = 0;
-                for (; k + 1 < j; k += 2) { p0 += Li[k] * Lj[k]; p1 += Li[k + 1] * Lj[k + 1]; }
-                if (k < j) p0 += Li[k] * Lj[k];
-                s0 = Li[j] - (p0 + p1);
+                for (; k + 7 < j; k += 8) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) p[u] += Li[k + u] * Lj[k + u];
+                }
+                for (; k < j; ++k) p[0] += Li[k] * Lj[k];
+                s0 = Li[j] - (((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7])));
             }
             if (a1) {
                 const double* Li = S + i1 * ls;
-                double p0 = 0.0, p1 = 0.0;
+                double p[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
                 int k = 0;
-                for (; k + 1 < j; k += 2) { p0 += Li[k] * Lj[k]; p1 += Li[k + 1] * Lj[k + 1]; }
-                if (k < j) p0 += Li[k] * Lj[k];
-                s1 = Li[j] - (p0 + p1);
+                for (; k + 7 < j; k += 8) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) p[u] += Li[k + u] * Lj[k + u];
+                }
+                for (; k < j; ++k) p[0] += Li[k] * Lj[k];
+                s1 = Li[j] - (((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7])));
             }
             const double d = j < 64 ? __shfl(s0, j, 64) : __shfl(s1, j - 64, 64);
             if (!(d > 0.0)) { bad = 1; break; }
@@ -744,27 +810,6 @@ __device__ void compute_step(BaShared& sh, const WinCtx& c) {
         sh.D_f[f] = sqrt(d / radius);
         sh.b[f] = sh.s_f[f] * sh.g_f[f];
     }
-    for (int e = threadIdx.x; e < nf * ls; e += BA_THREADS) sh.S[e] = 0.0;
-    __syncthreads();
-    for (int k = 0; k < w.K; ++k) {
-        int pf = w.pose_f[k];
-        if (pf < 0) continue;
-        for (int e = threadIdx.x; e < 36; e += BA_THREADS) {
-            int i = e / 6, j = e % 6;
-            int a = min(i, j), b = max(i, j);
-            int idx = a * 6 - (a * (a - 1)) / 2 + (b - a);
-            sh.S[(pf + i) * ls + pf + j] = sh.U[k][idx] * sh.s_f[pf + i] * sh.s_f[pf + j];
-        }
-    }
-    if (w.is_vi) {
-        const int ni = w.ni, np = w.np;
-        for (int e = threadIdx.x; e < ni * ni; e += BA_THREADS) {
-            int p = e / ni, q = e % ni;
-            sh.S[(np + p) * ls + np + q] = c.Himu[e] * sh.s_f[np + p] * sh.s_f[np + q];
-        }
-    }
-    __syncthreads();
-    for (int f = threadIdx.x; f < nf; f += BA_THREADS) sh.S[f * ls + f] += sh.D_f[f] * sh.D_f[f];
     double anybad = block_max((double)bad, sh.redm);
     if (anybad > 0.0) {
         if (threadIdx.x == 0) sh.st.valid = 0;
@@ -782,6 +827,8 @@ __device__ void compute_step(BaShared& sh, const WinCtx& c) {
             case 5: schur_gemm<5>(sh, c); break;
             default: schur_gemm<6>(sh, c); break;
         }
+    } else {
+        assemble_S(sh, c);
     }
     prof_mark(sh, PF_GEMM);
     // (4) reduced solve
@@ -1148,7 +1195,8 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
         int* lk = reinterpret_cast<int*>(c.ws + c.L.lk);
         for (int e = threadIdx.x; e < 16 * L; e += BA_THREADS) lk[e] = -1;
         __syncthreads();
-        for (int o = threadIdx.x; o < N; o += BA_THREADS) lk[16 * c.obs_lm[o] + c.obs_kf[o]] = o;
+        for (int o = threadIdx.x; o < N; o += BA_THREADS)
+            if (c.lm_var[c.obs_lm[o]]) lk[16 * c.obs_lm[o] + c.obs_kf[o]] = o;
     }
     init_params(sh, c, false);
 
