@@ -35,7 +35,7 @@ struct LmState {
 };
 
 struct __align__(16) BaShared {
-    double S[BA_NF_MAX * (BA_NF_MAX + 1)];  // row stride nf|1 (odd: conflict-free column walks)
+    double S[BA_NF_MAX * (BA_NF_MAX + 1)];  // row stride s_ld(nf) (odd), rows padded to 16-row tiles
     double stage[BA_STAGE];      // with S: the Schur panels At | Bt (k-major, see schur_gemm)
     double gcol[BA_GCOL];
     double b[BA_NF_MAX], s_f[BA_NF_MAX], g_f[BA_NF_MAX], colsq_f[BA_NF_MAX], D_f[BA_NF_MAX];
@@ -57,6 +57,10 @@ struct __align__(16) BaShared {
 static_assert(sizeof(BaShared) <= 160 * 1024, "BaShared exceeds the 160 KB LDS of a gfx950 CU");
 static_assert(offsetof(BaShared, stage) == offsetof(BaShared, S) + sizeof(double) * BA_NF_MAX * (BA_NF_MAX + 1),
               "Schur panels span S and stage contiguously");
+
+// row stride of S: tile-padded size, odd (conflict-free column walks)
+__host__ __device__ constexpr int s_ld(int nf) { return (16 * ((nf + 15) >> 4)) | 1; }
+static_assert(16 * ((BA_NF_MAX + 15) >> 4) * s_ld(BA_NF_MAX) <= BA_NF_MAX * (BA_NF_MAX + 1), "S padding");
 
 // per-phase shader-clock accounting (diagnostic; enabled when BaPools::prof != nullptr)
 enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST, PF_FILL };
@@ -481,9 +485,10 @@ __device__ void linearise(BaShared& sh, const WinCtx& c, bool first) {
 // itself, so this runs after the landmark loop.
 __device__ void assemble_S(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
-    const int nf = w.nf, ls = nf | 1;
-    for (int e = threadIdx.x; e < nf * ls; e += BA_THREADS) sh.S[e] = 0.0;
+    const int nf = w.nf, ls = s_ld(nf), npS = 16 * ((nf + 15) >> 4);
+    for (int e = threadIdx.x; e < npS * ls; e += BA_THREADS) sh.S[e] = 0.0;
     __syncthreads();
+    for (int f = nf + threadIdx.x; f < npS; f += BA_THREADS) { sh.S[f * ls + f] = 1.0; sh.b[f] = 0.0; }
     for (int e = threadIdx.x; e < 36 * w.K; e += BA_THREADS) {
         const int k = e / 36, ij = e - 36 * k;
         const int pf = sh.posef[k];
@@ -656,7 +661,7 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
         prof_mark(sh, PF_GEMM);
     }
     assemble_S(sh, c);
-    const int ls = w.nf | 1;
+    const int ls = s_ld(w.nf);
 #pragma unroll
     for (int m = 0; m < TPW; ++m) {
         if (trow[m] < 0) continue;
@@ -678,83 +683,149 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     __syncthreads();
 }
 
-// Cholesky of S (nf x nf, LDS, nf <= 128, row stride ls = nf|1) then solve S y = b (y overwrites b).
-// Left-looking and wave-synchronous: wave 0 alone computes column j for its rows i = lane, lane+64
-// (L[i][j] = (S[i][j] - sum_k L[i][k] L[j][k]) / L[j][j]) with no workgroup barrier per column;
-// the other waves wait at one barrier.  The odd row stride makes the per-lane row walks hit 32
-// distinct bank pairs.  Returns false (uniformly) when S is not positive definite.
-__device__ bool cholesky_solve(BaShared& sh, int nf) {
+// Cholesky of S (nf x nf in LDS, padded to nb = ceil(nf/16) 16x16 tiles with an identity tail,
+// row stride s_ld(nf)) then solve S y = b (y overwrites b).  Blocked right-looking:
+//   (A) wave 0 factors the diagonal tile in registers (lane i = row i, pivots and column entries
+//       broadcast with v_readlane) and forms its triangular inverse; Linv_J^T goes to the stage area;
+//   (B) panel tiles L_IJ = S_IJ Linv_J^T on v_mfma_f64_16x16x4_f64, one tile per wave at a time;
+//   (C) trailing lower tiles S_IK -= L_IJ L_KJ^T on the matrix cores.
+// Three workgroup barriers per tile column.  The two triangular solves walk the tile columns with
+// one wave (lanes = 16 rows x 4 column groups).  Fixed operation order: bitwise reproducible.
+// Returns false (uniformly) when a pivot is not positive (S not positive definite).
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __noinline__ bool cholesky_solve(BaShared& sh, int nf) {
     double* S = sh.S;
-    const int ls = nf | 1;
-    int& chol_bad = sh.chol_bad;
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        int bad = 0;
-        for (int j = 0; j < nf && !bad; ++j) {
-            const double* Lj = S + j * ls;
-            double s0 = 0.0, s1 = 0.0;  // rows i0 = lane, i1 = lane + 64 (only i >= j matter)
-            const int i0 = lane, i1 = lane + 64;
-            const bool a0 = i0 >= j && i0 < nf, a1 = i1 >= j && i1 < nf;
-            // dot products of row prefixes: 8 independent partial sums per row keep 8+ LDS reads in
-            // flight per latency (the loop is latency-bound otherwise)
-            if (a0) {
-                const double* Li = S + i0 * ls;
-                double p[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-                int k = 0;
-                for (; k + 7 < j; k += 8) {
+    double* LB = sh.stage;  // [nb][16 m][16 c] = Linv_J[c][m]
+    const int ls = s_ld(nf), nb = (nf + 15) >> 4;
+    constexpr int NW = BA_THREADS / 64;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r16 = lane & 15, kk = lane >> 4;
+    for (int J = 0; J < nb; ++J) {
+        const int c0 = 16 * J;
+        // (A) diagonal tile
+        if (wid == 0) {
+            const int i = r16;
+            double d[16], il[16];
+            const double* row = S + (c0 + i) * ls + c0;
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) p[u] += Li[k + u] * Lj[k + u];
-                }
-                for (; k < j; ++k) p[0] += Li[k] * Lj[k];
-                s0 = Li[j] - (((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7])));
-            }
-            if (a1) {
-                const double* Li = S + i1 * ls;
-                double p[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-                int k = 0;
-                for (; k + 7 < j; k += 8) {
+            for (int k = 0; k < 16; ++k) d[k] = row[k];  // k > i: upper triangle, never used
+            int bad = 0;
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) p[u] += Li[k + u] * Lj[k + u];
-                }
-                for (; k < j; ++k) p[0] += Li[k] * Lj[k];
-                s1 = Li[j] - (((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7])));
+            for (int j = 0; j < 16; ++j) {
+                const double piv = readlane_d(d[j], j);
+                bad |= !(piv > 0.0);
+                const double lj = sqrt(piv);
+                il[j] = 1.0 / lj;
+                const double cj = i == j ? lj : d[j] * il[j];
+                d[j] = cj;
+#pragma unroll
+                for (int k = j + 1; k < 16; ++k) d[k] -= cj * readlane_d(cj, k);
             }
-            const double d = j < 64 ? __shfl(s0, j, 64) : __shfl(s1, j - 64, 64);
-            if (!(d > 0.0)) { bad = 1; break; }
-            const double ld = sqrt(d), il = 1.0 / ld;
+            // column i of Linv (lower): x[q] = Linv[q][i]
+            double x[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                double s = q == i ? 1.0 : 0.0;
+#pragma unroll
+                for (int m = 0; m < q; ++m) s -= readlane_d(d[m], q) * x[m];
+                x[q] = s * il[q];
+            }
+            // LB[m][c] = Linv[c][m]: lane m holds column m of Linv, i.e. Linv[c][m] = x[c]
+            if (kk == 0) {
+                double* dst = LB + 256 * J + 16 * i;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) dst[q] = x[q];
+            }
+            if (lane == 0) sh.chol_bad = bad;
+        }
+        __syncthreads();
+        if (sh.chol_bad) return false;
+        // (B) panel: L_IJ = S_IJ Linv_J^T
+        const double* lb = LB + 256 * J;
+        for (int I = J + 1 + wid; I < nb; I += NW) {
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            double* A = S + 16 * I * ls + c0;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const double a = A[r16 * ls + 4 * st + kk];
+                const double bb = lb[(4 * st + kk) * 16 + r16];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[(kk + 4 * r) * ls + r16] = acc[r];
+        }
+        __syncthreads();
+        // (C) trailing update of the lower tiles (I, K), J < K <= I < nb
+        const int m = nb - J - 1, nt = m * (m + 1) / 2;
+        for (int t = wid; t < nt; t += NW) {
+            int I = 0, tt = t;
+            while (tt > I) { tt -= I + 1; ++I; }
+            const int Kt = tt + J + 1;
+            I += J + 1;
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            const double* Ai = S + 16 * I * ls + c0;
+            const double* Bk = S + 16 * Kt * ls + c0;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const double a = Ai[r16 * ls + 4 * st + kk];
+                const double bb = Bk[r16 * ls + 4 * st + kk];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+            }
+            double* C = S + 16 * I * ls + 16 * Kt;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) C[(kk + 4 * r) * ls + r16] -= acc[r];
+        }
+        __syncthreads();
+    }
+    // triangular solves by wave 0: lane (row r16 of the tile column, column group kk)
+    if (wid == 0) {
+        double* y = sh.b;
+        for (int J = 0; J < nb; ++J) {  // forward: y_J = Linv_J (b_J - sum_{K<J} L_JK y_K)
+            const double* Lr = S + (16 * J + r16) * ls;
+            double p0 = 0.0, p1 = 0.0;
+            int cix = kk;
+            for (; cix + 4 < 16 * J; cix += 8) { p0 += Lr[cix] * y[cix]; p1 += Lr[cix + 4] * y[cix + 4]; }
+            if (cix < 16 * J) p0 += Lr[cix] * y[cix];
+            double t = p0 + p1;
+            t += __shfl_xor(t, 16, 64);
+            t += __shfl_xor(t, 32, 64);
+            t = y[16 * J + r16] - t;
+            const double* lb = LB + 256 * J;
+            double v = 0.0;
+#pragma unroll
+            for (int mm = 0; mm < 16; ++mm) v += lb[16 * mm + r16] * readlane_d(t, mm);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            if (a0) S[i0 * ls + j] = i0 == j ? ld : s0 * il;
-            if (a1) S[i1 * ls + j] = i1 == j ? ld : s1 * il;
+            if (kk == 0) y[16 * J + r16] = v;
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        if (lane == 0) chol_bad = bad;
-    }
-    __syncthreads();
-    if (chol_bad) return false;
-    // triangular solves by wave 0 (wave-synchronous); rows owned lane, lane+64
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        double b0 = lane < nf ? sh.b[lane] : 0.0;
-        double b1 = lane + 64 < nf ? sh.b[lane + 64] : 0.0;
-        for (int j = 0; j < nf; ++j) {
-            double bj = j < 64 ? __shfl(b0, j, 64) : __shfl(b1, j - 64, 64);
-            double yj = bj / S[j * ls + j];
-            if (lane == j) b0 = yj;
-            if (lane + 64 == j) b1 = yj;
-            if (lane > j && lane < nf) b0 -= S[lane * ls + j] * yj;
-            if (lane + 64 > j && lane + 64 < nf) b1 -= S[(lane + 64) * ls + j] * yj;
+        for (int J = nb - 1; J >= 0; --J) {  // backward: x_J = Linv_J^T (y_J - sum_{K>J} L_KJ^T x_K)
+            double p0 = 0.0, p1 = 0.0;
+            int cix = 16 * (J + 1) + kk;
+            const int cend = 16 * nb;
+            for (; cix + 4 < cend; cix += 8) {
+                p0 += S[cix * ls + 16 * J + r16] * y[cix];
+                p1 += S[(cix + 4) * ls + 16 * J + r16] * y[cix + 4];
+            }
+            if (cix < cend) p0 += S[cix * ls + 16 * J + r16] * y[cix];
+            double t = p0 + p1;
+            t += __shfl_xor(t, 16, 64);
+            t += __shfl_xor(t, 32, 64);
+            t = y[16 * J + r16] - t;
+            const double* lb = LB + 256 * J;
+            double v = 0.0;
+#pragma unroll
+            for (int mm = 0; mm < 16; ++mm) v += lb[16 * r16 + mm] * readlane_d(t, mm);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            if (kk == 0) y[16 * J + r16] = v;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        for (int j = nf - 1; j >= 0; --j) {
-            double bj = j < 64 ? __shfl(b0, j, 64) : __shfl(b1, j - 64, 64);
-            double yj = bj / S[j * ls + j];
-            if (lane == j) b0 = yj;
-            if (lane + 64 == j) b1 = yj;
-            if (lane < j) b0 -= S[j * ls + lane] * yj;
-            if (lane + 64 < j) b1 -= S[j * ls + lane + 64] * yj;
-        }
-        if (lane < nf) sh.b[lane] = b0;
-        if (lane + 64 < nf) sh.b[lane + 64] = b1;
     }
     __syncthreads();
     return true;
@@ -763,7 +834,7 @@ __device__ bool cholesky_solve(BaShared& sh, int nf) {
 // One LM step computation (ComputeTrustRegionStep): returns validity uniformly via sh.st.valid.
 __device__ void compute_step(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
-    const int N = w.N, L = w.L, nf = w.nf, ls = nf | 1;
+    const int N = w.N, L = w.L, nf = w.nf;
     const double radius = sh.st.radius;
     const double dmin = 1e-6, dmax = 1e32;
     double* Vi = c.ws + c.L.Vi;
