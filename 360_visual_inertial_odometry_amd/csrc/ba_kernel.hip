@@ -53,6 +53,7 @@ struct __align__(16) BaShared {
     int prof_on;
     int chol_bad;
     int posef[BA_KMAX];          // copy of BaWin::pose_f (per-lane indexed in the Schur fill)
+    int pvalid[BA_KMAX];         // preint_valid
 };
 static_assert(sizeof(BaShared) <= 160 * 1024, "BaShared exceeds the 160 KB LDS of a gfx950 CU");
 static_assert(offsetof(BaShared, stage) == offsetof(BaShared, S) + sizeof(double) * BA_NF_MAX * (BA_NF_MAX + 1),
@@ -63,7 +64,7 @@ __host__ __device__ constexpr int s_ld(int nf) { return (16 * ((nf + 15) >> 4)) 
 static_assert(16 * ((BA_NF_MAX + 15) >> 4) * s_ld(BA_NF_MAX) <= BA_NF_MAX * (BA_NF_MAX + 1), "S padding");
 
 // per-phase shader-clock accounting (diagnostic; enabled when BaPools::prof != nullptr)
-enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST, PF_FILL };
+enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST, PF_FILL, PF_PFX, PF_ASM };
 __device__ __forceinline__ void prof_mark(BaShared& sh, int slot) {
     if (sh.prof_on && threadIdx.x == 0) {
         unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -73,6 +74,9 @@ __device__ __forceinline__ void prof_mark(BaShared& sh, int slot) {
 }
 
 // ------------------------------------------------------------------------------------------
+// wave index as a wave-uniform (scalar) value: branches on it stay scalar
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 // fixed-order block reductions
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -291,62 +295,274 @@ struct WinCtx {
 };
 
 // pose cache for the parameter set at (xp): T_wb = SE3(T_init) * exp(delta), etc.
-__device__ void pose_cache(BaShared& sh, const WinCtx& c, const double* xp) {
+__device__ __forceinline__ void pose_cache(BaShared& sh, const WinCtx& c, const double* xp) {
     int K = c.w->K;
     for (int k = threadIdx.x; k < K; k += BA_THREADS) pose_cache_one(sh.pinit[k], xp + 6 * k, sh.pc[k]);
 }
 
-// Evaluate cost (and the Jacobian when want_jac) at the point (xp, xl, xv, xb).
-// Returns the total cost of the ACTIVE residual blocks.  Sets sh.st.fail on a PnP evaluation failure.
-__device__ double evaluate(BaShared& sh, const WinCtx& c, const double* xp, const double* xl, const double* xv,
-                           const double* xb, bool want_jac) {
+// Landmark-chunk walker: lane (jf, kf) = (landmark slot, keyframe) of a chunk of LC = BA_THREADS/K
+// landmarks; its observation is lk[16 l + kf] (or -1).  A landmark's observations are contiguous in
+// the landmark-sorted SoA arrays, so consecutive lanes touch consecutive observations (coalesced),
+// a lane keeps one keyframe (its pose cache / pose sums) for the whole walk, and landmark sums are
+// fixed-order reductions over the K lanes of a slot through LDS.
+struct Walk {
+    int LC, jf, kf;
+    bool on;
+};
+__device__ __forceinline__ Walk walk_geom(int K) {
+    Walk g;
+    const int k = K > 0 ? K : 1;
+    g.LC = BA_THREADS / k;
+    g.jf = threadIdx.x / k;
+    g.kf = threadIdx.x - g.jf * k;
+    g.on = K > 0 && g.jf < g.LC;
+    return g;
+}
+
+// IMU factors (one lane per factor): cost, and residual/Jacobian into LDS when want_jac
+__device__ __forceinline__ double imu_factors(BaShared& sh, const WinCtx& c, const double* xv, const double* xb, bool want_jac) {
     const BaWin& w = *c.w;
-    const int N = w.N, K = w.K;
+    double cost = 0.0;
+    if (!w.is_vi) return 0.0;
+    for (int k = 1 + threadIdx.x; k < w.K; k += BA_THREADS) {
+        if (!c.preint_valid[k]) continue;
+        double r[9];
+        imu_eval(c.preint[k], c.sqi + 81 * k, w.gravity, sh.pc[k - 1], sh.pc[k], xv + 3 * (k - 1), xb, xb + 3,
+                 xv + 3 * k, want_jac, r, sh.imu_J[k]);
+        double sq = 0.0;
+        for (int i = 0; i < 9; ++i) {
+            sq += r[i] * r[i];
+            if (want_jac) sh.imu_r[k][i] = r[i];
+        }
+        cost += 0.5 * sq;
+    }
+    return cost;
+}
+
+__device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool first, double gm);
+
+// Cost + residuals/Jacobians + normal-equation statistics at (xp, xl, xv, xb) in one walk:
+// BAFactor::Evaluate per observation lane (Factors.cpp:327-542) with Huber/Corrector scaling,
+// the scaled r/J stored for the step (SoA), per-landmark V = Jl^T Jl and g_l = Jl^T r, per-pose
+// U = Jp^T Jp and g_p = Jp^T r, then the IMU factors and the f-space gradient (lin_tail).
+// Returns the total cost of the ACTIVE residual blocks; sets sh.st.fail on a PnP evaluation failure.
+__device__ __forceinline__ double eval_lin(BaShared& sh, const WinCtx& c, const double* xp, const double* xl, const double* xv,
+                           const double* xb, bool first) {
+    const BaWin& w = *c.w;
+    const int N = w.N, K = w.K, L = w.L;
     pose_cache(sh, c, xp);
     __syncthreads();
-    double cost = 0.0;
-    int fail = 0;
+    const Walk g = walk_geom(K);
+    const int pf = g.on ? sh.posef[g.kf] : -1;
+    const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
     double* r0 = c.ws + c.L.r;
     double* jp = c.ws + c.L.jp;
     double* jl = c.ws + c.L.jl;
-    for (int o = threadIdx.x; o < N; o += BA_THREADS) {
-        int k = c.obs_kf[o], l = c.obs_lm[o];
-        bool active = w.pose_f[k] >= 0 || c.lm_var[l];
-        if (!active) continue;
-        double Pw[3] = {xl[3 * l], xl[3 * l + 1], xl[3 * l + 2]};
-        double r[2], Jp[12], Jl[6];
-        bool jzero;
-        int f = factor_eval(sh.pc[k], sh.Rcb_raw[k], Pw, (double)c.obs_uv[2 * o], (double)c.obs_uv[2 * o + 1], w.cols,
-                            w.rows, w.Lw, c.outlier[o] != 0, w.is_pnp, want_jac, r, Jp, Jl, jzero);
-        if (f) { fail = 1; continue; }
-        double cst, sc;
-        huber(w.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
-        cost += cst;
-        if (want_jac) {
-            r0[o] = r[0] * sc;
-            r0[N + o] = r[1] * sc;
+    double* V = c.ws + c.L.V;
+    double* gl = c.ws + c.L.gl;
+    double* sl = c.ws + c.L.s_l;
+    double acc[27];
 #pragma unroll
-            for (int i = 0; i < 12; ++i) jp[(int64_t)i * N + o] = jzero ? 0.0 : Jp[i] * sc;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) jl[(int64_t)i * N + o] = jzero ? 0.0 : Jl[i] * sc;
+    for (int i = 0; i < 27; ++i) acc[i] = 0.0;
+    double cost = 0.0, gm = 0.0;
+    int fail = 0;
+    // software pipeline: observation index two chunks ahead, its inputs one chunk ahead
+    struct EvD { double P[3]; float u, v; int o, lv, out; };
+    auto ld_o = [&](int l0n) -> int {
+        const int l = l0n + g.jf;
+        return (g.on && l < L) ? lk[16 * l + g.kf] : -1;
+    };
+    auto ld_ev = [&](int l0n, int o, EvD& d) {
+        d.o = o;
+        if (o >= 0) {
+            const int l = l0n + g.jf;
+            d.lv = c.lm_var[l];
+            d.out = c.outlier[o];
+            d.u = c.obs_uv[2 * o];
+            d.v = c.obs_uv[2 * o + 1];
+            d.P[0] = xl[3 * l]; d.P[1] = xl[3 * l + 1]; d.P[2] = xl[3 * l + 2];
         }
-    }
-    if (w.is_vi) {
-        for (int k = 1 + threadIdx.x; k < K; k += BA_THREADS) {
-            if (!c.preint_valid[k]) continue;
-            double r[9];
-            imu_eval(c.preint[k], c.sqi + 81 * k, w.gravity, sh.pc[k - 1], sh.pc[k], xv + 3 * (k - 1), xb, xb + 3,
-                     xv + 3 * k, want_jac, r, sh.imu_J[k]);
-            double sq = 0.0;
-            for (int i = 0; i < 9; ++i) {
-                sq += r[i] * r[i];
-                if (want_jac) sh.imu_r[k][i] = r[i];
+    };
+    EvD cur;
+    int o_nn = ld_o(g.LC);
+    ld_ev(0, ld_o(0), cur);
+    for (int l0 = 0, ci = 0; l0 < L; l0 += g.LC, ++ci) {
+        EvD nxt;
+        nxt.o = -1;
+        int o_n2 = -1;
+        if (l0 + g.LC < L) {
+            ld_ev(l0 + g.LC, o_nn, nxt);
+            o_n2 = ld_o(l0 + 2 * g.LC);
+        }
+        const int o = cur.o;
+        double v9[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) v9[i] = 0.0;
+        if (o >= 0) {
+            const bool lv = cur.lv != 0;
+            if (pf >= 0 || lv) {
+                double Pw[3] = {cur.P[0], cur.P[1], cur.P[2]};
+                double r[2], Jp[12], Jl[6];
+                bool jz;
+                const int f = factor_eval(sh.pc[g.kf], sh.Rcb_raw[g.kf], Pw, (double)cur.u, (double)cur.v, w.cols,
+                                          w.rows, w.Lw, cur.out != 0, w.is_pnp, true, r, Jp, Jl, jz);
+                if (f) {
+                    fail = 1;
+                } else {
+                    double cst, sc;
+                    huber(w.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
+                    cost += cst;
+                    const double ra = r[0] * sc, rb = r[1] * sc;
+                    r0[o] = ra;
+                    r0[N + o] = rb;
+                    double a[6], b[6], la[3], lb[3];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) {
+                        a[i] = jz ? 0.0 : Jp[i] * sc;
+                        b[i] = jz ? 0.0 : Jp[6 + i] * sc;
+                        jp[(int64_t)i * N + o] = a[i];
+                        jp[(int64_t)(6 + i) * N + o] = b[i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        la[i] = jz ? 0.0 : Jl[i] * sc;
+                        lb[i] = jz ? 0.0 : Jl[3 + i] * sc;
+                        jl[(int64_t)i * N + o] = la[i];
+                        jl[(int64_t)(3 + i) * N + o] = lb[i];
+                    }
+                    if (pf >= 0) {
+                        int idx = 0;
+#pragma unroll
+                        for (int i = 0; i < 6; ++i)
+#pragma unroll
+                            for (int j = i; j < 6; ++j) acc[idx++] += a[i] * a[j] + b[i] * b[j];
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) acc[21 + i] += a[i] * ra + b[i] * rb;
+                    }
+                    if (lv) {
+                        v9[0] = la[0] * la[0] + lb[0] * lb[0];
+                        v9[1] = la[0] * la[1] + lb[0] * lb[1];
+                        v9[2] = la[0] * la[2] + lb[0] * lb[2];
+                        v9[3] = la[1] * la[1] + lb[1] * lb[1];
+                        v9[4] = la[1] * la[2] + lb[1] * lb[2];
+                        v9[5] = la[2] * la[2] + lb[2] * lb[2];
+                        v9[6] = la[0] * ra + lb[0] * rb;
+                        v9[7] = la[1] * ra + lb[1] * rb;
+                        v9[8] = la[2] * ra + lb[2] * rb;
+                    }
+                }
             }
-            cost += 0.5 * sq;
+        }
+        // landmark sums over the slot's K lanes (double-buffered: one barrier per chunk)
+        double* rb_ = sh.S + (ci & 1) * 9 * BA_THREADS;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) rb_[i * BA_THREADS + threadIdx.x] = v9[i];
+        __syncthreads();
+        if ((int)threadIdx.x < g.LC) {
+            const int lj = l0 + threadIdx.x;
+            if (lj < L && c.lm_var[lj]) {
+                double v[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) v[i] = 0.0;
+#pragma unroll
+                for (int kf = 0; kf < BA_KMAX; ++kf)
+                    if (kf < K)
+#pragma unroll
+                        for (int i = 0; i < 9; ++i) v[i] += rb_[i * BA_THREADS + threadIdx.x * K + kf];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) V[(int64_t)i * L + lj] = v[i];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) gl[(int64_t)i * L + lj] = v[6 + i];
+                gm = fmax(gm, fmax(fabs(v[6]), fmax(fabs(v[7]), fabs(v[8]))));
+                if (first) {
+                    sl[lj] = 1.0 / (1.0 + sqrt(v[0]));
+                    sl[(int64_t)L + lj] = 1.0 / (1.0 + sqrt(v[3]));
+                    sl[2 * (int64_t)L + lj] = 1.0 / (1.0 + sqrt(v[5]));
+                }
+            }
+        }
+        cur = nxt;
+        o_nn = o_n2;
+    }
+    prof_mark(sh, PF_EVAL_J);
+    // pose sums: lanes of one keyframe combined in slot order
+    __syncthreads();
+    double* pr = sh.S;
+#pragma unroll
+    for (int i = 0; i < 27; ++i) pr[i * BA_THREADS + threadIdx.x] = acc[i];
+    cost += imu_factors(sh, c, xv, xb, true);
+    __syncthreads();
+    for (int e = threadIdx.x; e < 27 * K; e += BA_THREADS) {
+        const int k = e / 27, i = e - 27 * k;
+        if (sh.posef[k] < 0) continue;
+        double s = 0.0;
+#pragma unroll 8
+        for (int j = 0; j < g.LC; ++j) s += pr[i * BA_THREADS + j * K + k];
+        sh.U[k][i] = s;
+    }
+    const double total = block_sum(cost, sh.red);
+    const double anyfail = block_max((double)fail, sh.redm);
+    if (threadIdx.x == 0 && anyfail > 0.0) sh.st.fail = 1;
+    __syncthreads();
+    lin_tail(sh, c, first, gm);
+    return total;
+}
+
+// cost only at (xp, xl, xv, xb) (candidate evaluation), same walk
+__device__ __forceinline__ double eval_cost(BaShared& sh, const WinCtx& c, const double* xp, const double* xl, const double* xv,
+                            const double* xb) {
+    const BaWin& w = *c.w;
+    const int K = w.K, L = w.L;
+    pose_cache(sh, c, xp);
+    __syncthreads();
+    const Walk g = walk_geom(K);
+    const int pf = g.on ? sh.posef[g.kf] : -1;
+    const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
+    double cost = 0.0;
+    int fail = 0;
+    struct EvD { double P[3]; float u, v; int o, lv, out; };
+    auto ld_o = [&](int l) -> int { return (g.on && l < L) ? lk[16 * l + g.kf] : -1; };
+    auto ld_ev = [&](int l, int o, EvD& d) {
+        d.o = o;
+        if (o >= 0) {
+            d.lv = c.lm_var[l];
+            d.out = c.outlier[o];
+            d.u = c.obs_uv[2 * o];
+            d.v = c.obs_uv[2 * o + 1];
+            d.P[0] = xl[3 * l]; d.P[1] = xl[3 * l + 1]; d.P[2] = xl[3 * l + 2];
+        }
+    };
+    if (g.on) {
+        EvD cur;
+        int o_nn = ld_o(g.jf + g.LC);
+        ld_ev(g.jf, ld_o(g.jf), cur);
+        for (int l = g.jf; l < L; l += g.LC) {
+            EvD nxt;
+            nxt.o = -1;
+            int o_n2 = -1;
+            if (l + g.LC < L) {
+                ld_ev(l + g.LC, o_nn, nxt);
+                o_n2 = ld_o(l + 2 * g.LC);
+            }
+            if (cur.o >= 0 && (pf >= 0 || cur.lv)) {
+                double r[2], Jp[12], Jl[6];
+                bool jz;
+                if (factor_eval(sh.pc[g.kf], sh.Rcb_raw[g.kf], cur.P, (double)cur.u, (double)cur.v, w.cols, w.rows,
+                                w.Lw, cur.out != 0, w.is_pnp, false, r, Jp, Jl, jz)) {
+                    fail = 1;
+                } else {
+                    double cst, sc;
+                    huber(w.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
+                    cost += cst;
+                }
+            }
+            cur = nxt;
+            o_nn = o_n2;
         }
     }
-    double total = block_sum(cost, sh.red);
-    double anyfail = block_max((double)fail, sh.redm);
+    cost += imu_factors(sh, c, xv, xb, false);
+    const double total = block_sum(cost, sh.red);
+    const double anyfail = block_max((double)fail, sh.redm);
     if (threadIdx.x == 0 && anyfail > 0.0) sh.st.fail = 1;
     __syncthreads();
     return total;
@@ -362,92 +578,46 @@ __device__ __forceinline__ int imu_col(const BaWin& w, int k, int c) {
     return f < 0 ? -1 : f - w.np;
 }
 
-// Normal-equation statistics after a Jacobian evaluation: per-pose U/g, per-landmark V/g,
-// IMU H/g; gradient max-norm; column norms (for the Jacobi scaling at iteration 0).
-__device__ void linearise(BaShared& sh, const WinCtx& c, bool first) {
+// inverse of imu_col: column (0..11) of factor k holding imu index p, or -1
+__device__ __forceinline__ int imu_colinv(const BaWin& w, int k, int p) {
+    const int f = p + w.np;
+    if (w.vel_f[k - 1] >= 0 && f >= w.vel_f[k - 1] && f < w.vel_f[k - 1] + 3) return f - w.vel_f[k - 1];
+    if (w.bg_f >= 0 && f >= w.bg_f && f < w.bg_f + 3) return 3 + f - w.bg_f;
+    if (w.ba_f >= 0 && f >= w.ba_f && f < w.ba_f + 3) return 6 + f - w.ba_f;
+    if (w.vel_f[k] >= 0 && f >= w.vel_f[k] && f < w.vel_f[k] + 3) return 9 + f - w.vel_f[k];
+    return -1;
+}
+
+// After eval_lin: IMU normal equations (imu-space H, g), f-space gradient, column norms (Jacobi
+// scaling at iteration 0) and the gradient max-norm (gm = landmark part from the walk).
+__device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool first, double gm) {
     const BaWin& w = *c.w;
-    const int N = w.N, K = w.K, L = w.L;
-    const double* r0 = c.ws + c.L.r;
-    const double* jp = c.ws + c.L.jp;
-    const double* jl = c.ws + c.L.jl;
-    double gm = 0.0;
-    // landmarks
-    double* V = c.ws + c.L.V;
-    double* gl = c.ws + c.L.gl;
-    double* sl = c.ws + c.L.s_l;
-    for (int l = threadIdx.x; l < L; l += BA_THREADS) {
-        if (!c.lm_var[l]) continue;
-        double v[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-        for (int o = c.lm_ptr[l]; o < c.lm_ptr[l + 1]; ++o) {
-            double a0 = jl[o], a1 = jl[(int64_t)N + o], a2 = jl[2 * (int64_t)N + o];
-            double b0 = jl[3 * (int64_t)N + o], b1 = jl[4 * (int64_t)N + o], b2 = jl[5 * (int64_t)N + o];
-            double ra = r0[o], rb = r0[N + o];
-            v[0] += a0 * a0 + b0 * b0; v[1] += a0 * a1 + b0 * b1; v[2] += a0 * a2 + b0 * b2;
-            v[3] += a1 * a1 + b1 * b1; v[4] += a1 * a2 + b1 * b2; v[5] += a2 * a2 + b2 * b2;
-            g[0] += a0 * ra + b0 * rb; g[1] += a1 * ra + b1 * rb; g[2] += a2 * ra + b2 * rb;
-        }
-        for (int i = 0; i < 6; ++i) V[(int64_t)i * L + l] = v[i];
-        for (int i = 0; i < 3; ++i) gl[(int64_t)i * L + l] = g[i];
-        gm = fmax(gm, fmax(fabs(g[0]), fmax(fabs(g[1]), fabs(g[2]))));
-        if (first) {
-            sl[l] = 1.0 / (1.0 + sqrt(v[0]));
-            sl[(int64_t)L + l] = 1.0 / (1.0 + sqrt(v[3]));
-            sl[2 * (int64_t)L + l] = 1.0 / (1.0 + sqrt(v[5]));
-        }
-    }
-    // poses: one wave per pose, lanes over that pose's observations
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int k = wid; k < K; k += BA_THREADS / 64) {
-        if (w.pose_f[k] < 0) continue;
-        double acc[27];
-#pragma unroll
-        for (int i = 0; i < 27; ++i) acc[i] = 0.0;
-        for (int q = c.kf_ptr[k] + lane; q < c.kf_ptr[k + 1]; q += 64) {
-            int o = c.kf_obs[q];
-            double a[6], b[6];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) { a[i] = jp[(int64_t)i * N + o]; b[i] = jp[(int64_t)(6 + i) * N + o]; }
-            double ra = r0[o], rb = r0[N + o];
-            int idx = 0;
-#pragma unroll
-            for (int i = 0; i < 6; ++i)
-#pragma unroll
-                for (int j = i; j < 6; ++j) acc[idx++] += a[i] * a[j] + b[i] * b[j];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) acc[21 + i] += a[i] * ra + b[i] * rb;
-        }
-#pragma unroll
-        for (int i = 0; i < 27; ++i) acc[i] = wave_sum(acc[i]);
-        if (lane == 0)
-            for (int i = 0; i < 27; ++i) sh.U[k][i] = acc[i];
-    }
+    const int K = w.K;
     // IMU: per-factor residual/J already in LDS; assemble imu-space H (global) and g.  Factors are
     // added one after another (fixed order); inside a factor the 12 columns map to distinct entries.
     if (w.is_vi) {
+        // one lane per entry of H (and of g), factors added in order: no read-modify-write rounds
         const int ni = w.ni;
-        for (int e = threadIdx.x; e < ni * ni; e += BA_THREADS) c.Himu[e] = 0.0;
-        for (int p = threadIdx.x; p < ni; p += BA_THREADS) c.gimu[p] = 0.0;
-        __syncthreads();
-        for (int k = 1; k < K; ++k) {
-            if (!c.preint_valid[k]) continue;
-            for (int e = threadIdx.x; e < 144 + 12; e += BA_THREADS) {
-                if (e < 144) {
-                    int cp = e / 12, cq = e % 12;
-                    int p = imu_col(w, k, cp), q = imu_col(w, k, cq);
-                    if (p < 0 || q < 0) continue;
-                    double h = 0.0;
-                    for (int i = 0; i < 9; ++i) h += sh.imu_J[k][12 * i + cp] * sh.imu_J[k][12 * i + cq];
-                    c.Himu[p * ni + q] += h;
+        for (int e = threadIdx.x; e < ni * ni + ni; e += BA_THREADS) {
+            const bool isg = e >= ni * ni;
+            const int p = isg ? e - ni * ni : e / ni, q = isg ? 0 : e - (e / ni) * ni;
+            double acc = 0.0;
+            for (int k = 1; k < K; ++k) {
+                if (!sh.pvalid[k]) continue;
+                const int cp = imu_colinv(w, k, p);
+                if (cp < 0) continue;
+                double h = 0.0;
+                if (isg) {
+                    for (int i = 0; i < 9; ++i) h += sh.imu_J[k][12 * i + cp] * sh.imu_r[k][i];
                 } else {
-                    int cp = e - 144;
-                    int p = imu_col(w, k, cp);
-                    if (p < 0) continue;
-                    double g = 0.0;
-                    for (int i = 0; i < 9; ++i) g += sh.imu_J[k][12 * i + cp] * sh.imu_r[k][i];
-                    c.gimu[p] += g;
+                    const int cq = imu_colinv(w, k, q);
+                    if (cq < 0) continue;
+                    for (int i = 0; i < 9; ++i) h += sh.imu_J[k][12 * i + cp] * sh.imu_J[k][12 * i + cq];
                 }
+                acc += h;
             }
-            __syncthreads();
+            if (isg) c.gimu[p] = acc;
+            else c.Himu[e] = acc;
         }
     }
     __syncthreads();
@@ -483,7 +653,7 @@ __device__ void linearise(BaShared& sh, const WinCtx& c, bool first) {
 // Reduced system before the Schur update (schur_eliminator_impl.h:179-377 E^T E-free part): zero,
 // Jacobi-scaled pose blocks U, IMU block, LM diagonal.  Also the panel area of schur_gemm is S
 // itself, so this runs after the landmark loop.
-__device__ void assemble_S(BaShared& sh, const WinCtx& c) {
+__device__ __forceinline__ void assemble_S(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
     const int nf = w.nf, ls = s_ld(nf), npS = 16 * ((nf + 15) >> 4);
     for (int e = threadIdx.x; e < npS * ls; e += BA_THREADS) sh.S[e] = 0.0;
@@ -510,15 +680,15 @@ __device__ void assemble_S(BaShared& sh, const WinCtx& c) {
     __syncthreads();
 }
 
-// Schur GEMM: S_pp -= Y W^T and b_p -= Y g over landmark chunks (Y = W~ V~^-1), on
-// v_mfma_f64_16x16x4_f64.  Per chunk of LC landmarks, fill lanes (landmark slot, keyframe) write
-// their pose's 6 rows of the k-major LDS panels At/Bt (k = 3*landmark + component; the value, or
-// zero when the keyframe does not see the landmark).  Each wave owns a fixed set of the
-// lower-triangle 16x16 output tiles (the Cholesky reads S on and below the diagonal only) and
-// accumulates them over all chunks in registers, the rhs column on the VALU beside it.  The panels
-// alias S (assembled afterwards), and the global loads of chunk c+1 (observation index one chunk
-// further ahead) are in flight while chunk c runs on the matrix cores.  Fixed per-lane k order and
-// a fixed shuffle tree: bitwise reproducible.
+// Schur GEMM (schur_eliminator_impl.h:179-377): with V~_l = L_l L_l^T (L_l^-1 kept per landmark),
+// S_pp -= Z Z^T and b_p -= Z h over landmark chunks, where Z = W~ L^-T (the pose x landmark block,
+// 6x3 per observation) and h = L^-1 g~_l.  One k-major LDS panel Zt (k = 3*landmark slot + comp)
+// feeds both MFMA operands: a step reads T fragments and issues all T(T+1)/2 lower-triangle tile
+// products (v_mfma_f64_16x16x4_f64).  The k-steps of a chunk are split over the waves (every wave
+// owns every tile: no per-tile branches, balanced), partial tiles are combined wave after wave
+// into S at the end (fixed order).  Two panel buffers: while the matrix cores run chunk c, the
+// fill lanes (landmark slot, keyframe) write chunk c+1 from registers whose global loads were
+// issued one chunk earlier; one barrier per chunk.  Bitwise reproducible.
 using d4 = __attribute__((ext_vector_type(4))) double;
 
 constexpr int BA_PANEL = BA_NF_MAX * (BA_NF_MAX + 1) + BA_STAGE;  // S followed by stage
@@ -526,54 +696,52 @@ __host__ __device__ constexpr int schur_ks(int T) { return (T & 1) ? 16 * T : 16
 __host__ __device__ constexpr int schur_kc(int LC) { return (3 * LC + 3) & ~3; }
 __host__ __device__ constexpr int schur_lc(int T) {
     int lc = 1;
-    while (2 * schur_kc(lc + 1) * schur_ks(T) <= BA_PANEL && schur_kc(lc + 1) <= BA_GCOL) ++lc;
+    while (2 * schur_kc(lc + 1) * schur_ks(T) <= BA_PANEL && 2 * schur_kc(lc + 1) <= BA_GCOL) ++lc;
     return lc;
 }
 
-template <int T>
-__device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
+template <int TM>
+__device__ __forceinline__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
     const int N = w.N, L = w.L, K = w.K, np = w.np;
-    constexpr int KS = schur_ks(T);     // k-row stride (doubles): the 4 k-rows of a fragment hit both bank halves
-    constexpr int LCMAX = schur_lc(T);
+    constexpr int T = TM;               // pose-row tiles
     constexpr int NT = T * (T + 1) / 2;
-    constexpr int TPW = (NT + 3) / 4;   // lower tiles per wave
-    constexpr int RPW = (T + 3) / 4;    // rhs row groups per wave
+    constexpr int G = T >= 5 ? 2 : 1;   // wave groups: each owns a contiguous range of the NT tiles
+    constexpr int H = (NT + G - 1) / G; // tiles per group (accumulator registers: 8 per tile)
+    constexpr int KS = schur_ks(T);     // k-row stride (doubles): a fragment's 4 k-rows hit both bank halves
+    constexpr int LCMAX = schur_lc(T);
+    constexpr int NW = BA_THREADS / 64;
     const int LC = min(LCMAX, BA_THREADS / K);  // landmarks per chunk: one fill lane per (landmark, keyframe)
     const int KC = schur_kc(LC);
-    double* At = sh.S;
-    double* Bt = sh.S + KC * KS;
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wid = wave_id(), lane = threadIdx.x & 63;
     const int r16 = lane & 15, kk = lane >> 4;
     const double* jp = c.ws + c.L.jp;
     const double* jl = c.ws + c.L.jl;
-    const double* Vi = c.ws + c.L.Vi;
+    const double* Li = c.ws + c.L.Vi;   // L^-1 of V~ per landmark: i00 i10 i11 i20 i21 i22
     const double* gl = c.ws + c.L.gl;
     const double* sl = c.ws + c.L.s_l;
     const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
-    int trow[TPW], tcol[TPW];
+    d4 acc[H];
 #pragma unroll
-    for (int m = 0; m < TPW; ++m) {
-        int t = wid + 4 * m, r = 0;
-        if (t >= NT) { trow[m] = -1; tcol[m] = 0; continue; }
-        while (t > r) { t -= r + 1; ++r; }
-        trow[m] = r; tcol[m] = t;
-    }
-    d4 acc[TPW];
+    for (int t = 0; t < H; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    constexpr int WPG = (BA_THREADS / 64) / G;  // waves per group: they split the k-steps
+    const int grp = wave_id() / WPG, mem = wave_id() - grp * WPG;
+    double bacc[T];
 #pragma unroll
-    for (int m = 0; m < TPW; ++m) acc[m] = d4{0.0, 0.0, 0.0, 0.0};
-    double bacc[RPW];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) bacc[q] = 0.0;
+    for (int r = 0; r < T; ++r) bacc[r] = 0.0;
 
     const int jf = threadIdx.x / K, kf = threadIdx.x - jf * K;
     const int pf = jf < LC ? sh.posef[kf] : -1;
-    // prefetch registers: observation of the chunk after next, data of the next chunk
-    int o_next = -1;
-    double pj[12], lj[6], sv[3], vv[6], gq = 0.0;
-    auto load_obs = [&](int l0n) -> int {
+    // prefetch registers (one chunk ahead); a loaded value is consumed only where it is used
+    int o_nx = -1, v_nx = 0;
+    double pj[12], lj[6], sv[3], li[6];
+    double hg[3], hs[3], hl[6];
+    int hv = 0;
+    auto load_obs = [&](int l0n, int& o, int& v) {
         const int l = l0n + jf;
-        return (pf >= 0 && l < L) ? lk[16 * l + kf] : -1;
+        o = -1;
+        v = 0;
+        if (pf >= 0 && l < L) { o = lk[16 * l + kf]; v = c.lm_var[l]; }  // independent loads
     };
     auto load_data = [&](int l0n, int o) {
         const int l = l0n + jf;
@@ -585,26 +753,23 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) sv[i] = sl[(int64_t)i * L + l];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) vv[i] = Vi[(int64_t)i * L + l];
+            for (int i = 0; i < 6; ++i) li[i] = Li[(int64_t)i * L + l];
         }
-        gq = 0.0;
-        if (threadIdx.x < KC) {
-            const int lg = l0n + threadIdx.x / 3, cg = threadIdx.x % 3;
-            if (lg < min(l0n + LC, L) && c.lm_var[lg]) gq = gl[(int64_t)cg * L + lg] * sl[(int64_t)cg * L + lg];
+        hv = 0;
+        const int lg = l0n + (int)threadIdx.x;
+        if ((int)threadIdx.x < LC && lg < L) {
+            hv = c.lm_var[lg];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { hg[i] = gl[(int64_t)i * L + lg]; hs[i] = sl[(int64_t)i * L + lg]; }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) hl[i] = Li[(int64_t)i * L + lg];
         }
     };
-    for (int e = threadIdx.x; e < 2 * KC * KS; e += BA_THREADS) sh.S[e] = 0.0;
-    int o_cur = load_obs(0);
-    load_data(0, o_cur);
-    o_next = load_obs(LC);
-    __syncthreads();
-    for (int l0 = 0; l0 < L; l0 += LC) {
-        const int l1 = min(l0 + LC, L);
-        // ---- fill chunk [l0, l1) from the prefetch registers
-        if (threadIdx.x < KC) sh.gcol[threadIdx.x] = gq;
+    auto fill = [&](int buf, int o) {
+        double* Zt = sh.S + buf * KC * KS;
         if (pf >= 0) {
-            double Y[6][3], Wv[6][3];
-            if (o_cur >= 0) {
+            double Z[6][3];
+            if (o >= 0) {
                 const double b0 = lj[0] * sv[0], b1 = lj[1] * sv[1], b2 = lj[2] * sv[2];
                 const double d0 = lj[3] * sv[0], d1 = lj[4] * sv[1], d2 = lj[5] * sv[2];
 #pragma unroll
@@ -612,75 +777,135 @@ __device__ void schur_gemm(BaShared& sh, const WinCtx& c) {
                     const double sp = sh.s_f[pf + i];
                     const double a = pj[i] * sp, e = pj[6 + i] * sp;
                     const double W0 = a * b0 + e * d0, W1 = a * b1 + e * d1, W2 = a * b2 + e * d2;
-                    Wv[i][0] = W0; Wv[i][1] = W1; Wv[i][2] = W2;
-                    Y[i][0] = W0 * vv[0] + W1 * vv[1] + W2 * vv[2];
-                    Y[i][1] = W0 * vv[1] + W1 * vv[3] + W2 * vv[4];
-                    Y[i][2] = W0 * vv[2] + W1 * vv[4] + W2 * vv[5];
+                    Z[i][0] = W0 * li[0];
+                    Z[i][1] = W0 * li[1] + W1 * li[2];
+                    Z[i][2] = W0 * li[3] + W1 * li[4] + W2 * li[5];
                 }
             } else {
 #pragma unroll
                 for (int i = 0; i < 6; ++i)
 #pragma unroll
-                    for (int cc = 0; cc < 3; ++cc) { Y[i][cc] = 0.0; Wv[i][cc] = 0.0; }
+                    for (int cc = 0; cc < 3; ++cc) Z[i][cc] = 0.0;
             }
 #pragma unroll
             for (int cc = 0; cc < 3; ++cc)
 #pragma unroll
-                for (int i = 0; i < 6; ++i) {
-                    At[(3 * jf + cc) * KS + pf + i] = Y[i][cc];
-                    Bt[(3 * jf + cc) * KS + pf + i] = Wv[i][cc];
-                }
+                for (int i = 0; i < 6; ++i) Zt[(3 * jf + cc) * KS + pf + i] = Z[i][cc];
         }
-        __syncthreads();
-        prof_mark(sh, PF_FILL);
-        // ---- prefetch: data of the next chunk, observation index of the one after
-        o_cur = o_next;
-        if (l1 < L) {
-            load_data(l1, o_cur);
-            o_next = load_obs(l1 + LC);
-        }
-        // ---- MFMA over the chunk
-        const int nsteps = (3 * (l1 - l0) + 3) >> 2;
-        for (int st = 0; st < nsteps; ++st) {
-            const int kr = (4 * st + kk) * KS;
-#pragma unroll
-            for (int m = 0; m < TPW; ++m) {
-                if (trow[m] < 0) continue;
-                const double a = At[kr + 16 * trow[m] + r16];
-                const double b = Bt[kr + 16 * tcol[m] + r16];
-                acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[m], 0, 0, 0);
+        if ((int)threadIdx.x < LC) {
+            double* G = sh.gcol + buf * KC;
+            double h0 = 0.0, h1 = 0.0, h2 = 0.0;
+            if (hv) {
+                const double g0 = hg[0] * hs[0], g1 = hg[1] * hs[1], g2 = hg[2] * hs[2];
+                h0 = hl[0] * g0;
+                h1 = hl[1] * g0 + hl[2] * g1;
+                h2 = hl[3] * g0 + hl[4] * g1 + hl[5] * g2;
             }
-            const double g = sh.gcol[4 * st + kk];
-#pragma unroll
-            for (int q = 0; q < RPW; ++q) {
-                const int rg = wid + 4 * q;
-                if (rg < T) bacc[q] += At[kr + 16 * rg + r16] * g;
-            }
+            G[3 * threadIdx.x] = h0;
+            G[3 * threadIdx.x + 1] = h1;
+            G[3 * threadIdx.x + 2] = h2;
         }
+    };
+    // both panels zero: rows of constant poses, padding rows and padding k-rows stay zero
+    for (int e = threadIdx.x; e < 2 * KC * KS; e += BA_THREADS) sh.S[e] = 0.0;
+    for (int e = threadIdx.x; e < 2 * KC; e += BA_THREADS) sh.gcol[e] = 0.0;
+    {
+        int o0, v0;
+        load_obs(0, o0, v0);
+        load_data(0, v0 ? o0 : -1);
         __syncthreads();
-        prof_mark(sh, PF_GEMM);
+        fill(0, v0 ? o0 : -1);
     }
-    assemble_S(sh, c);
-    const int ls = s_ld(w.nf);
-#pragma unroll
-    for (int m = 0; m < TPW; ++m) {
-        if (trow[m] < 0) continue;
-        const int col = 16 * tcol[m] + r16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = 16 * trow[m] + 4 * r + kk;
-            if (row < np && col < np) sh.S[row * ls + col] -= acc[m][r];
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-        double v = bacc[q];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        const int row = 16 * (wid + 4 * q) + r16;
-        if (kk == 0 && wid + 4 * q < T && row < np) sh.b[row] -= v;
+    if (LC < L) {
+        load_obs(LC, o_nx, v_nx);
+        load_data(LC, v_nx ? o_nx : -1);
     }
     __syncthreads();
+    prof_mark(sh, PF_FILL);
+    for (int l0 = 0, ci = 0; l0 < L; l0 += LC, ++ci) {
+        const int buf = ci & 1;
+        const int l1 = min(l0 + LC, L);
+        // ---- matrix cores: this wave's k-steps of chunk ci
+        {
+            const double* Zt = sh.S + buf * KC * KS;
+            const double* Gc = sh.gcol + buf * KC;
+            const int nsteps = (3 * (l1 - l0) + 3) >> 2;
+            for (int st = mem; st < nsteps; st += WPG) {
+                const int kr = (4 * st + kk) * KS;
+                double f[T];
+#pragma unroll
+                for (int r = 0; r < T; ++r) f[r] = Zt[kr + 16 * r + r16];
+                if (grp == 0) {
+#pragma unroll
+                    for (int r = 0, t = 0; r < T; ++r)
+#pragma unroll
+                        for (int q = 0; q <= r; ++q, ++t)
+                            if (t < H) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[r], f[q], acc[t], 0, 0, 0);
+                    const double g = Gc[4 * st + kk];
+#pragma unroll
+                    for (int r = 0; r < T; ++r) bacc[r] += f[r] * g;
+                } else {
+#pragma unroll
+                    for (int r = 0, t = 0; r < T; ++r)
+#pragma unroll
+                        for (int q = 0; q <= r; ++q, ++t)
+                            if (t >= H) acc[t - H] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[r], f[q], acc[t - H], 0, 0, 0);
+                }
+            }
+        }
+        prof_mark(sh, PF_GEMM);
+        // ---- fill chunk ci+1 into the other buffer, then issue the loads of chunk ci+2
+        if (l1 < L) {
+            const int o = v_nx ? o_nx : -1;
+            fill(buf ^ 1, o);
+            if (l1 + LC < L) {
+                load_obs(l1 + LC, o_nx, v_nx);
+                load_data(l1 + LC, v_nx ? o_nx : -1);
+            }
+        }
+        __syncthreads();
+        prof_mark(sh, PF_PFX);
+    }
+    assemble_S(sh, c);
+    // partial tiles and rhs of each wave into S / b, wave after wave (fixed order)
+    const int ls = s_ld(w.nf);
+#pragma unroll
+    for (int r = 0; r < T; ++r) {
+        bacc[r] += __shfl_xor(bacc[r], 16, 64);
+        bacc[r] += __shfl_xor(bacc[r], 32, 64);
+    }
+    for (int wv = 0; wv < NW; ++wv) {
+        if (wid == wv) {
+            auto put = [&](int r, int q, const d4& a) {
+                const int col = 16 * q + r16;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int row = 16 * r + 4 * e + kk;
+                    if (row < np && col < np) sh.S[row * ls + col] -= a[e];
+                }
+            };
+            if (grp == 0) {
+#pragma unroll
+                for (int r = 0, t = 0; r < T; ++r)
+#pragma unroll
+                    for (int q = 0; q <= r; ++q, ++t)
+                        if (t < H) put(r, q, acc[t]);
+            } else {
+#pragma unroll
+                for (int r = 0, t = 0; r < T; ++r)
+#pragma unroll
+                    for (int q = 0; q <= r; ++q, ++t)
+                        if (t >= H) put(r, q, acc[t - H]);
+            }
+#pragma unroll
+            for (int r = 0; r < T; ++r) {
+                const int row = 16 * r + r16;
+                if (kk == 0 && row < np) sh.b[row] -= bacc[r];
+            }
+        }
+        __syncthreads();
+    }
+    prof_mark(sh, PF_ASM);
 }
 
 // Cholesky of S (nf x nf in LDS, padded to nb = ceil(nf/16) 16x16 tiles with an identity tail,
@@ -703,7 +928,7 @@ __device__ __noinline__ bool cholesky_solve(BaShared& sh, int nf) {
     double* LB = sh.stage;  // [nb][16 m][16 c] = Linv_J[c][m]
     const int ls = s_ld(nf), nb = (nf + 15) >> 4;
     constexpr int NW = BA_THREADS / 64;
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wid = wave_id(), lane = threadIdx.x & 63;
     const int r16 = lane & 15, kk = lane >> 4;
     for (int J = 0; J < nb; ++J) {
         const int c0 = 16 * J;
@@ -832,7 +1057,7 @@ __device__ __noinline__ bool cholesky_solve(BaShared& sh, int nf) {
 }
 
 // One LM step computation (ComputeTrustRegionStep): returns validity uniformly via sh.st.valid.
-__device__ void compute_step(BaShared& sh, const WinCtx& c) {
+__device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
     const int N = w.N, L = w.L, nf = w.nf;
     const double radius = sh.st.radius;
@@ -867,12 +1092,12 @@ __device__ void compute_step(BaShared& sh, const WinCtx& c) {
         double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
         double i10 = -l10 * i00 * i11, i21 = -l21 * i11 * i22;
         double i20 = -(l20 * i00 + l21 * i10) * i22;
-        Vi[l] = i00 * i00 + i10 * i10 + i20 * i20;
-        Vi[(int64_t)L + l] = i10 * i11 + i20 * i21;
-        Vi[2 * (int64_t)L + l] = i20 * i22;
-        Vi[3 * (int64_t)L + l] = i11 * i11 + i21 * i21;
-        Vi[4 * (int64_t)L + l] = i21 * i22;
-        Vi[5 * (int64_t)L + l] = i22 * i22;
+        Vi[l] = i00;   // L^-1 (lower): V~^-1 = L^-T L^-1 is applied factor by factor
+        Vi[(int64_t)L + l] = i10;
+        Vi[2 * (int64_t)L + l] = i11;
+        Vi[3 * (int64_t)L + l] = i20;
+        Vi[4 * (int64_t)L + l] = i21;
+        Vi[5 * (int64_t)L + l] = i22;
     }
     // (2) f-space: LM diagonal and S/b init
     for (int f = threadIdx.x; f < nf; f += BA_THREADS) {
@@ -911,77 +1136,156 @@ __device__ void compute_step(BaShared& sh, const WinCtx& c) {
         __syncthreads();
         return;
     }
-    // (5) back-substitution for the points: y_l = V~^-1 (g~_l - W~^T y_p)
-    const double* jp = c.ws + c.L.jp;
-    const double* jl = c.ws + c.L.jl;
-    double fin = 0.0;
-    for (int l = threadIdx.x; l < L; l += BA_THREADS) {
-        if (!c.lm_var[l]) continue;
-        double s[3] = {sl[l], sl[(int64_t)L + l], sl[2 * (int64_t)L + l]};
-        double rhs[3];
-        for (int cc = 0; cc < 3; ++cc) rhs[cc] = gl[(int64_t)cc * L + l] * s[cc];
-        for (int o = c.lm_ptr[l]; o < c.lm_ptr[l + 1]; ++o) {
-            int pf = w.pose_f[c.obs_kf[o]];
-            if (pf < 0) continue;
-            double e0 = 0, e1 = 0;  // (Jp s_p) y_p  for both residual rows
-            for (int i = 0; i < 6; ++i) {
-                double yp = sh.b[pf + i] * sh.s_f[pf + i];
-                e0 += jp[(int64_t)i * N + o] * yp;
-                e1 += jp[(int64_t)(6 + i) * N + o] * yp;
-            }
-            for (int cc = 0; cc < 3; ++cc)
-                rhs[cc] -= s[cc] * (jl[(int64_t)cc * N + o] * e0 + jl[(int64_t)(3 + cc) * N + o] * e1);
-        }
-        double vi[6];
-        for (int i = 0; i < 6; ++i) vi[i] = Vi[(int64_t)i * L + l];
-        double y0 = vi[0] * rhs[0] + vi[1] * rhs[1] + vi[2] * rhs[2];
-        double y1 = vi[1] * rhs[0] + vi[3] * rhs[1] + vi[4] * rhs[2];
-        double y2 = vi[2] * rhs[0] + vi[4] * rhs[1] + vi[5] * rhs[2];
-        yl[l] = y0; yl[(int64_t)L + l] = y1; yl[2 * (int64_t)L + l] = y2;
-        if (!isfinite(y0) || !isfinite(y1) || !isfinite(y2)) fin = 1.0;
-    }
-    for (int f = threadIdx.x; f < nf; f += BA_THREADS)
-        if (!isfinite(sh.b[f])) fin = 1.0;
-    double nonfinite = block_max(fin, sh.redm);
-    if (threadIdx.x == 0) sh.st.valid = nonfinite > 0.0 ? 0 : 1;
+    // (5) back-substitution for the points, y_l = V~^-1 (g~_l - W~^T y_p), in one walk with the
+    // observation part of the model change -(J delta)^T (r + J delta / 2) (trust_region_minimizer.cc
+    // :424-439) and the landmark candidates: the Jacobians are read once, coalesced.
+    for (int f = threadIdx.x; f < nf; f += BA_THREADS) sh.D_f[f] = -sh.b[f] * sh.s_f[f];  // delta_f
     __syncthreads();
-    prof_mark(sh, PF_BACKSUB);
-}
-
-// delta = -y .* s ; model cost change -(J delta)^T (r + J delta / 2); candidate = x + delta
-__device__ void make_candidate(BaShared& sh, const WinCtx& c) {
-    const BaWin& w = *c.w;
-    const int N = w.N, L = w.L, K = w.K;
+    const int K = w.K;
+    const Walk g = walk_geom(K);
+    const int pf = g.on ? sh.posef[g.kf] : -1;
+    const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
     const double* r0 = c.ws + c.L.r;
     const double* jp = c.ws + c.L.jp;
     const double* jl = c.ws + c.L.jl;
-    const double* sl = c.ws + c.L.s_l;
-    const double* yl = c.ws + c.L.y_l;
-    double* ws = c.ws;
-    // f-space deltas into sh.D_f (reuse) : delta_f = -y_f * s_f
-    for (int f = threadIdx.x; f < w.nf; f += BA_THREADS) sh.D_f[f] = -sh.b[f] * sh.s_f[f];
-    __syncthreads();
-    double mc = 0.0, sn = 0.0, xn = 0.0;
-    for (int o = threadIdx.x; o < N; o += BA_THREADS) {
-        int k = c.obs_kf[o], l = c.obs_lm[o];
-        int pf = w.pose_f[k];
-        bool lv = c.lm_var[l];
-        if (pf < 0 && !lv) continue;
-        double m0 = 0, m1 = 0;
-        if (pf >= 0)
-            for (int i = 0; i < 6; ++i) {
-                double d = sh.D_f[pf + i];
-                m0 += jp[(int64_t)i * N + o] * d;
-                m1 += jp[(int64_t)(6 + i) * N + o] * d;
+    const double* xl = c.ws + c.L.x_lm;
+    double* cl = c.ws + c.L.c_lm;
+    double* red = sh.S;                    // [3][BA_THREADS] per-lane W^T-terms
+    double* dls = sh.S + 3 * BA_THREADS;   // [LC][3] landmark steps of the chunk
+    double fin = 0.0, mc = 0.0, sn = 0.0, xn = 0.0;
+    // software pipeline: observation index two chunks ahead, lane and slot data one chunk ahead
+    struct ObsD { double j6[6], p12[12], ra, rb; int o, lv; };
+    struct LmD { double sv[3], gv[3], vi[6], x[3]; int lv; };
+    auto ld_o = [&](int l0n) -> int {
+        const int l = l0n + g.jf;
+        return (g.on && l < L) ? lk[16 * l + g.kf] : -1;
+    };
+    auto ld_obs = [&](int l0n, int o, ObsD& d) {
+        d.o = o;
+        d.lv = 0;
+        if (o >= 0) {
+            d.lv = c.lm_var[l0n + g.jf];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) d.j6[i] = jl[(int64_t)i * N + o];
+            d.ra = r0[o];
+            d.rb = r0[N + o];
+            if (pf >= 0) {
+#pragma unroll
+                for (int i = 0; i < 12; ++i) d.p12[i] = jp[(int64_t)i * N + o];
             }
-        if (lv)
+        }
+    };
+    auto ld_lm = [&](int l0n, LmD& d) {
+        const int lj = l0n + threadIdx.x;
+        d.lv = 0;
+        if ((int)threadIdx.x < g.LC && lj < L) {
+            d.lv = c.lm_var[lj];
+#pragma unroll
             for (int cc = 0; cc < 3; ++cc) {
-                double d = -yl[(int64_t)cc * L + l] * sl[(int64_t)cc * L + l];
-                m0 += jl[(int64_t)cc * N + o] * d;
-                m1 += jl[(int64_t)(3 + cc) * N + o] * d;
+                d.sv[cc] = sl[(int64_t)cc * L + lj];
+                d.gv[cc] = gl[(int64_t)cc * L + lj];
+                d.x[cc] = xl[3 * lj + cc];
             }
-        mc -= m0 * (r0[o] + m0 / 2.0) + m1 * (r0[N + o] + m1 / 2.0);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) d.vi[i] = Vi[(int64_t)i * L + lj];
+        }
+    };
+    ObsD cur;
+    LmD lcur;
+    int o_nn = ld_o(g.LC);
+    ld_obs(0, ld_o(0), cur);
+    ld_lm(0, lcur);
+    for (int l0 = 0; l0 < L; l0 += g.LC) {
+        ObsD nxt;
+        LmD lnxt;
+        nxt.o = -1; nxt.lv = 0; lnxt.lv = 0;
+        int o_n2 = -1;
+        if (l0 + g.LC < L) {
+            ld_obs(l0 + g.LC, o_nn, nxt);
+            ld_lm(l0 + g.LC, lnxt);
+            o_n2 = ld_o(l0 + 2 * g.LC);
+        }
+        const bool lv = cur.o >= 0 && cur.lv;
+        const bool act = cur.o >= 0 && (pf >= 0 || cur.lv);
+        double e0 = 0.0, e1 = 0.0;
+        if (act && pf >= 0) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double d = sh.D_f[pf + i];
+                e0 += cur.p12[i] * d;
+                e1 += cur.p12[6 + i] * d;
+            }
+        }
+        const bool contrib = lv && pf >= 0;
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc)
+            red[cc * BA_THREADS + threadIdx.x] = contrib ? cur.j6[cc] * e0 + cur.j6[3 + cc] * e1 : 0.0;
+        __syncthreads();
+        if ((int)threadIdx.x < g.LC) {
+            const int lj = l0 + threadIdx.x;
+            if (lj < L) {
+                double d[3] = {0.0, 0.0, 0.0};
+                if (lcur.lv) {
+                    double rhs[3];
+#pragma unroll
+                    for (int cc = 0; cc < 3; ++cc) {
+                        double t = 0.0;
+#pragma unroll
+                        for (int kf = 0; kf < BA_KMAX; ++kf)
+                            if (kf < K) t += red[cc * BA_THREADS + threadIdx.x * K + kf];
+                        rhs[cc] = lcur.gv[cc] * lcur.sv[cc] + lcur.sv[cc] * t;
+                    }
+                    const double* li = lcur.vi;  // y = L^-T (L^-1 rhs)
+                    const double t0 = li[0] * rhs[0];
+                    const double t1 = li[1] * rhs[0] + li[2] * rhs[1];
+                    const double t2 = li[3] * rhs[0] + li[4] * rhs[1] + li[5] * rhs[2];
+                    const double y0 = li[0] * t0 + li[1] * t1 + li[3] * t2;
+                    const double y1 = li[2] * t1 + li[4] * t2;
+                    const double y2 = li[5] * t2;
+                    yl[lj] = y0;
+                    yl[(int64_t)L + lj] = y1;
+                    yl[2 * (int64_t)L + lj] = y2;
+                    if (!isfinite(y0) || !isfinite(y1) || !isfinite(y2)) fin = 1.0;
+                    d[0] = -y0 * lcur.sv[0];
+                    d[1] = -y1 * lcur.sv[1];
+                    d[2] = -y2 * lcur.sv[2];
+                }
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) {
+                    const double x = lcur.x[cc];
+                    const double cnd = lcur.lv ? x + d[cc] : x;
+                    cl[3 * lj + cc] = cnd;
+                    if (lcur.lv) {
+                        const double dd = x - cnd;
+                        sn += dd * dd;
+                        xn += cnd * cnd;
+                    }
+                    dls[3 * threadIdx.x + cc] = d[cc];
+                }
+            }
+        }
+        __syncthreads();
+        if (act) {
+            double m0 = e0, m1 = e1;
+            if (lv) {
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) {
+                    const double d = dls[3 * g.jf + cc];
+                    m0 += cur.j6[cc] * d;
+                    m1 += cur.j6[3 + cc] * d;
+                }
+            }
+            mc -= m0 * (cur.ra + m0 / 2.0) + m1 * (cur.rb + m1 / 2.0);
+        }
+        cur = nxt;
+        lcur = lnxt;
+        o_nn = o_n2;
     }
+    for (int f = threadIdx.x; f < nf; f += BA_THREADS)
+        if (!isfinite(sh.b[f])) fin = 1.0;
+    prof_mark(sh, PF_BACKSUB);
+    // IMU part of the model change, pose / velocity / bias candidates and norms
+    double* ws = c.ws;
     if (w.is_vi) {
         for (int k = 1 + threadIdx.x; k < K; k += BA_THREADS) {
             if (!c.preint_valid[k]) continue;
@@ -996,25 +1300,16 @@ __device__ void make_candidate(BaShared& sh, const WinCtx& c) {
             for (int i = 0; i < 9; ++i) mc -= m[i] * (sh.imu_r[k][i] + m[i] / 2.0);
         }
     }
-    // candidate and norms (x - candidate computed like Ceres' (x_ - candidate_x_).norm())
     double* xp = ws + c.L.x_pose; double* cp_ = ws + c.L.c_pose;
-    double* xl = ws + c.L.x_lm;   double* cl = ws + c.L.c_lm;
     double* xv = ws + c.L.x_vel;  double* cv = ws + c.L.c_vel;
     double* xb = ws + c.L.x_bias; double* cb = ws + c.L.c_bias;
     for (int e = threadIdx.x; e < 6 * K; e += BA_THREADS) {
         int k = e / 6, i = e % 6;
-        int pf = w.pose_f[k];
+        int pfk = w.pose_f[k];
         double x = xp[e];
-        double cnd = pf >= 0 ? x + sh.D_f[pf + i] : x;
+        double cnd = pfk >= 0 ? x + sh.D_f[pfk + i] : x;
         cp_[e] = cnd;
-        if (pf >= 0) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
-    }
-    for (int e = threadIdx.x; e < 3 * L; e += BA_THREADS) {
-        int l = e / 3, cc = e % 3;
-        double x = xl[e];
-        double cnd = c.lm_var[l] ? x + (-yl[(int64_t)cc * L + l] * sl[(int64_t)cc * L + l]) : x;
-        cl[e] = cnd;
-        if (c.lm_var[l]) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
+        if (pfk >= 0) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
     }
     if (w.is_vi) {
         for (int e = threadIdx.x; e < 3 * K; e += BA_THREADS) {
@@ -1027,17 +1322,19 @@ __device__ void make_candidate(BaShared& sh, const WinCtx& c) {
         }
         for (int e = threadIdx.x; e < 6; e += BA_THREADS) {
             int f = e < 3 ? w.bg_f + e : w.ba_f + e - 3;
-            bool act = e < 3 ? w.bg_f >= 0 : w.ba_f >= 0;
+            bool a = e < 3 ? w.bg_f >= 0 : w.ba_f >= 0;
             double x = xb[e];
-            double cnd = act ? x + sh.D_f[f] : x;
+            double cnd = a ? x + sh.D_f[f] : x;
             cb[e] = cnd;
-            if (act) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
+            if (a) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
         }
     }
-    double mct = block_sum(mc, sh.red);
-    double snt = block_sum(sn, sh.red);
-    double xnt = block_sum(xn, sh.red);
+    const double nonfinite = block_max(fin, sh.redm);
+    const double mct = block_sum(mc, sh.red);
+    const double snt = block_sum(sn, sh.red);
+    const double xnt = block_sum(xn, sh.red);
     if (threadIdx.x == 0) {
+        sh.st.valid = nonfinite > 0.0 ? 0 : 1;
         sh.st.model_change = mct;
         sh.st.step_norm = sqrt(snt);
         sh.st.cand_x_norm2 = xnt;
@@ -1046,7 +1343,7 @@ __device__ void make_candidate(BaShared& sh, const WinCtx& c) {
     prof_mark(sh, PF_CAND);
 }
 
-__device__ void accept_candidate(BaShared& sh, const WinCtx& c) {
+__device__ __forceinline__ void accept_candidate(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
     double* ws = c.ws;
     const int K = w.K, L = w.L;
@@ -1059,7 +1356,7 @@ __device__ void accept_candidate(BaShared& sh, const WinCtx& c) {
 
 // ------------------------------------------------------------------------------------------
 // One ceres::Solve from the current workspace point.  Ceres semantics: see trust_region_minimizer.cc.
-__device__ void lm_solve(BaShared& sh, const WinCtx& c) {
+__device__ __forceinline__ void lm_solve(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
     double* ws = c.ws;
     double* xp = ws + c.L.x_pose;
@@ -1083,8 +1380,8 @@ __device__ void lm_solve(BaShared& sh, const WinCtx& c) {
     __syncthreads();
     // IterationZero
     prof_mark(sh, PF_CTRL);
-    double cost = evaluate(sh, c, xp, xl, xv, xb, true);
-    prof_mark(sh, PF_EVAL_J);
+    double cost = eval_lin(sh, c, xp, xl, xv, xb, true);
+    prof_mark(sh, PF_LIN);
     if (sh.st.fail) {
         if (threadIdx.x == 0) {
             sh.st.termination = VIO_TERM_FAILURE;
@@ -1095,8 +1392,6 @@ __device__ void lm_solve(BaShared& sh, const WinCtx& c) {
         __syncthreads();
         return;
     }
-    linearise(sh, c, true);
-    prof_mark(sh, PF_LIN);
     if (threadIdx.x == 0) {
         LmState& s = sh.st;
         s.x_cost = cost;
@@ -1129,7 +1424,6 @@ __device__ void lm_solve(BaShared& sh, const WinCtx& c) {
         compute_step(sh, c);
         bool valid = sh.st.valid;
         if (valid) {
-            make_candidate(sh, c);
             if (threadIdx.x == 0) sh.st.valid = sh.st.model_change > 0.0;
             __syncthreads();
             valid = sh.st.valid;
@@ -1154,7 +1448,7 @@ __device__ void lm_solve(BaShared& sh, const WinCtx& c) {
         if (threadIdx.x == 0) { sh.st.consecutive_invalid = 0; sh.st.fail = 0; }
         __syncthreads();
         prof_mark(sh, PF_CTRL);
-        double cc = evaluate(sh, c, ws + c.L.c_pose, ws + c.L.c_lm, ws + c.L.c_vel, ws + c.L.c_bias, false);
+        double cc = eval_cost(sh, c, ws + c.L.c_pose, ws + c.L.c_lm, ws + c.L.c_vel, ws + c.L.c_bias);
         prof_mark(sh, PF_EVAL_C);
         if (threadIdx.x == 0) {
             LmState& s = sh.st;
@@ -1178,15 +1472,13 @@ __device__ void lm_solve(BaShared& sh, const WinCtx& c) {
         if (sh.st.step_ok) {
             accept_candidate(sh, c);
             prof_mark(sh, PF_CTRL);
-            double nc = evaluate(sh, c, xp, xl, xv, xb, true);
-            prof_mark(sh, PF_EVAL_J);
+            double nc = eval_lin(sh, c, xp, xl, xv, xb, false);
+            prof_mark(sh, PF_LIN);
             if (sh.st.fail) {
                 if (threadIdx.x == 0) { sh.st.termination = VIO_TERM_FAILURE; sh.st.done = 1; }
                 __syncthreads();
                 break;
             }
-            linearise(sh, c, false);
-            prof_mark(sh, PF_LIN);
             if (threadIdx.x == 0) {
                 LmState& s = sh.st;
                 s.x_norm = sqrt(s.cand_x_norm2);
@@ -1204,7 +1496,7 @@ __device__ void lm_solve(BaShared& sh, const WinCtx& c) {
 }
 
 // reset the free parameters of the window to their initial values
-__device__ void init_params(BaShared& sh, const WinCtx& c, bool poses_only) {
+__device__ __forceinline__ void init_params(BaShared& sh, const WinCtx& c, bool poses_only) {
     const BaWin& w = *c.w;
     double* ws = c.ws;
     for (int e = threadIdx.x; e < 6 * w.K; e += BA_THREADS) ws[c.L.x_pose + e] = 0.0;
@@ -1261,13 +1553,16 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
         if (w.is_vi && k >= 1 && c.preint_valid[k]) imu_sqrt_info(c.preint[k], c.sqi + 81 * k);
     }
     for (int o = threadIdx.x; o < N; o += BA_THREADS) c.outlier[o] = 0;
-    for (int k = threadIdx.x; k < BA_KMAX; k += BA_THREADS) sh.posef[k] = k < K ? w.pose_f[k] : -1;
+    for (int k = threadIdx.x; k < BA_KMAX; k += BA_THREADS) {
+        sh.posef[k] = k < K ? w.pose_f[k] : -1;
+        sh.pvalid[k] = k < K ? c.preint_valid[k] : 0;
+    }
     {   // (landmark, keyframe) -> observation table for the Schur fill (pairs are unique: host-checked)
         int* lk = reinterpret_cast<int*>(c.ws + c.L.lk);
         for (int e = threadIdx.x; e < 16 * L; e += BA_THREADS) lk[e] = -1;
         __syncthreads();
         for (int o = threadIdx.x; o < N; o += BA_THREADS)
-            if (c.lm_var[c.obs_lm[o]]) lk[16 * c.obs_lm[o] + c.obs_kf[o]] = o;
+            lk[16 * c.obs_lm[o] + c.obs_kf[o]] = o;
     }
     init_params(sh, c, false);
 
