@@ -364,11 +364,18 @@ __device__ uint32_t uniform_below(Mt19937& g, uint32_t range) {  // uniform in [
     return (uint32_t)(prod >> 32);
 }
 
-__global__ void __launch_bounds__(64) ransac_sample_kernel(RansacArgs R) {
-    __shared__ Mt19937 g;
-    if (threadIdx.x != 0) return;
-    const int n = *R.n_good;
-    if (n < 3) return;
+// Parallel form of the same stream (one workgroup): the raw mt19937 words of RS_BLOCKS state
+// blocks are generated by a three-phase parallel twist (i in [0,227) reads only old words;
+// [227,454) and [454,624) read words that the previous phase produced) and tempered in parallel;
+// uniform_int_distribution's rejection test depends on a word alone, so accepted draws are a
+// prefix-scan compaction; a hypothesis consumes draws until it holds 3 distinct indices, and the
+// hypothesis chain is followed one wave at a time, 64 hypotheses per step while each consumes
+// exactly 3 draws (the common case).  Bitwise the sequential sampler; if the generated stream runs
+// out (tiny n: many duplicate redraws) the sequential sampler runs instead.
+constexpr int RS_THREADS = 1024;
+constexpr int RS_BLOCKS = 8;
+constexpr int RS_RAW = 624 * RS_BLOCKS;
+__device__ void ransac_sample_seq(const RansacArgs& R, Mt19937& g, int n) {
     g.seed(R.seed);
     for (int it = 0; it < R.iters; ++it) {
         int got[3];
@@ -382,6 +389,116 @@ __global__ void __launch_bounds__(64) ransac_sample_kernel(RansacArgs R) {
         R.samples[3 * it] = got[0];
         R.samples[3 * it + 1] = got[1];
         R.samples[3 * it + 2] = got[2];
+    }
+}
+__global__ void __launch_bounds__(RS_THREADS) ransac_sample_kernel(RansacArgs R) {
+    __shared__ uint32_t mt[624];
+    __shared__ uint32_t acc[RS_RAW];    // accepted draws (compacted), in stream order
+    __shared__ uint8_t len3[RS_RAW];    // 1: a hypothesis starting at draw p consumes exactly 3 draws
+    __shared__ int wsum[RS_THREADS / 64];
+    __shared__ int s_m, s_fallback;
+    const int n = *R.n_good;
+    if (n < 3 || R.iters <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) {  // seeding recurrence (sequential, 623 steps)
+        uint32_t v = R.seed;
+        mt[0] = v;
+        for (int i = 1; i < 624; ++i) {
+            v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
+            mt[i] = v;
+        }
+        s_m = 0;
+        s_fallback = 0;
+    }
+    __syncthreads();
+    const uint32_t range = (uint32_t)n;
+    const uint32_t thr = (uint32_t)(-range) % range;
+    for (int blk = 0; blk < RS_BLOCKS; ++blk) {
+        // twist: phases [0,227) [227,454) [454,624)
+        const int lo[3] = {0, 227, 454}, hi[3] = {227, 454, 624};
+        for (int ph = 0; ph < 3; ++ph) {
+            const int i = lo[ph] + tid;
+            uint32_t nv = 0;
+            if (i < hi[ph]) {
+                const uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
+                nv = mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            }
+            __syncthreads();
+            if (i < hi[ph]) mt[i] = nv;
+            __syncthreads();
+        }
+        // temper + accept test + compaction (stream order)
+        int accepted = 0;
+        uint32_t val = 0;
+        if (tid < 624) {
+            uint32_t y = mt[tid];
+            y ^= y >> 11;
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= y >> 18;
+            const uint64_t prod = (uint64_t)y * range;
+            const uint32_t low = (uint32_t)prod;
+            accepted = !(low < range && low < thr);
+            val = (uint32_t)(prod >> 32);
+        }
+        const unsigned long long bal = __ballot(accepted);
+        if (lane == 0) wsum[wid] = __popcll(bal);
+        __syncthreads();
+        int off = s_m;
+        for (int q = 0; q < wid; ++q) off += wsum[q];
+        if (accepted) acc[off + __popcll(bal & ((1ull << lane) - 1ull))] = val;
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+            for (int q = 0; q < RS_THREADS / 64; ++q) t += wsum[q];
+            s_m += t;
+        }
+        __syncthreads();
+    }
+    const int M = s_m;
+    for (int p = tid; p < M; p += RS_THREADS)
+        len3[p] = (p + 2 < M && acc[p] != acc[p + 1] && acc[p] != acc[p + 2] && acc[p + 1] != acc[p + 2]) ? 1 : 0;
+    __syncthreads();
+    if (wid == 0) {
+        int s = 0, h = 0;
+        bool fb = false;
+        while (h < R.iters && !fb) {
+            const int p = s + 3 * lane;
+            const bool ok = h + lane < R.iters && p + 2 < M && len3[p];
+            const unsigned long long bad = __ballot(!ok);
+            const int f = bad ? __ffsll((long long)bad) - 1 : 64;
+            if (lane < f) {
+                R.samples[3 * (h + lane)] = (int)acc[p];
+                R.samples[3 * (h + lane) + 1] = (int)acc[p + 1];
+                R.samples[3 * (h + lane) + 2] = (int)acc[p + 2];
+            }
+            s += 3 * f;
+            h += f;
+            if (h >= R.iters) break;
+            if (f < 64) {  // hypothesis h consumes more than 3 draws (a duplicate) or the stream ends
+                int got[3], k = 0, q = s;
+                while (k < 3 && q < M) {
+                    const int idx = (int)acc[q++];
+                    bool dup = false;
+                    for (int u = 0; u < k; ++u) dup |= got[u] == idx;
+                    if (!dup) got[k++] = idx;
+                }
+                if (k < 3) { fb = true; break; }
+                if (lane == 0) {
+                    R.samples[3 * h] = got[0];
+                    R.samples[3 * h + 1] = got[1];
+                    R.samples[3 * h + 2] = got[2];
+                }
+                s = q;
+                ++h;
+            }
+        }
+        if (lane == 0) s_fallback = fb ? 1 : 0;
+    }
+    __syncthreads();
+    if (s_fallback && tid == 0) {
+        __shared__ Mt19937 g;  // stream exhausted: the sequential sampler from the seed
+        ransac_sample_seq(R, g, n);
     }
 }
 
@@ -641,19 +758,26 @@ __device__ void gf_eig_tile(const GfArgs& G, int ex0, int ey0, uint8_t (*src)[Gf
     __syncthreads();
 }
 
+// Each workgroup walks GF_SUB tiles down the image (fewer, longer-lived workgroups; one global
+// atomic per workgroup instead of one per tile / wave).
+constexpr int GF_SUB = 4;
 __global__ void __launch_bounds__(256) gftt_max_kernel(GfArgs G) {
     using T = GfTile<2>;
     __shared__ uint8_t src[T::SH][T::SW + 4];
     __shared__ float cov[T::CH][T::CW][3];
     __shared__ float eig[T::EH][T::EW];
     __shared__ uint32_t red[4];
-    const int ex0 = blockIdx.x * GF_BX, ey0 = blockIdx.y * GF_BY;
-    gf_eig_tile<2>(G, ex0, ey0, src, cov, eig);
     uint32_t m = 0;  // ord(-inf-ish): any value beats 0
-    for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
-        int ey = e / T::EW, ex = e % T::EW;
-        int X = ex0 + ex, Y = ey0 + ey;
-        if (X < G.W && Y < G.H && gf_masked_in(G, X, Y)) m = max(m, ord_f32(eig[ey][ex]));
+    for (int sub = 0; sub < GF_SUB; ++sub) {
+        const int ex0 = blockIdx.x * GF_BX, ey0 = (blockIdx.y * GF_SUB + sub) * GF_BY;
+        if (ey0 >= G.H) break;
+        gf_eig_tile<2>(G, ex0, ey0, src, cov, eig);
+        for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
+            int ey = e / T::EW, ex = e % T::EW;
+            int X = ex0 + ex, Y = ey0 + ey;
+            if (X < G.W && Y < G.H && gf_masked_in(G, X, Y)) m = max(m, ord_f32(eig[ey][ex]));
+        }
+        __syncthreads();  // eig / src are rewritten by the next tile
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
@@ -670,60 +794,81 @@ __global__ void __launch_bounds__(256) gftt_cand_kernel(GfArgs G) {
     __shared__ uint8_t src[T::SH][T::SW + 4];
     __shared__ float cov[T::CH][T::CW][3];
     __shared__ float eig[T::EH][T::EW];
-    const int ox = blockIdx.x * GF_BX, oy = blockIdx.y * GF_BY;
-    gf_eig_tile<3>(G, ox - 1, oy - 1, src, cov, eig);
-    // threshold (THRESH_TOZERO with the float threshold) in place
+    __shared__ unsigned long long keys[GF_SUB * GF_BX * GF_BY];
+    __shared__ unsigned int s_cnt, s_base;
+    if (threadIdx.x == 0) s_cnt = 0;
+    // threshold (THRESH_TOZERO with the float threshold)
     const uint32_t mo = *G.max_ord;
     double maxv = mo ? (double)unord_f32(mo) : 0.0;  // minMaxLoc over the mask, 0 when empty
     if (maxv < 0.0) maxv = 0.0;
     const float thr = (float)(maxv * G.quality);
-    for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
-        int ey = e / T::EW, ex = e % T::EW;
-        if (!(eig[ey][ex] > thr)) eig[ey][ex] = 0.f;
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < GF_BX * GF_BY; e += 256) {
-        int ty = e / GF_BX, tx = e % GF_BX;
-        int X = ox + tx, Y = oy + ty;
-        bool c = false;
-        float v = 0.f;
-        if (X >= 1 && X < G.W - 1 && Y >= 1 && Y < G.H - 1) {
-            v = eig[ty + 1][tx + 1];
-            if (v != 0.f && gf_masked_in(G, X, Y)) {
-                float m = v;
-                for (int ky = 0; ky < 3; ++ky)
-                    for (int kx = 0; kx < 3; ++kx) m = fmaxf(m, eig[ty + ky][tx + kx]);
-                c = (v == m);
+    for (int sub = 0; sub < GF_SUB; ++sub) {
+        const int ox = blockIdx.x * GF_BX, oy = (blockIdx.y * GF_SUB + sub) * GF_BY;
+        if (oy >= G.H) break;
+        gf_eig_tile<3>(G, ox - 1, oy - 1, src, cov, eig);
+        for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
+            int ey = e / T::EW, ex = e % T::EW;
+            if (!(eig[ey][ex] > thr)) eig[ey][ex] = 0.f;
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < GF_BX * GF_BY; e += 256) {
+            int ty = e / GF_BX, tx = e % GF_BX;
+            int X = ox + tx, Y = oy + ty;
+            bool c = false;
+            float v = 0.f;
+            if (X >= 1 && X < G.W - 1 && Y >= 1 && Y < G.H - 1) {
+                v = eig[ty + 1][tx + 1];
+                if (v != 0.f && gf_masked_in(G, X, Y)) {
+                    float m = v;
+                    for (int ky = 0; ky < 3; ++ky)
+                        for (int kx = 0; kx < 3; ++kx) m = fmaxf(m, eig[ty + ky][tx + kx]);
+                    c = (v == m);
+                }
             }
+            unsigned long long bal = __ballot(c);
+            int lane = threadIdx.x & 63;
+            int cnt = __popcll(bal);
+            unsigned int base = 0;
+            if (cnt) {
+                if (lane == __ffsll((long long)bal) - 1) base = atomicAdd(&s_cnt, (unsigned int)cnt);  // LDS
+                base = __shfl(base, __ffsll((long long)bal) - 1, 64);
+            }
+            if (c)
+                keys[base + __popcll(bal & ((1ull << lane) - 1ull))] =
+                    ((unsigned long long)__float_as_uint(v) << 32) | (unsigned int)(Y * G.W + X);
         }
-        unsigned long long bal = __ballot(c);
-        int lane = threadIdx.x & 63;
-        int cnt = __popcll(bal);
-        unsigned int base = 0;
-        if (cnt) {
-            if (lane == __ffsll((long long)bal) - 1) base = atomicAdd(G.n_cand, (unsigned int)cnt);
-            base = __shfl(base, __ffsll((long long)bal) - 1, 64);
-        }
-        if (c) {
-            unsigned int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-            if (pos < G.cand_cap)
-                G.cand[pos] = ((unsigned long long)__float_as_uint(v) << 32) | (unsigned int)(Y * G.W + X);
-        }
+        __syncthreads();  // eig / src are rewritten by the next tile
     }
+    const unsigned int n = s_cnt;
+    if (n == 0) return;
+    if (threadIdx.x == 0) s_base = atomicAdd(G.n_cand, n);
+    __syncthreads();
+    const unsigned int base = s_base;
+    for (unsigned int i = threadIdx.x; i < n; i += 256)
+        if (base + i < G.cand_cap) G.cand[base + i] = keys[i];
 }
 
 // greedy min-distance selection over the sorted candidates (goodFeaturesToTrack tail).
 // One workgroup.  Accepted corners live in a grid of cell = round(min_dist) with <= 3 per cell.
 constexpr int GS_THREADS = 256;
 constexpr int GS_SLOTS = 3;
+template <bool GLOBAL_GRID>
 __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const unsigned long long* keys,
                                                                   const unsigned int* n_keys, unsigned int cap,
                                                                   int fast) {
     extern __shared__ uint32_t grid_lds[];
     __shared__ int s_good[GS_THREADS];
+    __shared__ unsigned int s_idx[GS_THREADS];  // the batch's candidate addresses
+    __shared__ unsigned int s_sv[GS_THREADS];   // survivors of the pre-filter, batch order: y << 16 | x
+    __shared__ unsigned long long s_conf[GS_THREADS][GS_THREADS / 64];
+    __shared__ int s_wcnt[GS_THREADS / 64];
+    __shared__ unsigned long long s_am[GS_THREADS / 64];  // accepted survivors of the batch
+    __shared__ unsigned long long s_dm[GS_THREADS / 64];  // decided survivors
+    __shared__ uint32_t s_slot_val[GS_THREADS];
+    __shared__ int s_slot_idx[GS_THREADS];
     __shared__ int s_acc;
     __shared__ int s_stop;
-    uint32_t* grid = G.grid_global ? G.grid_global : grid_lds;
+    uint32_t* grid = GLOBAL_GRID ? G.grid_global : grid_lds;  // static address space (no flat access)
     const int ncell = G.gw * G.gh;
     for (int e = threadIdx.x; e < ncell * GS_SLOTS; e += GS_THREADS) grid[e] = 0xffffffffu;
     if (threadIdx.x == 0) { s_acc = 0; s_stop = 0; }
@@ -732,18 +877,27 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
     const int cell = G.cell;
     const double md2 = G.min_dist * G.min_dist;
     auto conflicts = [&](int x, int y, int slot_lane_only) -> bool {
-        int xc = x / cell, yc = y / cell;
-        int x1 = max(xc - 1, 0), y1 = max(yc - 1, 0), x2 = min(xc + 1, G.gw - 1), y2 = min(yc + 1, G.gh - 1);
-        for (int yy = y1; yy <= y2; ++yy)
-            for (int xx = x1; xx <= x2; ++xx)
-                for (int s = 0; s < GS_SLOTS; ++s) {
-                    uint32_t p = grid[(yy * G.gw + xx) * GS_SLOTS + s];
-                    if (p == 0xffffffffu) break;
-                    float ddx = (float)x - (float)(p & 0xffffu), ddy = (float)y - (float)(p >> 16);
-                    if ((double)(ddx * ddx + ddy * ddy) < md2) return true;
+        const int xc = x / cell, yc = y / cell;
+        bool hit = false;
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int xx = xc + dx, yy = yc + dy;
+                if (xx < 0 || yy < 0 || xx >= G.gw || yy >= G.gh) continue;
+#pragma unroll
+                for (int s = 0; s < GS_SLOTS; ++s) {  // every slot read (independent loads), empty = 0xffffffff
+                    const uint32_t p = grid[(yy * G.gw + xx) * GS_SLOTS + s];
+                    const float ddx = (float)x - (float)(p & 0xffffu), ddy = (float)y - (float)(p >> 16);
+                    hit |= p != 0xffffffffu && (double)(ddx * ddx + ddy * ddy) < md2;
                 }
-        return false;
+            }
+        return hit;
     };
+#ifdef GFTT_DEBUG
+    unsigned long long t_start = __builtin_amdgcn_s_memtime(), t_pre = 0, t_mask = 0, t_greedy = 0, tq;
+    int nb_dbg = 0, nsv_dbg = 0;
+#endif
     for (unsigned int c0 = 0; c0 < total; c0 += GS_THREADS) {
         // (1) parallel pre-filter against the corners accepted in earlier batches
         unsigned int ci = c0 + threadIdx.x;
@@ -751,51 +905,146 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
         if (ci < total) {
             unsigned int idx = (unsigned int)(keys[ci] & 0xffffffffu);
             good = !conflicts((int)(idx % G.W), (int)(idx / G.W), 0);
+            s_idx[threadIdx.x] = idx;
         }
         s_good[threadIdx.x] = good;
         __syncthreads();
-        // (2) in-order resolution inside the batch by wave 0 (lane k checks grid slot k)
-        if (threadIdx.x < 64) {
-            const int lane = threadIdx.x;
-            const int nb = min((unsigned int)GS_THREADS, total - c0);
-            for (int j = 0; j < nb; ++j) {
-                if (!s_good[j]) continue;
-                unsigned int idx = (unsigned int)(keys[c0 + j] & 0xffffffffu);
-                int x = (int)(idx % G.W), y = (int)(idx / G.W);
-                int xc = x / cell, yc = y / cell;
-                // 9 cells x 3 slots = 27 lanes
-                bool conf = false;
-                if (lane < 27) {
-                    int cc = lane / GS_SLOTS, s = lane % GS_SLOTS;
-                    int xx = xc - 1 + cc % 3, yy = yc - 1 + cc / 3;
-                    if (xx >= 0 && yy >= 0 && xx < G.gw && yy < G.gh) {
-                        uint32_t p = grid[(yy * G.gw + xx) * GS_SLOTS + s];
-                        if (p != 0xffffffffu) {
-                            float ddx = (float)x - (float)(p & 0xffffu), ddy = (float)y - (float)(p >> 16);
-                            conf = (double)(ddx * ddx + ddy * ddy) < md2;
-                        }
+#ifdef GFTT_DEBUG
+        tq = __builtin_amdgcn_s_memtime(); t_pre += tq - t_start; t_start = tq;
+#endif
+        // (2) in-order resolution inside the batch.  Survivors of (1) are compacted (batch order);
+        // survivor r gets a bitmask of the earlier survivors within min_dist of it; thread 0 walks
+        // the masks in order (accept r iff none of its conflicts was accepted) and inserts the
+        // accepted corners into the grid in acceptance order.
+        {
+            const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+            const unsigned long long bal = __ballot(good);
+            if (lane == 0) s_wcnt[wid] = __popcll(bal);
+            __syncthreads();
+            int rank = __popcll(bal & ((1ull << lane) - 1ull));
+            for (int q = 0; q < wid; ++q) rank += s_wcnt[q];
+            int nsv = 0;
+            for (int q = 0; q < GS_THREADS / 64; ++q) nsv += s_wcnt[q];
+#ifdef GFTT_DEBUG
+            nb_dbg++; nsv_dbg += nsv;
+#endif
+            int x = 0, y = 0;
+            if (good) {
+                const unsigned int idx = s_idx[threadIdx.x];
+                x = (int)(idx % G.W);
+                y = (int)(idx / G.W);
+                s_sv[rank] = ((unsigned int)y << 16) | (unsigned int)x;
+            }
+            __syncthreads();
+            if (good) {
+#pragma unroll
+                for (int q = 0; q < GS_THREADS / 64; ++q) {  // word q of the mask stays in a register
+                    unsigned long long m = 0ull;
+                    const int jend = min(rank - 64 * q, 64);
+#pragma unroll 8
+                    for (int b = 0; b < jend; ++b) {
+                        const unsigned int pj = s_sv[64 * q + b];
+                        const float ddx = (float)x - (float)(pj & 0xffff), ddy = (float)y - (float)(pj >> 16);
+                        if ((double)(ddx * ddx + ddy * ddy) < md2) m |= 1ull << b;
+                    }
+                    s_conf[rank][q] = m;
+                }
+            }
+            __syncthreads();
+#ifdef GFTT_DEBUG
+            tq = __builtin_amdgcn_s_memtime(); t_mask += tq - t_start; t_start = tq;
+#endif
+            // greedy in batch order, resolved in rounds: a survivor is accepted once none of its earlier
+            // conflicting survivors can still be accepted (all decided rejected), rejected once one of
+            // them is accepted.  Identical to the sequential walk; rounds = longest conflict chain.
+            if (threadIdx.x < GS_THREADS / 64) { s_am[threadIdx.x] = 0ull; s_dm[threadIdx.x] = 0ull; }
+            __syncthreads();
+            bool decided = !good;
+            unsigned long long cf[GS_THREADS / 64];
+#pragma unroll
+            for (int q = 0; q < GS_THREADS / 64; ++q) cf[q] = good ? s_conf[rank][q] : 0ull;
+            for (;;) {
+                bool acc_now = false, dec_now = false;
+                if (!decided) {
+                    unsigned long long hit = 0ull, open = 0ull;
+#pragma unroll
+                    for (int q = 0; q < GS_THREADS / 64; ++q) {
+                        hit |= cf[q] & s_am[q];
+                        open |= cf[q] & ~s_dm[q];
+                    }
+                    if (hit) dec_now = true;
+                    else if (!open) { dec_now = true; acc_now = true; }
+                }
+                const int any = __syncthreads_or(dec_now ? 1 : 0);
+                if (!any) break;
+                if (dec_now) {
+                    decided = true;
+                    atomicOr(&s_dm[rank >> 6], 1ull << (rank & 63));
+                    if (acc_now) atomicOr(&s_am[rank >> 6], 1ull << (rank & 63));
+                }
+                __syncthreads();
+            }
+            // max_corners: keep the first (max_corners - s_acc) accepted in order
+            if (threadIdx.x == 0 && G.max_corners > 0) {
+                int room = G.max_corners - s_acc;
+                for (int q = 0; q < GS_THREADS / 64; ++q) {
+                    unsigned long long m = s_am[q];
+                    const int c = __popcll(m);
+                    if (c >= room) {
+                        while (__popcll(m) > room) m &= ~(1ull << (63 - __clzll(m)));  // drop the highest bits
+                        s_am[q] = m;
+                        for (int q2 = q + 1; q2 < GS_THREADS / 64; ++q2) s_am[q2] = 0ull;
+                        if (__popcll(m) == room) s_stop = 1;
+                        break;
+                    }
+                    room -= c;
+                }
+            }
+            __syncthreads();
+            // accepted survivors in acceptance (= batch) order: corners[s_acc + rank]; grid slots as the
+            // sequential insertion would leave them (the i-th insertion into a cell holding e0 entries
+            // goes to slot min(e0 + i, GS_SLOTS - 1); an overflowing slot keeps the last one)
+            const int nacc_before = s_acc;
+            int nacc = 0;
+#pragma unroll
+            for (int q = 0; q < GS_THREADS / 64; ++q) nacc += __popcll(s_am[q]);
+            if (good && ((s_am[rank >> 6] >> (rank & 63)) & 1ull)) {
+                int before = 0;
+                for (int q = 0; q < (rank >> 6); ++q) before += __popcll(s_am[q]);
+                before += __popcll(s_am[rank >> 6] & ((1ull << (rank & 63)) - 1ull));
+                const int kk = nacc_before + before;
+                G.corners[2 * kk] = (float)x;
+                G.corners[2 * kk + 1] = (float)y;
+                const int xc = x / cell, yc = y / cell;
+                int i_cell = 0, m_cell = 0;
+                for (int r = 0; r < nsv; ++r) {
+                    if (!((s_am[r >> 6] >> (r & 63)) & 1ull)) continue;
+                    const int xr = (int)(s_sv[r] & 0xffffu), yr = (int)(s_sv[r] >> 16);
+                    if (xr / cell == xc && yr / cell == yc) {
+                        if (r < rank) ++i_cell;
+                        ++m_cell;
                     }
                 }
-                if (__ballot(conf) != 0ull) continue;
-                if (lane == 0) {
-                    int k = s_acc;
-                    uint32_t* cellp = &grid[(yc * G.gw + xc) * GS_SLOTS];
-                    int s = 0;
-                    while (s < GS_SLOTS - 1 && cellp[s] != 0xffffffffu) ++s;
-                    cellp[s] = ((uint32_t)y << 16) | (uint32_t)x;
-                    G.corners[2 * k] = (float)x;
-                    G.corners[2 * k + 1] = (float)y;
-                    s_acc = k + 1;
-                    if (G.max_corners > 0 && k + 1 == G.max_corners) s_stop = 1;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-                if (s_stop) break;
+                uint32_t* cellp = &grid[(yc * G.gw + xc) * GS_SLOTS];
+                int e0 = 0;
+                while (e0 < GS_SLOTS && cellp[e0] != 0xffffffffu) ++e0;  // entries from earlier batches
+                const int slot = min(e0 + i_cell, GS_SLOTS - 1);
+                if (e0 + i_cell < GS_SLOTS - 1 || i_cell == m_cell - 1) s_slot_val[rank] = ((uint32_t)y << 16) | (uint32_t)x, s_slot_idx[rank] = (yc * G.gw + xc) * GS_SLOTS + slot;
+                else s_slot_idx[rank] = -1;
             }
+            __syncthreads();
+            if (good && ((s_am[rank >> 6] >> (rank & 63)) & 1ull) && s_slot_idx[rank] >= 0)
+                grid[s_slot_idx[rank]] = s_slot_val[rank];
+            if (threadIdx.x == 0) s_acc = nacc_before + nacc;
         }
         __syncthreads();
         if (s_stop) break;
     }
+#ifdef GFTT_DEBUG
+    if (threadIdx.x == 0)
+        printf("gftt_select: total %u batches %d survivors %d pre %llu mask %llu greedy %llu rest %llu\n", total, nb_dbg, nsv_dbg,
+               t_pre, t_mask, t_greedy, __builtin_amdgcn_s_memtime() - t_start);
+#endif
     if (threadIdx.x == 0) {
         *G.n_out = s_acc;
         // the top-K subset ran dry before max_corners: the exact pass over every candidate must decide
@@ -816,23 +1065,74 @@ __global__ void __launch_bounds__(256) gftt_hist_kernel(GfArgs G) {
         if (h[b]) atomicAdd(&G.hist[b], h[b]);
 }
 
-// cut bucket: the highest buckets holding >= topk_target candidates (never more than topk_cap)
-__global__ void __launch_bounds__(64) gftt_cut_kernel(GfArgs G) {
-    if (threadIdx.x != 0) return;
-    unsigned int cum = 0;
-    int cut = GF_BUCKETS;  // buckets >= cut form the top set (GF_BUCKETS: empty set)
-    for (int b = GF_BUCKETS - 1; b >= 0; --b) {
-        unsigned int c = G.hist[b];
-        if (c == 0) { cut = b; continue; }
-        if (cum + c > G.topk_cap) break;  // this bucket would overflow the top-K buffer
-        cum += c;
-        cut = b;
-        if (cum >= G.topk_target) break;
+// cut bucket: the highest buckets holding >= topk_target candidates (never more than topk_cap).
+// One workgroup: the histogram goes to LDS, suffix sums by a block scan, then the same top-down
+// walk as a sequential loop would make (first bucket from the top where the running count reaches
+// the target, or where the next nonempty bucket would overflow the buffer).
+constexpr int GC_THREADS = 1024;
+__global__ void __launch_bounds__(GC_THREADS) gftt_cut_kernel(GfArgs G) {
+    constexpr int PER = GF_BUCKETS / GC_THREADS;
+    __shared__ unsigned int suf[GF_BUCKETS + 1];  // suf[b] = sum of hist[b..]
+    __shared__ unsigned int part[GC_THREADS];
+    __shared__ int s_cut;
+    const int t = threadIdx.x;
+    // thread t owns buckets [t*PER, t*PER+PER): local suffix sums, then a scan over threads (top-down)
+    unsigned int h[PER];
+    unsigned int loc = 0;
+#pragma unroll
+    for (int i = PER - 1; i >= 0; --i) { h[i] = G.hist[t * PER + i]; loc += h[i]; }
+    part[t] = loc;
+    __syncthreads();
+    for (int off = 1; off < GC_THREADS; off <<= 1) {  // inclusive suffix scan over threads
+        unsigned int v = t + off < GC_THREADS ? part[t + off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
     }
-    unsigned int below = 0;
-    for (int q = 0; q < cut && q < GF_BUCKETS; ++q) below += G.hist[q];
-    G.cut[0] = cut;
-    G.cut[1] = below == 0 ? 1 : 0;  // every candidate is in the top set
+    unsigned int run = t + 1 < GC_THREADS ? part[t + 1] : 0u;
+#pragma unroll
+    for (int i = PER - 1; i >= 0; --i) { run += h[i]; suf[t * PER + i] = run; }
+    if (t == 0) { suf[GF_BUCKETS] = 0; s_cut = GF_BUCKETS; }
+    __syncthreads();
+    // sequential semantics: walking b down from the top, cum = suf[b+1] before bucket b;
+    // stop (cut = b+1 ... ) at the first nonempty b with cum + c > cap (cut stays above b), or
+    // after taking b when cum + c >= target (cut = b); empty buckets extend the cut downward.
+    // The walk ends at the largest b satisfying either condition; cut = b (take) or the lowest
+    // bucket above b that was reached, which is b + 1 after empty buckets are skipped upward.
+    int cand = -1;  // largest stopping bucket and its kind
+    for (int i = PER - 1; i >= 0; --i) {
+        const int b = t * PER + i;
+        const unsigned int c = h[i];
+        if (c == 0) continue;
+        const unsigned int cum = suf[b + 1];
+        if (cum + c > G.topk_cap || cum + c >= G.topk_target) { cand = b; break; }
+    }
+    // max over threads of the stopping bucket
+    part[t] = (unsigned int)(cand + 1);
+    __syncthreads();
+    for (int off = GC_THREADS / 2; off > 0; off >>= 1) {
+        if (t < off) part[t] = max(part[t], part[t + off]);
+        __syncthreads();
+    }
+    if (t == 0) {
+        const int bstop = (int)part[0] - 1;
+        int cut;
+        if (bstop < 0) {
+            cut = 0;  // never stopped: the walk reaches bucket 0 (every bucket taken or empty)
+        } else {
+            const unsigned int c = G.hist[bstop];
+            const unsigned int cum = suf[bstop + 1];
+            if (cum + c > G.topk_cap) {
+                // not taken: cut = the lowest bucket above bstop reached by the walk = bstop + 1
+                // (buckets bstop+1 .. were taken or empty)
+                cut = bstop + 1;
+            } else {
+                cut = bstop;  // taken and the target is reached
+            }
+        }
+        G.cut[0] = cut;
+        G.cut[1] = suf[0] - suf[cut < GF_BUCKETS ? cut : GF_BUCKETS] == 0 ? 1 : 0;  // nothing below the cut
+    }
 }
 
 __global__ void __launch_bounds__(256) gftt_topk_compact_kernel(GfArgs G) {
@@ -887,7 +1187,7 @@ hipError_t launch_lk(const LkArgs& a, hipStream_t st) {
 }
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st) {
     hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(1024), 0, st, r);
-    if (gen_samples) hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(64), 0, st, r);
+    if (gen_samples) hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(RS_THREADS), 0, st, r);
     if (r.iters > 0) hipLaunchKernelGGL(ransac_hyp_kernel, dim3((r.iters + 3) / 4), dim3(256), 0, st, r);
     hipLaunchKernelGGL(ransac_select_kernel, dim3(1), dim3(256), 0, st, r);
     return hipGetLastError();
@@ -898,7 +1198,7 @@ hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st) {
     return hipGetLastError();
 }
 static hipError_t gftt_candidates(const GfArgs& g, hipStream_t st) {
-    dim3 grd((g.W + GF_BX - 1) / GF_BX, (g.H + GF_BY - 1) / GF_BY);
+    dim3 grd((g.W + GF_BX - 1) / GF_BX, (g.H + GF_BY * GF_SUB - 1) / (GF_BY * GF_SUB));
     hipLaunchKernelGGL(gftt_max_kernel, grd, dim3(256), 0, st, g);
     hipLaunchKernelGGL(gftt_cand_kernel, grd, dim3(256), 0, st, g);
     return hipGetLastError();
@@ -911,13 +1211,17 @@ hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, h
     hipError_t e = gftt_candidates(g, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(gftt_hist_kernel, dim3(256), dim3(256), 0, st, g);
-    hipLaunchKernelGGL(gftt_cut_kernel, dim3(1), dim3(64), 0, st, g);
+    hipLaunchKernelGGL(gftt_cut_kernel, dim3(1), dim3(GC_THREADS), 0, st, g);
     hipLaunchKernelGGL(gftt_topk_compact_kernel, dim3(256), dim3(256), 0, st, g);
     size_t tb = sort_tmp_bytes;
     e = hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.topk, g.topk_sorted, (int)g.topk_cap, 0, 64, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(gftt_select_kernel, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
-                       (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
+    if (g.grid_global)
+        hipLaunchKernelGGL(gftt_select_kernel<true>, dim3(1), dim3(GS_THREADS), 0, st, g,
+                           (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
+    else
+        hipLaunchKernelGGL(gftt_select_kernel<false>, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
+                           (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
     return hipGetLastError();
 }
 // exact fallback: sort every candidate slot (unused slots hold 0 and sort to the end) and redo the
@@ -927,8 +1231,12 @@ hipError_t launch_gftt_full(const GfArgs& g, void* sort_tmp, size_t sort_tmp_byt
     hipError_t e = hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.cand, g.cand_sorted, (int)g.cand_cap,
                                                                0, 64, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(gftt_select_kernel, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
-                       (const unsigned long long*)g.cand_sorted, (const unsigned int*)g.n_cand, g.cand_cap, 0);
+    if (g.grid_global)
+        hipLaunchKernelGGL(gftt_select_kernel<true>, dim3(1), dim3(GS_THREADS), 0, st, g,
+                           (const unsigned long long*)g.cand_sorted, (const unsigned int*)g.n_cand, g.cand_cap, 0);
+    else
+        hipLaunchKernelGGL(gftt_select_kernel<false>, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
+                           (const unsigned long long*)g.cand_sorted, (const unsigned int*)g.n_cand, g.cand_cap, 0);
     return hipGetLastError();
 }
 size_t gftt_sort_tmp_bytes(unsigned int cap) {
@@ -938,7 +1246,7 @@ size_t gftt_sort_tmp_bytes(unsigned int cap) {
     return tb;
 }
 hipError_t gftt_select_set_lds(size_t bytes) {
-    return hipFuncSetAttribute((const void*)gftt_select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    return hipFuncSetAttribute((const void*)gftt_select_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 }  // namespace vio360
