@@ -70,12 +70,15 @@ constexpr int LK_WIN_MAX = 21;
 constexpr int LK_T = LK_WIN_MAX + 3;  // prev tile (patch + 1 bilinear + 1 Scharr each side)
 constexpr int LK_D = LK_WIN_MAX + 1;  // derivative / next tile
 
+constexpr int LK_MARGIN = 8;                 // staged next-frame region: the window +- 8 px
+constexpr int LK_R = LK_D + 2 * LK_MARGIN;
+
 struct LkShared {
+    uint8_t Jr[LK_R * LK_R];                 // next-frame region (reflect-101 values), origin (rx0, ry0)
     uint8_t It[LK_T * LK_T];
     int16_t dx[LK_D * LK_D], dy[LK_D * LK_D];
     int16_t Iw[LK_WIN_MAX * LK_WIN_MAX];
     int16_t dIx[LK_WIN_MAX * LK_WIN_MAX], dIy[LK_WIN_MAX * LK_WIN_MAX];
-    uint8_t Jt[LK_D * LK_D];
 };
 
 __device__ __forceinline__ long long wave_sum_i64(long long v) {
@@ -93,14 +96,22 @@ __device__ __forceinline__ void lk_weights(float a, float b, int& w00, int& w01,
     w11 = 16384 - w00 - w01 - w10;
 }
 
-// load the (win+1)x(win+1) next-frame tile at (ix, iy) with the REFLECT_101 pad semantics
-__device__ __forceinline__ void lk_load_J(uint8_t* Jt, const uint8_t* J, int w, int h, int pitch, int ix, int iy,
-                                          int win, int lane) {
-    const int n = (win + 1) * (win + 1);
-    for (int e = lane; e < n; e += 64) {
-        int ty = e / (win + 1), tx = e % (win + 1);
-        Jt[e] = J[(size_t)reflect101(iy + ty, h) * pitch + reflect101(ix + tx, w)];
+// make the staged region cover the (win+1)^2 window at (ix, iy); restage around it when it does
+// not (one global round trip per level instead of one per iteration).  Values are the
+// REFLECT_101-padded pixels, exactly what a per-window load would read.
+__device__ __forceinline__ void lk_region(uint8_t* Jr, int& rx0, int& ry0, const uint8_t* J, int w, int h, int pitch,
+                                          int ix, int iy, int win, int lane) {
+    const int D = win + 1;
+    if (ix >= rx0 && iy >= ry0 && ix + D <= rx0 + LK_R && iy + D <= ry0 + LK_R) return;
+    rx0 = ix - LK_MARGIN;
+    ry0 = iy - LK_MARGIN;
+    __builtin_amdgcn_wave_barrier();
+    for (int e = lane; e < LK_R * LK_R; e += 64) {
+        const int ty = e / LK_R, tx = e - ty * LK_R;
+        Jr[e] = J[(size_t)reflect101(ry0 + ty, h) * pitch + reflect101(rx0 + tx, w)];
     }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 }
 
 // Σ |diff| or the b-vector over the window for the current J tile
@@ -166,7 +177,7 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
         float a = px - ipx, b = py - ipy;
         int w00, w01, w10, w11;
         lk_weights(a, b, w00, w01, w10, w11);
-        long long sA11 = 0, sA12 = 0, sA22 = 0;
+        int sA11 = 0, sA12 = 0, sA22 = 0;  // per-lane partials fit int32 (<= 7 terms < 2^26 each)
         for (int e = lane; e < np; e += 64) {
             int y = e / win, x = e % win;
             const uint8_t* t = &S.It[(y + 1) * T + x + 1];
@@ -177,14 +188,12 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
             S.Iw[e] = (int16_t)ival;
             S.dIx[e] = (int16_t)ixv;
             S.dIy[e] = (int16_t)iyv;
-            sA11 += (long long)ixv * ixv;
-            sA12 += (long long)ixv * iyv;
-            sA22 += (long long)iyv * iyv;
+            sA11 += ixv * ixv;
+            sA12 += ixv * iyv;
+            sA22 += iyv * iyv;
         }
-        sA11 = wave_sum_i64(sA11);
-        sA12 = wave_sum_i64(sA12);
-        sA22 = wave_sum_i64(sA22);
-        const float A11 = (float)sA11 * FLT_SCALE, A12 = (float)sA12 * FLT_SCALE, A22 = (float)sA22 * FLT_SCALE;
+        const long long tA11 = wave_sum_i64(sA11), tA12 = wave_sum_i64(sA12), tA22 = wave_sum_i64(sA22);
+        const float A11 = (float)tA11 * FLT_SCALE, A12 = (float)tA12 * FLT_SCALE, A22 = (float)tA22 * FLT_SCALE;
         float Dt = A11 * A22 - A12 * A12;
         const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
         if (minEig < A.min_eig || Dt < FLT_EPSILON) {
@@ -194,6 +203,7 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
         Dt = 1.f / Dt;
         nx -= hw; ny -= hw;
         float pdx = 0.f, pdy = 0.f;
+        int rx0 = -(1 << 29), ry0 = -(1 << 29);  // no region staged for this level yet
         for (int j = 0; j < A.max_iters; ++j) {
             const int inx = (int)floorf(nx), iny = (int)floorf(ny);
             if (inx < -win || inx >= w || iny < -win || iny >= h) {
@@ -202,21 +212,17 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
             }
             a = nx - inx; b = ny - iny;
             lk_weights(a, b, w00, w01, w10, w11);
-            __builtin_amdgcn_wave_barrier();
-            lk_load_J(S.Jt, J, w, h, Lv.pitch, inx, iny, win, lane);
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            long long ib1 = 0, ib2 = 0;
+            lk_region(S.Jr, rx0, ry0, J, w, h, Lv.pitch, inx, iny, win, lane);
+            const uint8_t* Jw = S.Jr + (iny - ry0) * LK_R + (inx - rx0);
+            int ib1 = 0, ib2 = 0;  // per-lane partials fit int32 (<= 7 terms < 2^26 each)
             for (int e = lane; e < np; e += 64) {
                 int y = e / win, x = e % win;
-                const uint8_t* t = &S.Jt[y * D + x];
-                int diff = DESCALE(t[0] * w00 + t[1] * w01 + t[D] * w10 + t[D + 1] * w11, 9) - S.Iw[e];
-                ib1 += (long long)diff * S.dIx[e];
-                ib2 += (long long)diff * S.dIy[e];
+                const uint8_t* t = &Jw[y * LK_R + x];
+                int diff = DESCALE(t[0] * w00 + t[1] * w01 + t[LK_R] * w10 + t[LK_R + 1] * w11, 9) - S.Iw[e];
+                ib1 += diff * S.dIx[e];
+                ib2 += diff * S.dIy[e];
             }
-            ib1 = wave_sum_i64(ib1);
-            ib2 = wave_sum_i64(ib2);
-            const float b1 = (float)ib1 * FLT_SCALE, b2 = (float)ib2 * FLT_SCALE;
+            const float b1 = (float)wave_sum_i64(ib1) * FLT_SCALE, b2 = (float)wave_sum_i64(ib2) * FLT_SCALE;
             const float ddx = (A12 * b2 - A22 * b1) * Dt;
             const float ddy = (A12 * b1 - A11 * b2) * Dt;
             nx += ddx; ny += ddy;
@@ -236,15 +242,13 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
                 status = 0;
             } else {
                 lk_weights(fx - ix, fy - iy, w00, w01, w10, w11);
-                __builtin_amdgcn_wave_barrier();
-                lk_load_J(S.Jt, J, w, h, Lv.pitch, ix, iy, win, lane);
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                lk_region(S.Jr, rx0, ry0, J, w, h, Lv.pitch, ix, iy, win, lane);
+                const uint8_t* Jw = S.Jr + (iy - ry0) * LK_R + (ix - rx0);
                 long long es = 0;
                 for (int e = lane; e < np; e += 64) {
                     int y = e / win, x = e % win;
-                    const uint8_t* t = &S.Jt[y * D + x];
-                    int diff = DESCALE(t[0] * w00 + t[1] * w01 + t[D] * w10 + t[D + 1] * w11, 9) - S.Iw[e];
+                    const uint8_t* t = &Jw[y * LK_R + x];
+                    int diff = DESCALE(t[0] * w00 + t[1] * w01 + t[LK_R] * w10 + t[LK_R + 1] * w11, 9) - S.Iw[e];
                     es += diff < 0 ? -diff : diff;
                 }
                 es = wave_sum_i64(es);
@@ -1138,20 +1142,48 @@ __global__ void __launch_bounds__(GC_THREADS) gftt_cut_kernel(GfArgs G) {
 __global__ void __launch_bounds__(256) gftt_topk_compact_kernel(GfArgs G) {
     const unsigned int n = min(*G.n_cand, G.cand_cap);
     const unsigned int cut = (unsigned int)G.cut[0];
-    for (unsigned int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        unsigned long long k = G.cand[i];
-        if ((unsigned int)(k >> 52) >= cut) {
-            unsigned int pos = atomicAdd(G.n_top, 1u);
+    const int lane = threadIdx.x & 63;
+    for (unsigned int i0 = blockIdx.x * 256; i0 < n; i0 += gridDim.x * 256) {  // wave-uniform trip count
+        const unsigned int i = i0 + threadIdx.x;
+        unsigned long long k = 0;
+        bool take = false;
+        if (i < n) {
+            k = G.cand[i];
+            take = (unsigned int)(k >> 52) >= cut;
+        }
+        const unsigned long long bal = __ballot(take);  // one counter atomic per wave
+        if (!bal) continue;
+        const int leader = __ffsll((long long)bal) - 1;
+        unsigned int base = 0;
+        if (lane == leader) base = atomicAdd(G.n_top, (unsigned int)__popcll(bal));
+        base = __shfl(base, leader, 64);
+        if (take) {
+            const unsigned int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
             if (pos < G.topk_cap) G.topk[pos] = k;
         }
     }
+}
+
+// per-frame reset of the GFTT counters, histogram and top-K buffer (one launch instead of memsets)
+__global__ void __launch_bounds__(256) gftt_reset_kernel(GfArgs G, int* scal) {
+    const unsigned int t = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
+    if (t == 0) {
+        scal[2] = scal[3] = scal[4] = 0;             // max_ord, n_cand, n_out
+        scal[6] = scal[7] = scal[8] = scal[9] = 0;   // n_top, cut[2], incomplete
+    }
+    for (unsigned int i = t; i < GF_BUCKETS; i += stride) G.hist[i] = 0u;
+    for (unsigned int i = t; i < G.topk_cap; i += stride) G.topk[i] = 0ull;
+}
+hipError_t launch_gftt_reset(const GfArgs& g, int* scal, hipStream_t st) {
+    hipLaunchKernelGGL(gftt_reset_kernel, dim3(64), dim3(256), 0, st, g, scal);
+    return hipGetLastError();
 }
 
 // rasterise the discs of CreateFeatureMask (cv::circle filled, LINE_8; half-widths precomputed
 // on the host from OpenCV's midpoint Circle()) into a 1-bit-per-pixel exclusion mask
 __global__ void __launch_bounds__(128) disc_mask_kernel(DiscArgs D) {
     const int k = blockIdx.x;
-    if (k >= *D.n_pts_dev) return;
+    if (D.n_pts_dev && k >= *D.n_pts_dev) return;  // null: the grid is exactly the point count
     if (D.kept && !D.kept[D.src_index ? D.src_index[k] : k]) return;
     const int i = D.src_index ? D.src_index[k] : k;
     const float fx = D.pts[2 * i], fy = D.pts[2 * i + 1];
@@ -1226,10 +1258,12 @@ hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, h
 }
 // exact fallback: sort every candidate slot (unused slots hold 0 and sort to the end) and redo the
 // greedy pass from the strongest candidate
-hipError_t launch_gftt_full(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {
+hipError_t launch_gftt_full(const GfArgs& g, unsigned int count, void* sort_tmp, size_t sort_tmp_bytes,
+                            hipStream_t st) {
     size_t tb = sort_tmp_bytes;
-    hipError_t e = hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.cand, g.cand_sorted, (int)g.cand_cap,
-                                                               0, 64, st);
+    count = count < g.cand_cap ? count : g.cand_cap;
+    hipError_t e = hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.cand, g.cand_sorted, (int)count, 0, 64,
+                                                               st);
     if (e != hipSuccess) return e;
     if (g.grid_global)
         hipLaunchKernelGGL(gftt_select_kernel<true>, dim3(1), dim3(GS_THREADS), 0, st, g,

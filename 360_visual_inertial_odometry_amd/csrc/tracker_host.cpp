@@ -284,13 +284,9 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     g.topk_cap = t->topk_cap;
     g.topk_target = (unsigned int)std::min<size_t>(t->topk_cap, std::max<size_t>(4096, 16 * (size_t)max_corners));
     // scalars [2] max_ord [3] n_cand [4] n_out [6] n_top [7..8] cut [9] incomplete
-    VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal + 2, 0, 3 * sizeof(int), t->ctx->stream));
-    VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal + 6, 0, 4 * sizeof(int), t->ctx->stream));
-    VIO_HIP(t->ctx, hipMemsetAsync(t->d_hist, 0, sizeof(unsigned int) * GF_BUCKETS, t->ctx->stream));
-    VIO_HIP(t->ctx, hipMemsetAsync(t->d_topk, 0, sizeof(unsigned long long) * t->topk_cap, t->ctx->stream));
-    VIO_HIP(t->ctx, hipMemsetAsync(t->d_cand, 0, sizeof(unsigned long long) * t->cand_cap, t->ctx->stream));
     t->last_gf = g;
-    hipError_t e = launch_gftt(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+    hipError_t e = launch_gftt_reset(g, t->d_scal, t->ctx->stream);
+    if (e == hipSuccess) e = launch_gftt(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
     if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt kernels");
     return VIO_OK;
 }
@@ -304,10 +300,13 @@ int upload_frame(erp_tracker* t, int slot, const uint8_t* img, int stride) {
 
 int read_corners(erp_tracker* t, float* out_xy, int* n_out) {
     int n = 0, inc = 0;
-    VIO_HIP(t->ctx, hipMemcpyAsync(&inc, t->d_scal + 9, sizeof(int), hipMemcpyDeviceToHost, t->ctx->stream));
+    int sc[10];
+    VIO_HIP(t->ctx, hipMemcpyAsync(sc, t->d_scal, sizeof(sc), hipMemcpyDeviceToHost, t->ctx->stream));
     VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    inc = sc[9];
     if (inc) {  // the top-K subset did not decide: exact pass over every candidate
-        hipError_t e = launch_gftt_full(t->last_gf, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+        hipError_t e = launch_gftt_full(t->last_gf, (unsigned int)sc[3], t->d_sort_tmp, t->sort_tmp_bytes,
+                                        t->ctx->stream);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt exact fallback");
         VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal + 9, 0, sizeof(int), t->ctx->stream));
     }
@@ -422,9 +421,8 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         VIO_HIP(t->ctx, hipMemcpy(t->d_halfw, hw.data(), sizeof(int) * (radius + 1), hipMemcpyHostToDevice));
         t->halfw_r = radius;
     }
-    VIO_HIP(t->ctx, hipMemcpyAsync(t->d_scal + 5, &t->n_pts, sizeof(int), hipMemcpyHostToDevice, st));
     if (n > 0 && radius > 0) {
-        DiscArgs d{t->d_next, t->d_kept, nullptr, t->d_scal + 5, t->d_disc, t->disc_words, t->W, t->H, radius,
+        DiscArgs d{t->d_next, t->d_kept, nullptr, nullptr, t->d_disc, t->disc_words, t->W, t->H, radius,
                    t->d_halfw};
         hipError_t e = launch_disc_mask(d, n, st);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "disc_mask_kernel");
@@ -668,7 +666,6 @@ int frontend_detect(erp_frontend* f, std::vector<float>& corners) {
         std::vector<float> xy(2 * (size_t)n);
         for (int i = 0; i < n; ++i) { xy[2 * i] = f->feats[i].x; xy[2 * i + 1] = f->feats[i].y; }
         VIO_HIP(t->ctx, hipMemcpyAsync(t->d_pts, xy.data(), sizeof(float) * 2 * n, hipMemcpyHostToDevice, st));
-        VIO_HIP(t->ctx, hipMemcpyAsync(t->d_scal + 5, &n, sizeof(int), hipMemcpyHostToDevice, st));
         VIO_HIP(t->ctx, hipMemsetAsync(t->d_disc, 0, sizeof(uint32_t) * t->disc_words * t->H, st));
         const int radius = (int)f->p.min_distance;
         if (radius != t->halfw_r) {
@@ -677,7 +674,7 @@ int frontend_detect(erp_frontend* f, std::vector<float>& corners) {
             VIO_HIP(t->ctx, hipMemcpy(t->d_halfw, hw.data(), sizeof(int) * (radius + 1), hipMemcpyHostToDevice));
             t->halfw_r = radius;
         }
-        DiscArgs d{t->d_pts, nullptr, nullptr, t->d_scal + 5, t->d_disc, t->disc_words, t->W, t->H, radius, t->d_halfw};
+        DiscArgs d{t->d_pts, nullptr, nullptr, nullptr, t->d_disc, t->disc_words, t->W, t->H, radius, t->d_halfw};
         hipError_t e = launch_disc_mask(d, n, st);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "disc_mask_kernel");
     }

@@ -89,7 +89,7 @@ struct DiscArgs {
     const float* pts;       // [n][2]
     const uint8_t* kept;    // [n] or null (every point)
     const int* src_index;   // null: point k = pts[k]
-    const int* n_pts_dev;   // device scalar: number of points
+    const int* n_pts_dev;   // device scalar: number of points, or null (grid = point count)
     uint32_t* bits;
     int words, W, H, radius;
     const int* halfw;       // [radius+1]
@@ -101,7 +101,9 @@ hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st);
 hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st);
 // fast path (top-K) and the exact fallback over every candidate (used when `incomplete` is raised)
 hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st);
-hipError_t launch_gftt_full(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st);
+hipError_t launch_gftt_full(const GfArgs& g, unsigned int count, void* sort_tmp, size_t sort_tmp_bytes,
+                            hipStream_t st);  // sorts the first `count` candidates (n_cand read back)
+hipError_t launch_gftt_reset(const GfArgs& g, int* scal, hipStream_t st);
 size_t gftt_sort_tmp_bytes(unsigned int cap);
 hipError_t gftt_select_set_lds(size_t bytes);
 
