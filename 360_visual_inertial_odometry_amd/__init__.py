@@ -303,7 +303,7 @@ class BaBatch:
         return ms.value, cnt.value
 
     PHASES = ["setup", "eval+J", "linearise", "step-prep", "schur-gemm", "cholesky", "backsub",
-              "candidate", "eval-cost", "control", "post", "schur-fill", "schur-prefetch", "schur-assemble"]
+              "candidate", "eval-cost", "control", "post", "schur-fill", "schur-prefetch", "schur-assemble", "imu-eval", "imu-normal-eq"]
 
     def profile(self, enable=True):
         self.ctx.check(lib().vio_ba_batch_profile(self.h, int(enable)), "vio_ba_batch_profile")

@@ -132,6 +132,71 @@ __device__ __forceinline__ int factor_eval(const double* pc, const double* Rcb_r
     return 0;
 }
 
+// BAFactor::Evaluate as factor_eval, returning the Jacobian in compressed form: A = Jw R_cb_raw (2x3,
+// weighted) and Pb (point in the body frame); J_pose / J_point follow as in jac_from_ap.
+__device__ __forceinline__ int factor_eval_ap(const double* pc, const double* Rcb_raw, const double* Pw, double uo,
+                                              double vo, double cols, double rows, const double* Lw, bool outlier,
+                                              bool is_pnp, double* r, double* A, double* Pb, bool& jzero) {
+    jzero = true;
+    if (outlier) {
+        r[0] = 640.0; r[1] = 480.0;
+        return 0;
+    }
+    const double* Rbw = pc + 12;
+    const double* tbw = pc + 21;
+    const double* Rcw = pc + 24;
+    const double* tcw = pc + 33;
+    double Pc[3];
+    m3vec(Rcw, Pw, Pc);
+    Pc[0] += tcw[0]; Pc[1] += tcw[1]; Pc[2] += tcw[2];
+    double x = Pc[0], y = Pc[1], z = Pc[2];
+    double L = nrm3(Pc);
+    if (L < 1e-10) {
+        if (is_pnp) return 1;
+        r[0] = 640.0; r[1] = 360.0;
+        return 0;
+    }
+    const double inv2pi = 1.0 / (2.0 * M_PI);
+    double theta = atan2(x, z);
+    double phi = -asin(y / L);
+    double u = cols * (0.5 + theta / (2.0 * M_PI));
+    double v = rows * (0.5 - phi / M_PI);
+    double du = uo - u, dv = vo - v;
+    if (du > cols / 2.0) du -= cols;
+    else if (du < -cols / 2.0) du += cols;
+    if (fabs(du) > 100.0 || fabs(dv) > 100.0) {
+        r[0] = 100.0; r[1] = 100.0;
+        return 0;
+    }
+    r[0] = Lw[0] * du;
+    r[1] = Lw[2] * du + Lw[3] * dv;
+    double xz2 = x * x + z * z, L2 = L * L;
+    if (xz2 < 1e-10 || L2 < 1e-10) return 0;
+    jzero = false;
+    double xzn = sqrt(xz2);
+    double Jc[6];
+    Jc[0] = -cols * inv2pi * z / xz2;
+    Jc[1] = 0.0;
+    Jc[2] = cols * inv2pi * x / xz2;
+    Jc[3] = rows / M_PI * (x * y) / (L2 * xzn);
+    Jc[4] = -rows / M_PI * xzn / L2;
+    Jc[5] = rows / M_PI * (y * z) / (L2 * xzn);
+    double Jw[6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        Jw[j] = Lw[0] * Jc[j];
+        Jw[3 + j] = Lw[2] * Jc[j] + Lw[3] * Jc[3 + j];
+    }
+    m3vec(Rbw, Pw, Pb);
+    Pb[0] += tbw[0]; Pb[1] += tbw[1]; Pb[2] += tbw[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            A[3 * i + j] = Jw[3 * i] * Rcb_raw[j] + Jw[3 * i + 1] * Rcb_raw[3 + j] + Jw[3 * i + 2] * Rcb_raw[6 + j];
+    return 0;
+}
+
 // compute_chi_square (Factors.cpp:212-265, 544-612), unweighted e^T Info e
 __device__ __forceinline__ double factor_chi2(const double* pc, const double* Pw, double uo, double vo, double cols,
                                               double rows, const double* info, bool outlier, bool is_pnp) {

@@ -54,6 +54,8 @@ struct __align__(16) BaShared {
     int chol_bad;
     int posef[BA_KMAX];          // copy of BaWin::pose_f (per-lane indexed in the Schur fill)
     int pvalid[BA_KMAX];         // preint_valid
+    int8_t icol[BA_KMAX][12];
+    double Rlin[BA_KMAX][9];     // R_bw at the linearisation point (Jacobians are stored compressed)    // imu_col(w, k, c): imu-space index of column c of IMU factor k, or -1
 };
 static_assert(sizeof(BaShared) <= 160 * 1024, "BaShared exceeds the 160 KB LDS of a gfx950 CU");
 static_assert(offsetof(BaShared, stage) == offsetof(BaShared, S) + sizeof(double) * BA_NF_MAX * (BA_NF_MAX + 1),
@@ -64,7 +66,7 @@ __host__ __device__ constexpr int s_ld(int nf) { return (16 * ((nf + 15) >> 4)) 
 static_assert(16 * ((BA_NF_MAX + 15) >> 4) * s_ld(BA_NF_MAX) <= BA_NF_MAX * (BA_NF_MAX + 1), "S padding");
 
 // per-phase shader-clock accounting (diagnostic; enabled when BaPools::prof != nullptr)
-enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST, PF_FILL, PF_PFX, PF_ASM };
+enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST, PF_FILL, PF_PFX, PF_ASM, PF_IMU, PF_IMUH };
 __device__ __forceinline__ void prof_mark(BaShared& sh, int slot) {
     if (sh.prof_on && threadIdx.x == 0) {
         unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -300,6 +302,25 @@ __device__ __forceinline__ void pose_cache(BaShared& sh, const WinCtx& c, const 
     for (int k = threadIdx.x; k < K; k += BA_THREADS) pose_cache_one(sh.pinit[k], xp + 6 * k, sh.pc[k]);
 }
 
+// Compressed observation Jacobian (Factors.cpp:481-534): J_pose = [-A | A [Pb]x], J_point = A R_bw with
+// A = sqrt(rho') Jw R_cb (2x3, weighted and Huber-scaled) and Pb the point in the body frame, so the
+// workspace keeps 9 doubles per observation (A, Pb) instead of 18; R_bw comes from the pose (LDS).
+__device__ __forceinline__ void jac_from_ap(const double* A, const double* Pb, const double* Rbw, double* Jp,
+                                            double* Jl) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const double* a = A + 3 * i;
+        Jp[6 * i + 0] = -a[0];
+        Jp[6 * i + 1] = -a[1];
+        Jp[6 * i + 2] = -a[2];
+        Jp[6 * i + 3] = a[1] * Pb[2] - a[2] * Pb[1];
+        Jp[6 * i + 4] = a[2] * Pb[0] - a[0] * Pb[2];
+        Jp[6 * i + 5] = a[0] * Pb[1] - a[1] * Pb[0];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Jl[3 * i + j] = a[0] * Rbw[j] + a[1] * Rbw[3 + j] + a[2] * Rbw[6 + j];
+    }
+}
+
 // Landmark-chunk walker: lane (jf, kf) = (landmark slot, keyframe) of a chunk of LC = BA_THREADS/K
 // landmarks; its observation is lk[16 l + kf] (or -1).  A landmark's observations are contiguous in
 // the landmark-sorted SoA arrays, so consecutive lanes touch consecutive observations (coalesced),
@@ -352,12 +373,14 @@ __device__ __forceinline__ double eval_lin(BaShared& sh, const WinCtx& c, const 
     const int N = w.N, K = w.K, L = w.L;
     pose_cache(sh, c, xp);
     __syncthreads();
+    // R_bw at this linearisation point for the Schur / back-substitution walks (later barriers order it)
+    for (int e = threadIdx.x; e < 9 * K; e += BA_THREADS) sh.Rlin[e / 9][e % 9] = sh.pc[e / 9][12 + e % 9];
     const Walk g = walk_geom(K);
     const int pf = g.on ? sh.posef[g.kf] : -1;
     const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
     double* r0 = c.ws + c.L.r;
-    double* jp = c.ws + c.L.jp;
-    double* jl = c.ws + c.L.jl;
+    double* ja = c.ws + c.L.jp;          // A [6][N]
+    double* pbw = c.ws + c.L.jp + 6 * (int64_t)N;  // Pb [3][N]
     double* V = c.ws + c.L.V;
     double* gl = c.ws + c.L.gl;
     double* sl = c.ws + c.L.s_l;
@@ -402,10 +425,10 @@ __device__ __forceinline__ double eval_lin(BaShared& sh, const WinCtx& c, const 
             const bool lv = cur.lv != 0;
             if (pf >= 0 || lv) {
                 double Pw[3] = {cur.P[0], cur.P[1], cur.P[2]};
-                double r[2], Jp[12], Jl[6];
+                double r[2], Aj[6], Pb[3];
                 bool jz;
-                const int f = factor_eval(sh.pc[g.kf], sh.Rcb_raw[g.kf], Pw, (double)cur.u, (double)cur.v, w.cols,
-                                          w.rows, w.Lw, cur.out != 0, w.is_pnp, true, r, Jp, Jl, jz);
+                const int f = factor_eval_ap(sh.pc[g.kf], sh.Rcb_raw[g.kf], Pw, (double)cur.u, (double)cur.v, w.cols,
+                                             w.rows, w.Lw, cur.out != 0, w.is_pnp, r, Aj, Pb, jz);
                 if (f) {
                     fail = 1;
                 } else {
@@ -415,21 +438,23 @@ __device__ __forceinline__ double eval_lin(BaShared& sh, const WinCtx& c, const 
                     const double ra = r[0] * sc, rb = r[1] * sc;
                     r0[o] = ra;
                     r0[N + o] = rb;
-                    double a[6], b[6], la[3], lb[3];
 #pragma unroll
                     for (int i = 0; i < 6; ++i) {
-                        a[i] = jz ? 0.0 : Jp[i] * sc;
-                        b[i] = jz ? 0.0 : Jp[6 + i] * sc;
-                        jp[(int64_t)i * N + o] = a[i];
-                        jp[(int64_t)(6 + i) * N + o] = b[i];
+                        Aj[i] = jz ? 0.0 : Aj[i] * sc;
+                        ja[(int64_t)i * N + o] = Aj[i];
                     }
 #pragma unroll
                     for (int i = 0; i < 3; ++i) {
-                        la[i] = jz ? 0.0 : Jl[i] * sc;
-                        lb[i] = jz ? 0.0 : Jl[3 + i] * sc;
-                        jl[(int64_t)i * N + o] = la[i];
-                        jl[(int64_t)(3 + i) * N + o] = lb[i];
+                        Pb[i] = jz ? 0.0 : Pb[i];
+                        pbw[(int64_t)i * N + o] = Pb[i];
                     }
+                    double Jp[12], Jl[6];
+                    jac_from_ap(Aj, Pb, sh.pc[g.kf] + 12, Jp, Jl);
+                    double a[6], b[6], la[3], lb[3];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) { a[i] = Jp[i]; b[i] = Jp[6 + i]; }
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) { la[i] = Jl[i]; lb[i] = Jl[3 + i]; }
                     if (pf >= 0) {
                         int idx = 0;
 #pragma unroll
@@ -492,6 +517,7 @@ __device__ __forceinline__ double eval_lin(BaShared& sh, const WinCtx& c, const 
     for (int i = 0; i < 27; ++i) pr[i * BA_THREADS + threadIdx.x] = acc[i];
     cost += imu_factors(sh, c, xv, xb, true);
     __syncthreads();
+    prof_mark(sh, PF_IMU);
     for (int e = threadIdx.x; e < 27 * K; e += BA_THREADS) {
         const int k = e / 27, i = e - 27 * k;
         if (sh.posef[k] < 0) continue;
@@ -578,16 +604,6 @@ __device__ __forceinline__ int imu_col(const BaWin& w, int k, int c) {
     return f < 0 ? -1 : f - w.np;
 }
 
-// inverse of imu_col: column (0..11) of factor k holding imu index p, or -1
-__device__ __forceinline__ int imu_colinv(const BaWin& w, int k, int p) {
-    const int f = p + w.np;
-    if (w.vel_f[k - 1] >= 0 && f >= w.vel_f[k - 1] && f < w.vel_f[k - 1] + 3) return f - w.vel_f[k - 1];
-    if (w.bg_f >= 0 && f >= w.bg_f && f < w.bg_f + 3) return 3 + f - w.bg_f;
-    if (w.ba_f >= 0 && f >= w.ba_f && f < w.ba_f + 3) return 6 + f - w.ba_f;
-    if (w.vel_f[k] >= 0 && f >= w.vel_f[k] && f < w.vel_f[k] + 3) return 9 + f - w.vel_f[k];
-    return -1;
-}
-
 // After eval_lin: IMU normal equations (imu-space H, g), f-space gradient, column norms (Jacobi
 // scaling at iteration 0) and the gradient max-norm (gm = landmark part from the walk).
 __device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool first, double gm) {
@@ -596,31 +612,43 @@ __device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool fir
     // IMU: per-factor residual/J already in LDS; assemble imu-space H (global) and g.  Factors are
     // added one after another (fixed order); inside a factor the 12 columns map to distinct entries.
     if (w.is_vi) {
-        // one lane per entry of H (and of g), factors added in order: no read-modify-write rounds
+        // imu-space H and g accumulated in LDS (the S area is free until compute_step), factors
+        // added in order (one barrier per factor; inside a factor the 12 columns map to distinct
+        // entries), then written to the workspace once
         const int ni = w.ni;
-        for (int e = threadIdx.x; e < ni * ni + ni; e += BA_THREADS) {
-            const bool isg = e >= ni * ni;
-            const int p = isg ? e - ni * ni : e / ni, q = isg ? 0 : e - (e / ni) * ni;
-            double acc = 0.0;
-            for (int k = 1; k < K; ++k) {
-                if (!sh.pvalid[k]) continue;
-                const int cp = imu_colinv(w, k, p);
-                if (cp < 0) continue;
-                double h = 0.0;
-                if (isg) {
-                    for (int i = 0; i < 9; ++i) h += sh.imu_J[k][12 * i + cp] * sh.imu_r[k][i];
-                } else {
-                    const int cq = imu_colinv(w, k, q);
-                    if (cq < 0) continue;
+        double* Hs = sh.S;
+        double* gs = sh.S + NI_MAX * NI_MAX;
+        for (int e = threadIdx.x; e < ni * ni + ni; e += BA_THREADS) Hs[e < ni * ni ? e : NI_MAX * NI_MAX + e - ni * ni] = 0.0;
+        __syncthreads();
+        for (int k = 1; k < K; ++k) {
+            if (!sh.pvalid[k]) continue;
+            const int e = threadIdx.x;
+            if (e < 144) {
+                const int cp = e / 12, cq = e - 12 * (e / 12);
+                const int p = sh.icol[k][cp], q = sh.icol[k][cq];
+                if (p >= 0 && q >= 0) {
+                    double h = 0.0;
+#pragma unroll
                     for (int i = 0; i < 9; ++i) h += sh.imu_J[k][12 * i + cp] * sh.imu_J[k][12 * i + cq];
+                    Hs[p * ni + q] += h;
                 }
-                acc += h;
+            } else if (e < 156) {
+                const int cp = e - 144;
+                const int p = sh.icol[k][cp];
+                if (p >= 0) {
+                    double g = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 9; ++i) g += sh.imu_J[k][12 * i + cp] * sh.imu_r[k][i];
+                    gs[p] += g;
+                }
             }
-            if (isg) c.gimu[p] = acc;
-            else c.Himu[e] = acc;
+            __syncthreads();
         }
+        for (int e = threadIdx.x; e < ni * ni; e += BA_THREADS) c.Himu[e] = Hs[e];
+        for (int e = threadIdx.x; e < ni; e += BA_THREADS) c.gimu[e] = gs[e];
     }
     __syncthreads();
+    prof_mark(sh, PF_IMUH);
     // f-space gradient and column norms
     for (int f = threadIdx.x; f < w.nf; f += BA_THREADS) {
         double g, cs;
@@ -636,8 +664,8 @@ __device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool fir
             cs = sh.U[k][di];
         } else {
             int p = f - w.np;
-            g = c.gimu[p];
-            cs = c.Himu[p * w.ni + p];
+            g = sh.S[NI_MAX * NI_MAX + p];   // the LDS copies of gimu / Himu (lin_tail above)
+            cs = sh.S[p * w.ni + p];
         }
         sh.g_f[f] = g;
         sh.colsq_f[f] = cs;
@@ -715,8 +743,8 @@ __device__ __forceinline__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     const int KC = schur_kc(LC);
     const int wid = wave_id(), lane = threadIdx.x & 63;
     const int r16 = lane & 15, kk = lane >> 4;
-    const double* jp = c.ws + c.L.jp;
-    const double* jl = c.ws + c.L.jl;
+    const double* ja = c.ws + c.L.jp;                    // A [6][N]
+    const double* pbw = c.ws + c.L.jp + 6 * (int64_t)N;  // Pb [3][N]
     const double* Li = c.ws + c.L.Vi;   // L^-1 of V~ per landmark: i00 i10 i11 i20 i21 i22
     const double* gl = c.ws + c.L.gl;
     const double* sl = c.ws + c.L.s_l;
@@ -734,8 +762,11 @@ __device__ __forceinline__ void schur_gemm(BaShared& sh, const WinCtx& c) {
     const int pf = jf < LC ? sh.posef[kf] : -1;
     // prefetch registers (one chunk ahead); a loaded value is consumed only where it is used
     int o_nx = -1, v_nx = 0;
-    double pj[12], lj[6], sv[3], li[6];
+    double aj[6], pbv[3], sv[3], li[6];
     double hg[3], hs[3], hl[6];
+    double rbw[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) rbw[i] = sh.Rlin[kf < BA_KMAX ? kf : 0][i];
     int hv = 0;
     auto load_obs = [&](int l0n, int& o, int& v) {
         const int l = l0n + jf;
@@ -747,9 +778,9 @@ __device__ __forceinline__ void schur_gemm(BaShared& sh, const WinCtx& c) {
         const int l = l0n + jf;
         if (o >= 0) {
 #pragma unroll
-            for (int i = 0; i < 12; ++i) pj[i] = jp[(int64_t)i * N + o];
+            for (int i = 0; i < 6; ++i) aj[i] = ja[(int64_t)i * N + o];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) lj[i] = jl[(int64_t)i * N + o];
+            for (int i = 0; i < 3; ++i) pbv[i] = pbw[(int64_t)i * N + o];
 #pragma unroll
             for (int i = 0; i < 3; ++i) sv[i] = sl[(int64_t)i * L + l];
 #pragma unroll
@@ -770,6 +801,8 @@ __device__ __forceinline__ void schur_gemm(BaShared& sh, const WinCtx& c) {
         if (pf >= 0) {
             double Z[6][3];
             if (o >= 0) {
+                double pj[12], lj[6];
+                jac_from_ap(aj, pbv, rbw, pj, lj);
                 const double b0 = lj[0] * sv[0], b1 = lj[1] * sv[1], b2 = lj[2] * sv[2];
                 const double d0 = lj[3] * sv[0], d1 = lj[4] * sv[1], d2 = lj[5] * sv[2];
 #pragma unroll
@@ -923,7 +956,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __hiloint2double(hi, lo);
 }
 
-__device__ __noinline__ bool cholesky_solve(BaShared& sh, int nf) {
+__device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
     double* S = sh.S;
     double* LB = sh.stage;  // [nb][16 m][16 c] = Linv_J[c][m]
     const int ls = s_ld(nf), nb = (nf + 15) >> 4;
@@ -1146,15 +1179,18 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
     const int pf = g.on ? sh.posef[g.kf] : -1;
     const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
     const double* r0 = c.ws + c.L.r;
-    const double* jp = c.ws + c.L.jp;
-    const double* jl = c.ws + c.L.jl;
+    const double* ja = c.ws + c.L.jp;                    // A [6][N]
+    const double* pbw = c.ws + c.L.jp + 6 * (int64_t)N;  // Pb [3][N]
     const double* xl = c.ws + c.L.x_lm;
     double* cl = c.ws + c.L.c_lm;
+    double rbw[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) rbw[i] = sh.Rlin[g.kf < BA_KMAX ? g.kf : 0][i];
     double* red = sh.S;                    // [3][BA_THREADS] per-lane W^T-terms
     double* dls = sh.S + 3 * BA_THREADS;   // [LC][3] landmark steps of the chunk
     double fin = 0.0, mc = 0.0, sn = 0.0, xn = 0.0;
     // software pipeline: observation index two chunks ahead, lane and slot data one chunk ahead
-    struct ObsD { double j6[6], p12[12], ra, rb; int o, lv; };
+    struct ObsD { double a6[6], pb[3], ra, rb; int o, lv; };
     struct LmD { double sv[3], gv[3], vi[6], x[3]; int lv; };
     auto ld_o = [&](int l0n) -> int {
         const int l = l0n + g.jf;
@@ -1166,13 +1202,11 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
         if (o >= 0) {
             d.lv = c.lm_var[l0n + g.jf];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) d.j6[i] = jl[(int64_t)i * N + o];
+            for (int i = 0; i < 6; ++i) d.a6[i] = ja[(int64_t)i * N + o];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) d.pb[i] = pbw[(int64_t)i * N + o];
             d.ra = r0[o];
             d.rb = r0[N + o];
-            if (pf >= 0) {
-#pragma unroll
-                for (int i = 0; i < 12; ++i) d.p12[i] = jp[(int64_t)i * N + o];
-            }
         }
     };
     auto ld_lm = [&](int l0n, LmD& d) {
@@ -1208,18 +1242,20 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
         const bool lv = cur.o >= 0 && cur.lv;
         const bool act = cur.o >= 0 && (pf >= 0 || cur.lv);
         double e0 = 0.0, e1 = 0.0;
+        double j6[6], p12[12];
+        jac_from_ap(cur.a6, cur.pb, rbw, p12, j6);
         if (act && pf >= 0) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const double d = sh.D_f[pf + i];
-                e0 += cur.p12[i] * d;
-                e1 += cur.p12[6 + i] * d;
+                e0 += p12[i] * d;
+                e1 += p12[6 + i] * d;
             }
         }
         const bool contrib = lv && pf >= 0;
 #pragma unroll
         for (int cc = 0; cc < 3; ++cc)
-            red[cc * BA_THREADS + threadIdx.x] = contrib ? cur.j6[cc] * e0 + cur.j6[3 + cc] * e1 : 0.0;
+            red[cc * BA_THREADS + threadIdx.x] = contrib ? j6[cc] * e0 + j6[3 + cc] * e1 : 0.0;
         __syncthreads();
         if ((int)threadIdx.x < g.LC) {
             const int lj = l0 + threadIdx.x;
@@ -1271,8 +1307,8 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
 #pragma unroll
                 for (int cc = 0; cc < 3; ++cc) {
                     const double d = dls[3 * g.jf + cc];
-                    m0 += cur.j6[cc] * d;
-                    m1 += cur.j6[3 + cc] * d;
+                    m0 += j6[cc] * d;
+                    m1 += j6[3 + cc] * d;
                 }
             }
             mc -= m0 * (cur.ra + m0 / 2.0) + m1 * (cur.rb + m1 / 2.0);
@@ -1556,6 +1592,10 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
     for (int k = threadIdx.x; k < BA_KMAX; k += BA_THREADS) {
         sh.posef[k] = k < K ? w.pose_f[k] : -1;
         sh.pvalid[k] = k < K ? c.preint_valid[k] : 0;
+    }
+    for (int e = threadIdx.x; e < 12 * BA_KMAX; e += BA_THREADS) {
+        const int k = e / 12, cc = e - 12 * k;
+        sh.icol[k][cc] = (int8_t)((w.is_vi && k >= 1 && k < K) ? imu_col(w, k, cc) : -1);
     }
     {   // (landmark, keyframe) -> observation table for the Schur fill (pairs are unique: host-checked)
         int* lk = reinterpret_cast<int*>(c.ws + c.L.lk);
