@@ -30,8 +30,9 @@ struct LmState {
     double x_cost, cand_cost, min_cost, model_change, x_norm, gmax;
     double initial_cost, final_cost, fixed_cost, iter_cost, step_eval_current;
     double step_norm, cand_x_norm2, rel;
+    double fused_cost;           // cost at the candidate, evaluated inside compute_step
     int iteration, nsucc, nunsucc, consecutive_invalid;
-    int termination, done, step_ok, valid, fail, need_jac, pnp_round;
+    int termination, done, step_ok, valid, fail, need_jac, pnp_round, cand_fail;
 };
 
 struct __align__(16) BaShared {
@@ -54,8 +55,8 @@ struct __align__(16) BaShared {
     int chol_bad;
     int posef[BA_KMAX];          // copy of BaWin::pose_f (per-lane indexed in the Schur fill)
     int pvalid[BA_KMAX];         // preint_valid
-    int8_t icol[BA_KMAX][12];
-    double Rlin[BA_KMAX][9];     // R_bw at the linearisation point (Jacobians are stored compressed)    // imu_col(w, k, c): imu-space index of column c of IMU factor k, or -1
+    int8_t icol[BA_KMAX][12];    // imu_col(w, k, c): imu-space index of column c of IMU factor k, or -1
+    double Rlin[BA_KMAX][9];     // R_bw at the linearisation point (Jacobians are stored compressed)
 };
 static_assert(sizeof(BaShared) <= 160 * 1024, "BaShared exceeds the 160 KB LDS of a gfx950 CU");
 static_assert(offsetof(BaShared, stage) == offsetof(BaShared, S) + sizeof(double) * BA_NF_MAX * (BA_NF_MAX + 1),
@@ -77,6 +78,7 @@ __device__ __forceinline__ void prof_mark(BaShared& sh, int slot) {
 
 // ------------------------------------------------------------------------------------------
 // wave index as a wave-uniform (scalar) value: branches on it stay scalar
+static_assert(BA_THREADS >= 192 && BA_KMAX <= 64, "setup runs three per-keyframe jobs on waves 0..2");
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 // fixed-order block reductions
@@ -531,66 +533,6 @@ __device__ __forceinline__ double eval_lin(BaShared& sh, const WinCtx& c, const 
     if (threadIdx.x == 0 && anyfail > 0.0) sh.st.fail = 1;
     __syncthreads();
     lin_tail(sh, c, first, gm);
-    return total;
-}
-
-// cost only at (xp, xl, xv, xb) (candidate evaluation), same walk
-__device__ __forceinline__ double eval_cost(BaShared& sh, const WinCtx& c, const double* xp, const double* xl, const double* xv,
-                            const double* xb) {
-    const BaWin& w = *c.w;
-    const int K = w.K, L = w.L;
-    pose_cache(sh, c, xp);
-    __syncthreads();
-    const Walk g = walk_geom(K);
-    const int pf = g.on ? sh.posef[g.kf] : -1;
-    const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
-    double cost = 0.0;
-    int fail = 0;
-    struct EvD { double P[3]; float u, v; int o, lv, out; };
-    auto ld_o = [&](int l) -> int { return (g.on && l < L) ? lk[16 * l + g.kf] : -1; };
-    auto ld_ev = [&](int l, int o, EvD& d) {
-        d.o = o;
-        if (o >= 0) {
-            d.lv = c.lm_var[l];
-            d.out = c.outlier[o];
-            d.u = c.obs_uv[2 * o];
-            d.v = c.obs_uv[2 * o + 1];
-            d.P[0] = xl[3 * l]; d.P[1] = xl[3 * l + 1]; d.P[2] = xl[3 * l + 2];
-        }
-    };
-    if (g.on) {
-        EvD cur;
-        int o_nn = ld_o(g.jf + g.LC);
-        ld_ev(g.jf, ld_o(g.jf), cur);
-        for (int l = g.jf; l < L; l += g.LC) {
-            EvD nxt;
-            nxt.o = -1;
-            int o_n2 = -1;
-            if (l + g.LC < L) {
-                ld_ev(l + g.LC, o_nn, nxt);
-                o_n2 = ld_o(l + 2 * g.LC);
-            }
-            if (cur.o >= 0 && (pf >= 0 || cur.lv)) {
-                double r[2], Jp[12], Jl[6];
-                bool jz;
-                if (factor_eval(sh.pc[g.kf], sh.Rcb_raw[g.kf], cur.P, (double)cur.u, (double)cur.v, w.cols, w.rows,
-                                w.Lw, cur.out != 0, w.is_pnp, false, r, Jp, Jl, jz)) {
-                    fail = 1;
-                } else {
-                    double cst, sc;
-                    huber(w.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
-                    cost += cst;
-                }
-            }
-            cur = nxt;
-            o_nn = o_n2;
-        }
-    }
-    cost += imu_factors(sh, c, xv, xb, false);
-    const double total = block_sum(cost, sh.red);
-    const double anyfail = block_max((double)fail, sh.redm);
-    if (threadIdx.x == 0 && anyfail > 0.0) sh.st.fail = 1;
-    __syncthreads();
     return total;
 }
 
@@ -1175,6 +1117,42 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
     for (int f = threadIdx.x; f < nf; f += BA_THREADS) sh.D_f[f] = -sh.b[f] * sh.s_f[f];  // delta_f
     __syncthreads();
     const int K = w.K;
+    double fin = 0.0, mc = 0.0, sn = 0.0, xn = 0.0;
+    double ccost = 0.0;  // cost at the candidate (TrustRegionMinimizer evaluates it next; fused here)
+    int cfail = 0;
+    double* ws = c.ws;
+    double* xp = ws + c.L.x_pose; double* cp_ = ws + c.L.c_pose;
+    double* xv = ws + c.L.x_vel;  double* cv = ws + c.L.c_vel;
+    double* xb = ws + c.L.x_bias; double* cb = ws + c.L.c_bias;
+    for (int e = threadIdx.x; e < 6 * K; e += BA_THREADS) {
+        int k = e / 6, i = e % 6;
+        int pfk = w.pose_f[k];
+        double x = xp[e];
+        double cnd = pfk >= 0 ? x + sh.D_f[pfk + i] : x;
+        cp_[e] = cnd;
+        if (pfk >= 0) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
+    }
+    if (w.is_vi) {
+        for (int e = threadIdx.x; e < 3 * K; e += BA_THREADS) {
+            int k = e / 3, cc = e % 3;
+            int vf = w.vel_f[k];
+            double x = xv[e];
+            double cnd = vf >= 0 ? x + sh.D_f[vf + cc] : x;
+            cv[e] = cnd;
+            if (vf >= 0) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
+        }
+        for (int e = threadIdx.x; e < 6; e += BA_THREADS) {
+            int f = e < 3 ? w.bg_f + e : w.ba_f + e - 3;
+            bool a = e < 3 ? w.bg_f >= 0 : w.ba_f >= 0;
+            double x = xb[e];
+            double cnd = a ? x + sh.D_f[f] : x;
+            cb[e] = cnd;
+            if (a) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
+        }
+    }
+    __syncthreads();
+    pose_cache(sh, c, cp_);  // sh.pc now holds the candidate poses (the step uses sh.Rlin)
+    __syncthreads();
     const Walk g = walk_geom(K);
     const int pf = g.on ? sh.posef[g.kf] : -1;
     const int* lk = reinterpret_cast<const int*>(c.ws + c.L.lk);
@@ -1188,9 +1166,9 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
     for (int i = 0; i < 9; ++i) rbw[i] = sh.Rlin[g.kf < BA_KMAX ? g.kf : 0][i];
     double* red = sh.S;                    // [3][BA_THREADS] per-lane W^T-terms
     double* dls = sh.S + 3 * BA_THREADS;   // [LC][3] landmark steps of the chunk
-    double fin = 0.0, mc = 0.0, sn = 0.0, xn = 0.0;
+    double* cps = sh.S + 6 * BA_THREADS;   // [LC][3] landmark candidates of the chunk
     // software pipeline: observation index two chunks ahead, lane and slot data one chunk ahead
-    struct ObsD { double a6[6], pb[3], ra, rb; int o, lv; };
+    struct ObsD { double a6[6], pb[3], ra, rb; float u, v; int o, lv, out; };
     struct LmD { double sv[3], gv[3], vi[6], x[3]; int lv; };
     auto ld_o = [&](int l0n) -> int {
         const int l = l0n + g.jf;
@@ -1207,6 +1185,9 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
             for (int i = 0; i < 3; ++i) d.pb[i] = pbw[(int64_t)i * N + o];
             d.ra = r0[o];
             d.rb = r0[N + o];
+            d.u = c.obs_uv[2 * o];
+            d.v = c.obs_uv[2 * o + 1];
+            d.out = c.outlier[o];
         }
     };
     auto ld_lm = [&](int l0n, LmD& d) {
@@ -1297,6 +1278,7 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
                         xn += cnd * cnd;
                     }
                     dls[3 * threadIdx.x + cc] = d[cc];
+                    cps[3 * threadIdx.x + cc] = cnd;
                 }
             }
         }
@@ -1312,6 +1294,18 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
                 }
             }
             mc -= m0 * (cur.ra + m0 / 2.0) + m1 * (cur.rb + m1 / 2.0);
+            // the residual block at the candidate (point + pose of this lane)
+            double Pc[3] = {cps[3 * g.jf], cps[3 * g.jf + 1], cps[3 * g.jf + 2]};
+            double r[2], Jp[12], Jl[6];
+            bool jz;
+            if (factor_eval(sh.pc[g.kf], sh.Rcb_raw[g.kf], Pc, (double)cur.u, (double)cur.v, w.cols, w.rows, w.Lw,
+                            cur.out != 0, w.is_pnp, false, r, Jp, Jl, jz)) {
+                cfail = 1;
+            } else {
+                double cst, sc;
+                huber(w.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
+                ccost += cst;
+            }
         }
         cur = nxt;
         lcur = lnxt;
@@ -1320,8 +1314,7 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
     for (int f = threadIdx.x; f < nf; f += BA_THREADS)
         if (!isfinite(sh.b[f])) fin = 1.0;
     prof_mark(sh, PF_BACKSUB);
-    // IMU part of the model change, pose / velocity / bias candidates and norms
-    double* ws = c.ws;
+    // IMU part of the model change
     if (w.is_vi) {
         for (int k = 1 + threadIdx.x; k < K; k += BA_THREADS) {
             if (!c.preint_valid[k]) continue;
@@ -1336,44 +1329,20 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
             for (int i = 0; i < 9; ++i) mc -= m[i] * (sh.imu_r[k][i] + m[i] / 2.0);
         }
     }
-    double* xp = ws + c.L.x_pose; double* cp_ = ws + c.L.c_pose;
-    double* xv = ws + c.L.x_vel;  double* cv = ws + c.L.c_vel;
-    double* xb = ws + c.L.x_bias; double* cb = ws + c.L.c_bias;
-    for (int e = threadIdx.x; e < 6 * K; e += BA_THREADS) {
-        int k = e / 6, i = e % 6;
-        int pfk = w.pose_f[k];
-        double x = xp[e];
-        double cnd = pfk >= 0 ? x + sh.D_f[pfk + i] : x;
-        cp_[e] = cnd;
-        if (pfk >= 0) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
-    }
-    if (w.is_vi) {
-        for (int e = threadIdx.x; e < 3 * K; e += BA_THREADS) {
-            int k = e / 3, cc = e % 3;
-            int vf = w.vel_f[k];
-            double x = xv[e];
-            double cnd = vf >= 0 ? x + sh.D_f[vf + cc] : x;
-            cv[e] = cnd;
-            if (vf >= 0) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
-        }
-        for (int e = threadIdx.x; e < 6; e += BA_THREADS) {
-            int f = e < 3 ? w.bg_f + e : w.ba_f + e - 3;
-            bool a = e < 3 ? w.bg_f >= 0 : w.ba_f >= 0;
-            double x = xb[e];
-            double cnd = a ? x + sh.D_f[f] : x;
-            cb[e] = cnd;
-            if (a) { double d = x - cnd; sn += d * d; xn += cnd * cnd; }
-        }
-    }
+    ccost += imu_factors(sh, c, cv, cb, false);  // IMU factors at the candidate
     const double nonfinite = block_max(fin, sh.redm);
     const double mct = block_sum(mc, sh.red);
     const double snt = block_sum(sn, sh.red);
     const double xnt = block_sum(xn, sh.red);
+    const double cct = block_sum(ccost, sh.red);
+    const double cfl = block_max((double)cfail, sh.redm);
     if (threadIdx.x == 0) {
         sh.st.valid = nonfinite > 0.0 ? 0 : 1;
         sh.st.model_change = mct;
         sh.st.step_norm = sqrt(snt);
         sh.st.cand_x_norm2 = xnt;
+        sh.st.fused_cost = cct;
+        sh.st.cand_fail = cfl > 0.0 ? 1 : 0;
     }
     __syncthreads();
     prof_mark(sh, PF_CAND);
@@ -1484,7 +1453,10 @@ __device__ __forceinline__ void lm_solve(BaShared& sh, const WinCtx& c) {
         if (threadIdx.x == 0) { sh.st.consecutive_invalid = 0; sh.st.fail = 0; }
         __syncthreads();
         prof_mark(sh, PF_CTRL);
-        double cc = eval_cost(sh, c, ws + c.L.c_pose, ws + c.L.c_lm, ws + c.L.c_vel, ws + c.L.c_bias);
+        // candidate cost: evaluated inside compute_step (same residual blocks, same order of terms per lane)
+        double cc = sh.st.fused_cost;
+        if (threadIdx.x == 0 && sh.st.cand_fail) sh.st.fail = 1;
+        __syncthreads();
         prof_mark(sh, PF_EVAL_C);
         if (threadIdx.x == 0) {
             LmState& s = sh.st;
@@ -1579,14 +1551,22 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
     __syncthreads();
 
     // ---- setup: projected input rotations (SE3d(T_wb_init), SE3d(T_cb)), raw R_cb, IMU sqrt-info
-    for (int k = threadIdx.x; k < K; k += BA_THREADS) {
-        const double* pr = c.pose_raw + 24 * k;
-        polar3(pr, sh.pinit[k]);
-        for (int i = 0; i < 3; ++i) sh.pinit[k][9 + i] = pr[9 + i];
-        polar3(pr + 12, sh.pinit[k] + 12);
-        for (int i = 0; i < 3; ++i) sh.pinit[k][21 + i] = pr[21 + i];
-        for (int i = 0; i < 9; ++i) sh.Rcb_raw[k][i] = pr[12 + i];
-        if (w.is_vi && k >= 1 && c.preint_valid[k]) imu_sqrt_info(c.preint[k], c.sqi + 81 * k);
+    {   // three independent serial jobs per keyframe on three different waves (SIMDs): SO3 projection
+        // of R_init (wave 0), of R_cb (wave 1), IMU sqrt-information (wave 2); K <= BA_KMAX <= 64
+        const int job = threadIdx.x >> 6, k = threadIdx.x & 63;
+        if (k < K) {
+            const double* pr = c.pose_raw + 24 * k;
+            if (job == 0) {
+                polar3(pr, sh.pinit[k]);
+                for (int i = 0; i < 3; ++i) sh.pinit[k][9 + i] = pr[9 + i];
+            } else if (job == 1) {
+                polar3(pr + 12, sh.pinit[k] + 12);
+                for (int i = 0; i < 3; ++i) sh.pinit[k][21 + i] = pr[21 + i];
+                for (int i = 0; i < 9; ++i) sh.Rcb_raw[k][i] = pr[12 + i];
+            } else if (job == 2) {
+                if (w.is_vi && k >= 1 && c.preint_valid[k]) imu_sqrt_info(c.preint[k], c.sqi + 81 * k);
+            }
+        }
     }
     for (int o = threadIdx.x; o < N; o += BA_THREADS) c.outlier[o] = 0;
     for (int k = threadIdx.x; k < BA_KMAX; k += BA_THREADS) {
