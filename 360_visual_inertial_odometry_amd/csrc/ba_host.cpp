@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -19,6 +20,10 @@
 namespace vio360 {
 
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream);
+hipError_t launch_ba_phases(const BaPools& P, const BaWin* hw, int n, hipStream_t stream);
+size_t ba_phase_doubles(int K, int L, int T);
+const char* ba_phases_failed_launch();
+hipError_t ba_phases_prepare(const BaWin* hw, int n);
 bool global_ba_applicable(const vio_ba_problem& p);
 int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out);
 size_t ba_ws_extra_doubles();
@@ -152,7 +157,7 @@ int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
     w.o_ws = pk.ws_total;
     w.o_out = pk.out_total;
     BaWsLayout WL = ba_ws_layout(K, L, N);
-    pk.ws_total += WL.total + (int64_t)ba_ws_extra_doubles();
+    pk.ws_total += WL.total + (int64_t)ba_ws_extra_doubles() + (int64_t)ba_phase_doubles(K, L, w.T);
     pk.ws_total = (pk.ws_total + 31) & ~(int64_t)31;
     pk.out_total += ba_out_layout(K, L, N).total;
     // poses
@@ -227,6 +232,8 @@ struct BaDevice {
     BaPools P{};
     void* prof_buf = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipGraphExec_t phase_graph = nullptr;  // the captured phase-kernel sequence of this batch
+    bool reusable = false;                 // vio_ba_batch: replayed many times (graph); one-shot solves launch directly
     double ms_sum = 0.0;
     int ms_count = 0;
     bool timing_pending = false;
@@ -296,6 +303,8 @@ static void free_batch(BaDevice& d) {
     if (d.ev0) (void)hipEventDestroy(d.ev0);
     if (d.ev1) (void)hipEventDestroy(d.ev1);
     d.ev0 = d.ev1 = nullptr;
+    if (d.phase_graph) (void)hipGraphExecDestroy(d.phase_graph);
+    d.phase_graph = nullptr;
 }
 
 static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
@@ -353,10 +362,57 @@ static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
     return VIO_OK;
 }
 
+// Small batches of LocalBA / BA / VIBA windows (fewer than the chip has CUs to spare: a window's
+// observation walks then spread over many workgroups) run as the phase-kernel sequence
+// (ba_phases.inc); large batches, where one workgroup per window already fills the chip, and PnP
+// windows (outlier rounds inside one solve) run in ba_window_kernel.  Within a path a window's result
+// does not depend on the batch it is in.  Per-window phase profiling and VIO_BA_MONOLITHIC=1 put every
+// window on ba_window_kernel, VIO_BA_PHASES=1 every non-PnP window on the phase kernels (A/B runs).
+constexpr int PHASE_BATCH_MAX = 32;
+static bool env_flag(const char* name) {
+    const char* e = std::getenv(name);
+    return e && e[0] == '1';
+}
+static bool force_monolithic(const BaDevice& d) {
+    static const bool mono = env_flag("VIO_BA_MONOLITHIC"), phases = env_flag("VIO_BA_PHASES");
+    if (mono || d.P.prof) return true;
+    if (phases) return false;
+    int non_pnp = 0;
+    for (const BaWin& w : d.pk.win) non_pnp += w.is_pnp ? 0 : 1;
+    return non_pnp > PHASE_BATCH_MAX;
+}
+
 static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     if (timed) VIO_HIP(ctx, hipEventRecord(d.ev0, ctx->stream));
-    hipError_t e = launch_ba_windows(d.P, d.n, ctx->stream);
-    if (e != hipSuccess) return hip_fail(ctx, e, "ba_window_kernel launch");
+    bool any_pnp = false, any_other = false;
+    for (const BaWin& w : d.pk.win) (w.is_pnp ? any_pnp : any_other) = true;
+    const bool phases = any_other && !force_monolithic(d);
+    d.P.route = phases ? 1 : 0;
+    hipError_t e = hipSuccess;
+    const char* what = "ba_window_kernel launch";
+    if (phases) {
+        // ~70 launches per solve: a reusable batch captures them once into a graph (same arguments
+        // every run) and replays it; a one-shot solve launches them directly
+        e = ba_phases_prepare(d.pk.win.data(), d.n);
+        if (e != hipSuccess) what = "hipFuncSetAttribute(phase kernels)";
+        if (e == hipSuccess && !d.reusable) {
+            e = launch_ba_phases(d.P, d.pk.win.data(), d.n, ctx->stream);
+            if (e != hipSuccess) what = ba_phases_failed_launch();
+        } else if (e == hipSuccess && !d.phase_graph) {
+            hipGraph_t g = nullptr;
+            e = hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal);
+            if (e == hipSuccess) {
+                hipError_t el = launch_ba_phases(d.P, d.pk.win.data(), d.n, ctx->stream);
+                e = hipStreamEndCapture(ctx->stream, &g);
+                if (el != hipSuccess) e = el, what = ba_phases_failed_launch();
+            }
+            if (e == hipSuccess) e = hipGraphInstantiate(&d.phase_graph, g, nullptr, nullptr, 0);
+            if (g) (void)hipGraphDestroy(g);
+        }
+        if (e == hipSuccess && d.reusable) e = hipGraphLaunch(d.phase_graph, ctx->stream);
+    }
+    if (e == hipSuccess && (any_pnp || !phases)) e = launch_ba_windows(d.P, d.n, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, what);
     if (timed) {
         VIO_HIP(ctx, hipEventRecord(d.ev1, ctx->stream));
         d.timing_pending = true;
@@ -427,6 +483,7 @@ int vio_ba_batch_create(vio_ctx* ctx, const vio_ba_problem* probs, int n, vio_ba
     vio_ba_batch* b = new vio_ba_batch();
     b->ctx = ctx;
     b->dev.n = n;
+    b->dev.reusable = true;
     for (int i = 0; i < n; ++i) {
         int rc = pack_window(ctx, probs[i], b->dev.pk);
         if (rc != VIO_OK) { delete b; return rc; }

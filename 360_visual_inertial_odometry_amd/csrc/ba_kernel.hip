@@ -16,6 +16,8 @@
 #include <float.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "ba_types.h"
 #include "ba_factor_dev.h"
 #include "lie_dev.h"
@@ -24,6 +26,8 @@ namespace vio360 {
 
 constexpr int VI_KMAX = 10;  // VIBA windows on this path: K <= 10 (ni = 3K+6 <= 36)
 constexpr int NI_MAX = 3 * VI_KMAX + 6;
+// per-window workspace after ba_ws_layout(): IMU sqrt-information, imu-space H and g
+__host__ __device__ constexpr int64_t ba_ws_extra() { return 81 * BA_KMAX + NI_MAX * NI_MAX + NI_MAX + 32; }
 
 struct LmState {
     double radius, decrease_factor;
@@ -1520,6 +1524,7 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
     BaShared& sh = *reinterpret_cast<BaShared*>(smem_raw);
     const BaWin& w = P.win[blockIdx.x];
+    if (P.route == 1 && !w.is_pnp) return;  // solved by the phase kernels
     WinCtx c;
     c.w = &w;
     c.L = ba_ws_layout(w.K, w.L, w.N);
@@ -1733,7 +1738,7 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
 }
 
 size_t ba_shared_bytes() { return sizeof(BaShared); }
-size_t ba_ws_extra_doubles() { return 81 * BA_KMAX + NI_MAX * NI_MAX + NI_MAX + 32; }
+size_t ba_ws_extra_doubles() { return ba_ws_extra(); }
 
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream) {
     static bool attr_set = false;
@@ -1748,3 +1753,5 @@ hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream) {
 }
 
 }  // namespace vio360
+
+#include "ba_phases.inc"
