@@ -303,13 +303,14 @@ class BaBatch:
         return ms.value, cnt.value
 
     PHASES = ["setup", "eval+J", "linearise", "step-prep", "schur-gemm", "cholesky", "backsub",
-              "candidate", "eval-cost", "control", "post", "schur-fill", "schur-prefetch", "schur-assemble", "imu-eval", "imu-normal-eq"]
+              "candidate", "eval-cost", "control", "post", "schur-fill", "schur-prefetch", "schur-assemble", "imu-eval", "imu-normal-eq",
+              "eval-factors", "eval-landmarks", "backsub-jac", "backsub-landmarks", "backsub-candidate-cost"]
 
     def profile(self, enable=True):
         self.ctx.check(lib().vio_ba_batch_profile(self.h, int(enable)), "vio_ba_batch_profile")
 
     def phase_cycles(self):
-        out = (C.c_ulonglong * 16)()
+        out = (C.c_ulonglong * 24)()
         self.ctx.check(lib().vio_ba_batch_phase_cycles(self.h, out), "vio_ba_batch_phase_cycles")
         return {n: int(out[i]) for i, n in enumerate(self.PHASES)}
 

@@ -539,22 +539,23 @@ int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count) {
 int vio_ba_batch_profile(vio_ba_batch* b, int enable) {
     if (!b) return VIO_EINVAL;
     if (enable && !b->dev.prof_buf) {
-        VIO_HIP(b->ctx, hipMalloc(&b->dev.prof_buf, sizeof(unsigned long long) * 16 * b->dev.n));
-        VIO_HIP(b->ctx, hipMemsetAsync(b->dev.prof_buf, 0, sizeof(unsigned long long) * 16 * b->dev.n, b->ctx->stream));
+        VIO_HIP(b->ctx, hipMalloc(&b->dev.prof_buf, sizeof(unsigned long long) * VIO_BA_PROF_SLOTS * b->dev.n));
+        VIO_HIP(b->ctx, hipMemsetAsync(b->dev.prof_buf, 0, sizeof(unsigned long long) * VIO_BA_PROF_SLOTS * b->dev.n, b->ctx->stream));
     }
     b->dev.P.prof = enable ? (unsigned long long*)b->dev.prof_buf : nullptr;
     return VIO_OK;
 }
 
-int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out16) {
-    if (!b || !out16 || !b->dev.prof_buf) return VIO_EINVAL;
-    std::vector<unsigned long long> v(16 * b->dev.n);
+int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out) {
+    if (!b || !out || !b->dev.prof_buf) return VIO_EINVAL;
+    constexpr int NS = VIO_BA_PROF_SLOTS;
+    std::vector<unsigned long long> v(NS * b->dev.n);
     VIO_HIP(b->ctx, hipMemcpyAsync(v.data(), b->dev.prof_buf, sizeof(unsigned long long) * v.size(),
                                    hipMemcpyDeviceToHost, b->ctx->stream));
     VIO_HIP(b->ctx, hipStreamSynchronize(b->ctx->stream));
-    for (int s = 0; s < 16; ++s) {
-        out16[s] = 0;
-        for (int i = 0; i < b->dev.n; ++i) out16[s] += v[16 * i + s];
+    for (int s = 0; s < NS; ++s) {
+        out[s] = 0;
+        for (int i = 0; i < b->dev.n; ++i) out[s] += v[NS * i + s];
     }
     return VIO_OK;
 }

@@ -53,7 +53,7 @@ struct __align__(16) BaShared {
     double red[BA_THREADS / 64 + 4];
     double redm[BA_THREADS / 64 + 4];
     LmState st;
-    unsigned long long prof_acc[16];
+    unsigned long long prof_acc[VIO_BA_PROF_SLOTS];
     unsigned long long prof_last;
     int prof_on;
     int chol_bad;
@@ -69,9 +69,13 @@ static_assert(offsetof(BaShared, stage) == offsetof(BaShared, S) + sizeof(double
 // row stride of S: tile-padded size, odd (conflict-free column walks)
 __host__ __device__ constexpr int s_ld(int nf) { return (16 * ((nf + 15) >> 4)) | 1; }
 static_assert(16 * ((BA_NF_MAX + 15) >> 4) * s_ld(BA_NF_MAX) <= BA_NF_MAX * (BA_NF_MAX + 1), "S padding");
+static_assert(256 * (((BA_NF_MAX + 15) >> 4) + 1) + 16 <= BA_STAGE, "Cholesky tiles (Linv, L of the diagonal tile, rhs) fit the stage area");
 
 // per-phase shader-clock accounting (diagnostic; enabled when BaPools::prof != nullptr)
-enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST, PF_FILL, PF_PFX, PF_ASM, PF_IMU, PF_IMUH };
+enum { PF_SETUP = 0, PF_EVAL_J, PF_LIN, PF_PREP, PF_GEMM, PF_CHOL, PF_BACKSUB, PF_CAND, PF_EVAL_C, PF_CTRL, PF_POST, PF_FILL, PF_PFX, PF_ASM, PF_IMU, PF_IMUH,
+       PF_EV_F, PF_EV_L, PF_BS_J, PF_BS_L, PF_BS_C, PF_NSLOT = VIO_BA_PROF_SLOTS };
+// per-chunk marks inside the walks (PF_EV_*, PF_BS_*) cost a few percent: compiled in on demand
+constexpr bool kProfWalk = false;
 __device__ __forceinline__ void prof_mark(BaShared& sh, int slot) {
     if (sh.prof_on && threadIdx.x == 0) {
         unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -346,6 +350,33 @@ __device__ __forceinline__ Walk walk_geom(int K) {
     return g;
 }
 
+// Landmark sums of one walk chunk: q[i][slot*K + kf] (i < 9: the 6 V~ entries and 3 gradient entries
+// of each observation lane) summed over the K keyframe lanes of each landmark slot, kf ascending.
+// One lane per (entry, landmark) pair: a 9xLC job instead of LC lanes summing 9K values each.
+// Writes V / g_l (and the Jacobi scaling s_l on the first linearisation); returns the lane's
+// running max |g_l| (combined by a block max later, exact in any order).
+__device__ __forceinline__ double lm_sums9(const double* q, int l0, const Walk& g, int K, int L,
+                                           const uint8_t* lm_var, double* V, double* gl, double* sl, bool first,
+                                           double gm) {
+    for (int t = threadIdx.x; t < 9 * g.LC; t += BA_THREADS) {
+        const int i = t / g.LC, j = t - i * g.LC, lj = l0 + j;
+        if (lj >= L || !lm_var[lj]) continue;
+        const double* src = q + i * BA_THREADS + j * K;
+        double v = 0.0;
+#pragma unroll
+        for (int kf = 0; kf < BA_KMAX; ++kf)
+            if (kf < K) v += src[kf];
+        if (i < 6) {
+            V[(int64_t)i * L + lj] = v;
+        } else {
+            gl[(int64_t)(i - 6) * L + lj] = v;
+            gm = fmax(gm, fabs(v));
+        }
+        if (first && (i == 0 || i == 3 || i == 5)) sl[(int64_t)(i == 0 ? 0 : i == 3 ? 1 : 2) * L + lj] = 1.0 / (1.0 + sqrt(v));
+    }
+    return gm;
+}
+
 // IMU factors (one lane per factor): cost, and residual/Jacobian into LDS when want_jac
 __device__ __forceinline__ double imu_factors(BaShared& sh, const WinCtx& c, const double* xv, const double* xb, bool want_jac) {
     const BaWin& w = *c.w;
@@ -488,30 +519,10 @@ __device__ __forceinline__ double eval_lin(BaShared& sh, const WinCtx& c, const 
         double* rb_ = sh.S + (ci & 1) * 9 * BA_THREADS;
 #pragma unroll
         for (int i = 0; i < 9; ++i) rb_[i * BA_THREADS + threadIdx.x] = v9[i];
+        if (kProfWalk) prof_mark(sh, PF_EV_F);
         __syncthreads();
-        if ((int)threadIdx.x < g.LC) {
-            const int lj = l0 + threadIdx.x;
-            if (lj < L && c.lm_var[lj]) {
-                double v[9];
-#pragma unroll
-                for (int i = 0; i < 9; ++i) v[i] = 0.0;
-#pragma unroll
-                for (int kf = 0; kf < BA_KMAX; ++kf)
-                    if (kf < K)
-#pragma unroll
-                        for (int i = 0; i < 9; ++i) v[i] += rb_[i * BA_THREADS + threadIdx.x * K + kf];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) V[(int64_t)i * L + lj] = v[i];
-#pragma unroll
-                for (int i = 0; i < 3; ++i) gl[(int64_t)i * L + lj] = v[6 + i];
-                gm = fmax(gm, fmax(fabs(v[6]), fmax(fabs(v[7]), fabs(v[8]))));
-                if (first) {
-                    sl[lj] = 1.0 / (1.0 + sqrt(v[0]));
-                    sl[(int64_t)L + lj] = 1.0 / (1.0 + sqrt(v[3]));
-                    sl[2 * (int64_t)L + lj] = 1.0 / (1.0 + sqrt(v[5]));
-                }
-            }
-        }
+        gm = lm_sums9(rb_, l0, g, K, L, c.lm_var, V, gl, sl, first, gm);
+        if (kProfWalk) prof_mark(sh, PF_EV_L);
         cur = nxt;
         o_nn = o_n2;
     }
@@ -889,22 +900,39 @@ __device__ __forceinline__ void schur_gemm(BaShared& sh, const WinCtx& c) {
 
 // Cholesky of S (nf x nf in LDS, padded to nb = ceil(nf/16) 16x16 tiles with an identity tail,
 // row stride s_ld(nf)) then solve S y = b (y overwrites b).  Blocked right-looking:
-//   (A) wave 0 factors the diagonal tile in registers (lane i = row i, pivots and column entries
-//       broadcast with v_readlane) and forms its triangular inverse; Linv_J^T goes to the stage area;
+//   (A) wave 0 factors the diagonal tile in registers (lane i = row i; pivots and column entries
+//       broadcast with v_readlane; 1/sqrt by v_rsq_f64 + two Newton steps), writes the tile's L to
+//       LDS and forms the triangular inverse from LDS broadcast reads; Linv_J^T goes to the stage area;
 //   (B) panel tiles L_IJ = S_IJ Linv_J^T on v_mfma_f64_16x16x4_f64, one tile per wave at a time;
 //   (C) trailing lower tiles S_IK -= L_IJ L_KJ^T on the matrix cores.
 // Three workgroup barriers per tile column.  The two triangular solves walk the tile columns with
-// one wave (lanes = 16 rows x 4 column groups).  Fixed operation order: bitwise reproducible.
+// one wave (lanes = 16 rows x 4 column groups; the tile's right-hand side is broadcast through LDS).
+// Fixed operation order: bitwise reproducible.  (tools/probe/chol_probe.hip times the variants.)
 // Returns false (uniformly) when a pivot is not positive (S not positive definite).
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
     return __hiloint2double(hi, lo);
 }
+// 1/sqrt(p) to full double precision: hardware estimate + two Newton-Raphson steps
+__device__ __forceinline__ double rsq_nr(double p) {
+    double r = __builtin_amdgcn_rsq(p);
+    const double h = 0.5 * p;
+    r = r * fma(-h * r, r, 1.5);
+    r = r * fma(-h * r, r, 1.5);
+    return r;
+}
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
     double* S = sh.S;
     double* LB = sh.stage;  // [nb][16 m][16 c] = Linv_J[c][m]
+    double* LT = sh.stage + 256 * ((BA_NF_MAX + 15) >> 4);  // [16 m][16 q] = L_JJ[q][m]; then 16 rhs
+    double* TB = LT + 256;
     const int ls = s_ld(nf), nb = (nf + 15) >> 4;
     constexpr int NW = BA_THREADS / 64;
     const int wid = wave_id(), lane = threadIdx.x & 63;
@@ -923,20 +951,25 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
             for (int j = 0; j < 16; ++j) {
                 const double piv = readlane_d(d[j], j);
                 bad |= !(piv > 0.0);
-                const double lj = sqrt(piv);
-                il[j] = 1.0 / lj;
-                const double cj = i == j ? lj : d[j] * il[j];
+                const double r = rsq_nr(piv);
+                il[j] = r;
+                const double cj = i == j ? piv * r : d[j] * r;
                 d[j] = cj;
 #pragma unroll
                 for (int k = j + 1; k < 16; ++k) d[k] -= cj * readlane_d(cj, k);
             }
-            // column i of Linv (lower): x[q] = Linv[q][i]
+            if (kk == 0) {
+#pragma unroll
+                for (int m = 0; m < 16; ++m) LT[16 * m + i] = d[m];
+            }
+            wave_lds_sync();
+            // column i of Linv (lower): x[q] = Linv[q][i]; L[q][m] read as a broadcast
             double x[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 double s = q == i ? 1.0 : 0.0;
 #pragma unroll
-                for (int m = 0; m < q; ++m) s -= readlane_d(d[m], q) * x[m];
+                for (int m = 0; m < q; ++m) s -= LT[16 * m + q] * x[m];
                 x[q] = s * il[q];
             }
             // LB[m][c] = Linv[c][m]: lane m holds column m of Linv, i.e. Linv[c][m] = x[c]
@@ -1000,13 +1033,15 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
             t += __shfl_xor(t, 32, 64);
             t = y[16 * J + r16] - t;
             const double* lb = LB + 256 * J;
+            if (kk == 0) TB[r16] = t;
+            wave_lds_sync();
             double v = 0.0;
 #pragma unroll
-            for (int mm = 0; mm < 16; ++mm) v += lb[16 * mm + r16] * readlane_d(t, mm);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            for (int q = 0; q < 4; ++q) v += lb[16 * (kk + 4 * q) + r16] * TB[kk + 4 * q];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
             if (kk == 0) y[16 * J + r16] = v;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_lds_sync();
         }
         for (int J = nb - 1; J >= 0; --J) {  // backward: x_J = Linv_J^T (y_J - sum_{K>J} L_KJ^T x_K)
             double p0 = 0.0, p1 = 0.0;
@@ -1022,13 +1057,15 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
             t += __shfl_xor(t, 32, 64);
             t = y[16 * J + r16] - t;
             const double* lb = LB + 256 * J;
+            if (kk == 0) TB[r16] = t;
+            wave_lds_sync();
             double v = 0.0;
 #pragma unroll
-            for (int mm = 0; mm < 16; ++mm) v += lb[16 * r16 + mm] * readlane_d(t, mm);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            for (int q = 0; q < 4; ++q) v += lb[16 * r16 + kk + 4 * q] * TB[kk + 4 * q];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
             if (kk == 0) y[16 * J + r16] = v;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_lds_sync();
         }
     }
     __syncthreads();
@@ -1242,6 +1279,7 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
         for (int cc = 0; cc < 3; ++cc)
             red[cc * BA_THREADS + threadIdx.x] = contrib ? j6[cc] * e0 + j6[3 + cc] * e1 : 0.0;
         __syncthreads();
+        if (kProfWalk) prof_mark(sh, PF_BS_J);
         if ((int)threadIdx.x < g.LC) {
             const int lj = l0 + threadIdx.x;
             if (lj < L) {
@@ -1287,6 +1325,7 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
             }
         }
         __syncthreads();
+        if (kProfWalk) prof_mark(sh, PF_BS_L);
         if (act) {
             double m0 = e0, m1 = e1;
             if (lv) {
@@ -1311,6 +1350,7 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
                 ccost += cst;
             }
         }
+        if (kProfWalk) prof_mark(sh, PF_BS_C);
         cur = nxt;
         lcur = lnxt;
         o_nn = o_n2;
@@ -1550,7 +1590,7 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
     const int K = w.K, L = w.L, N = w.N;
     if (threadIdx.x == 0) {
         sh.prof_on = P.prof != nullptr;
-        for (int i = 0; i < 16; ++i) sh.prof_acc[i] = 0;
+        for (int i = 0; i < PF_NSLOT; ++i) sh.prof_acc[i] = 0;
         sh.prof_last = __builtin_amdgcn_s_memtime();
     }
     __syncthreads();
@@ -1734,7 +1774,7 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
     for (int e = threadIdx.x; e < 6; e += BA_THREADS) out[OL.bias + e] = c.ws[c.L.x_bias + e];
     __syncthreads();
     prof_mark(sh, PF_POST);
-    if (P.prof && threadIdx.x < 16) P.prof[16 * blockIdx.x + threadIdx.x] = sh.prof_acc[threadIdx.x];
+    if (P.prof && threadIdx.x < PF_NSLOT) P.prof[PF_NSLOT * blockIdx.x + threadIdx.x] = sh.prof_acc[threadIdx.x];
 }
 
 size_t ba_shared_bytes() { return sizeof(BaShared); }

@@ -175,10 +175,10 @@ int vio_ba_batch_download(vio_ba_batch* b, vio_ba_output* outs);
 int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count);
 void vio_ba_batch_destroy(vio_ba_batch* b);
 /* diagnostics: per-phase shader-clock accounting of the solver kernel (sum over windows of the
-   last run; 16 slots: setup, eval+J, linearise, step prep, Schur GEMM, Cholesky, back-subst,
-   candidate, eval cost, control, post) */
+   last run; VIO_BA_PROF_SLOTS slots, named in the Python mirror's BaBatch.PHASES) */
 int vio_ba_batch_profile(vio_ba_batch* b, int enable);
-int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out16);
+#define VIO_BA_PROF_SLOTS 24
+int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out /* [VIO_BA_PROF_SLOTS] */);
 
 /* ----------------------------------------------------------------------------------------- */
 /* ERP feature tracking                                                                       */
