@@ -22,6 +22,7 @@
 
 #include "ba_factor_dev.h"
 #include "ba_global.h"
+#include "chol_dev.h"
 #include "lie_dev.h"
 
 namespace vio360 {
@@ -349,53 +350,114 @@ using d4 = __attribute__((ext_vector_type(4))) double;
 // diagonal block: in-LDS right-looking Cholesky + lower-triangular inverse (for TRSM / TRSV).
 // One barrier per column: the trailing update reads the unscaled column j (T[i][c] -= T[i][j] T[c][j] / d)
 // and the column is scaled after the barrier, which the next column's update never touches.
+// Diagonal block k (64x64): L_kk and L_kk^-1, blocked over 16x16 tiles in LDS.  For each tile
+// column J: one wave factors the diagonal tile (chol16_wave), the panel tiles below become
+// L_IJ = S_IJ Linv_J^T and the trailing lower tiles S_IK -= L_IJ L_KJ^T, both on
+// v_mfma_f64_16x16x4_f64, one tile per wave.  The inverse is then built block row by block row,
+// X_IJ = -Linv_II sum_{J<=K<I} L_IK X_KJ, again on MFMA.  Dynamic LDS: CHOL_DIAG_LDS bytes.
+constexpr int TLD = NB + 1;  // odd row stride: the column reads of the MFMA operands spread over banks
+constexpr size_t CHOL_DIAG_LDS = sizeof(double) * (2 * NB * TLD + 4 * 256 + 256 + 4 * 16 * 17);
 __global__ void __launch_bounds__(256) chol_diag_kernel(double* S, int n, int k, double* Linv, int* fail) {
-    __shared__ double T[NB][NB + 1];
-    __shared__ double Iv[NB][NB + 1];
-    __shared__ double rdiag[NB];
+    extern __shared__ double dyn[];
+    double* T = dyn;             // [NB][TLD] S_kk, then L_kk
+    double* X = T + NB * TLD;    // [NB][TLD] L_kk^-1
+    double* LB = X + NB * TLD;   // [4][16 m][16 c] = Linv_J[c][m] of the diagonal tiles
+    double* LT = LB + 4 * 256;   // scratch of chol16_wave
+    double* P = LT + 256;        // [4 waves][16][17] product scratch of the inverse
+    __shared__ int bad_s;
     double* blk = S + (size_t)k * NB * n + (size_t)k * NB;
     for (int e = threadIdx.x; e < NB * NB; e += 256) {
-        int r = e >> 6, c = e & 63;
-        T[r][c] = c <= r ? blk[(size_t)r * n + c] : 0.0;
+        const int r = e >> 6, c = e & 63;
+        T[r * TLD + c] = c <= r ? blk[(size_t)r * n + c] : 0.0;
+        X[r * TLD + c] = 0.0;
     }
     __syncthreads();
-    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
-    bool ok = true;
-    for (int j = 0; j < NB; ++j) {
-        const double d = T[j][j];  // uniform: every thread reads the same LDS word
-        if (!(d > 0.0)) { ok = false; break; }
-        const double id = 1.0 / d;
-        for (int i = j + 1 + ty; i < NB; i += 16) {
-            const double lij = T[i][j] * id;
-            for (int c = j + 1 + tx; c <= i; c += 16) T[i][c] -= lij * T[c][j];
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int r16 = lane & 15, kk = lane >> 4;
+    constexpr int NT = NB / 16;
+    for (int J = 0; J < NT; ++J) {
+        const int c0 = 16 * J;
+        if (wid == 0) {
+            const int bad = chol16_wave<true>(T + c0 * TLD + c0, TLD, LB + 256 * J, LT, lane);
+            if (lane == 0) bad_s = bad;
         }
         __syncthreads();
-        const double sd = sqrt(d), isd = 1.0 / sd;
-        for (int i = j + 1 + threadIdx.x; i < NB; i += 256) T[i][j] *= isd;
-        if (threadIdx.x == 0) { T[j][j] = sd; rdiag[j] = isd; }
+        if (bad_s) {
+            if (threadIdx.x == 0) *fail = 1;
+            return;
+        }
+        const double* lb = LB + 256 * J;
+        for (int I = J + 1 + wid; I < NT; I += 4) {  // panel
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            double* A = T + 16 * I * TLD + c0;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const double a = A[r16 * TLD + 4 * st + kk];
+                const double bb = lb[(4 * st + kk) * 16 + r16];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[(kk + 4 * r) * TLD + r16] = acc[r];
+        }
+        __syncthreads();
+        const int m = NT - J - 1, nt = m * (m + 1) / 2;
+        for (int t = wid; t < nt; t += 4) {  // trailing lower tiles (I, K), J < K <= I
+            int I = 0, tt = t;
+            while (tt > I) { tt -= I + 1; ++I; }
+            const int Kt = tt + J + 1;
+            I += J + 1;
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            const double* Ai = T + 16 * I * TLD + c0;
+            const double* Bk = T + 16 * Kt * TLD + c0;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const double a = Ai[r16 * TLD + 4 * st + kk];
+                const double bb = Bk[r16 * TLD + 4 * st + kk];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+            }
+            double* C = T + 16 * I * TLD + 16 * Kt;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) C[(kk + 4 * r) * TLD + r16] -= acc[r];
+        }
+        __syncthreads();
     }
-    if (!ok) {
-        if (threadIdx.x == 0) *fail = 1;
-        return;
+    for (int e = threadIdx.x; e < NT * 256; e += 256) {  // diagonal tiles of the inverse
+        const int J = e >> 8, q = (e >> 4) & 15, i = e & 15;
+        X[(16 * J + q) * TLD + 16 * J + i] = LB[256 * J + 16 * i + q];
     }
     __syncthreads();
-    // inverse X = T^-1 row by row: X[r][c] = (delta_rc - sum_{c<=q<r} T[r][q] X[q][c]) / T[r][r];
-    // thread = (column c, quarter p) splits the q-sum, two shuffles combine the quarters
-    const int c = threadIdx.x >> 2, p = threadIdx.x & 3;
-    for (int r = 0; r < NB; ++r) {
-        double s = 0.0;
-        if (c < r)
-            for (int q = c + p; q < r; q += 4) s += T[r][q] * Iv[q][c];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        if (p == 0) Iv[r][c] = c > r ? 0.0 : ((r == c ? 1.0 : 0.0) - s) * rdiag[r];
+    for (int I = 1; I < NT; ++I) {
+        if (wid < I) {
+            const int J = wid;
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            for (int K = J; K < I; ++K)
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
+                    const double a = T[(16 * I + r16) * TLD + 16 * K + 4 * st + kk];
+                    const double bb = X[(16 * K + 4 * st + kk) * TLD + 16 * J + r16];
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+                }
+            double* Pw = P + wid * 16 * 17;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Pw[(kk + 4 * r) * 17 + r16] = acc[r];
+            wave_lds_sync();
+            d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const double a = LB[256 * I + (4 * st + kk) * 16 + r16];  // Linv_II[r16][4 st + kk]
+                const double bb = Pw[(4 * st + kk) * 17 + r16];
+                acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc2, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) X[(16 * I + kk + 4 * r) * TLD + 16 * J + r16] = -acc2[r];
+        }
         __syncthreads();
     }
     double* Li = Linv + (size_t)k * NB * NB;
     for (int e = threadIdx.x; e < NB * NB; e += 256) {
-        int r = e >> 6, cc = e & 63;
-        if (cc <= r) blk[(size_t)r * n + cc] = T[r][cc];
-        Li[e] = Iv[r][cc];
+        const int r = e >> 6, c = e & 63;
+        if (c <= r) blk[(size_t)r * n + c] = T[r * TLD + c];
+        Li[e] = X[r * TLD + c];
     }
 }
 
@@ -692,8 +754,12 @@ hipError_t gba_launch_step_prep(const GbaArgs& A, double radius, double* partial
 }
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
+    // > 64 KB of LDS: opt in (per call: the attribute is per device and the call is host-only)
+    const hipError_t ea = hipFuncSetAttribute((const void*)chol_diag_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)CHOL_DIAG_LDS);
+    if (ea != hipSuccess) return ea;
     for (int k = 0; k < nblk; ++k) {
-        hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, s, A.S, n, k, A.Linv, fail);
+        hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv, fail);
         const int m = nblk - k - 1;
         if (m > 0) {
             hipLaunchKernelGGL(chol_trsm_kernel, dim3(m), dim3(256), 0, s, A.S, n, k, (const double*)A.Linv);

@@ -20,6 +20,7 @@
 
 #include "ba_types.h"
 #include "ba_factor_dev.h"
+#include "chol_dev.h"
 #include "lie_dev.h"
 
 namespace vio360 {
@@ -905,29 +906,10 @@ __device__ __forceinline__ void schur_gemm(BaShared& sh, const WinCtx& c) {
 //       LDS and forms the triangular inverse from LDS broadcast reads; Linv_J^T goes to the stage area;
 //   (B) panel tiles L_IJ = S_IJ Linv_J^T on v_mfma_f64_16x16x4_f64, one tile per wave at a time;
 //   (C) trailing lower tiles S_IK -= L_IJ L_KJ^T on the matrix cores.
-// Three workgroup barriers per tile column.  The two triangular solves walk the tile columns with
+// chol16_wave (chol_dev.h) is the wave-level tile factor.  Three workgroup barriers per tile column.  The two triangular solves walk the tile columns with
 // one wave (lanes = 16 rows x 4 column groups; the tile's right-hand side is broadcast through LDS).
 // Fixed operation order: bitwise reproducible.  (tools/probe/chol_probe.hip times the variants.)
 // Returns false (uniformly) when a pivot is not positive (S not positive definite).
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-// 1/sqrt(p) to full double precision: hardware estimate + two Newton-Raphson steps
-__device__ __forceinline__ double rsq_nr(double p) {
-    double r = __builtin_amdgcn_rsq(p);
-    const double h = 0.5 * p;
-    r = r * fma(-h * r, r, 1.5);
-    r = r * fma(-h * r, r, 1.5);
-    return r;
-}
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
     double* S = sh.S;
     double* LB = sh.stage;  // [nb][16 m][16 c] = Linv_J[c][m]
@@ -941,43 +923,7 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
         const int c0 = 16 * J;
         // (A) diagonal tile
         if (wid == 0) {
-            const int i = r16;
-            double d[16], il[16];
-            const double* row = S + (c0 + i) * ls + c0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) d[k] = row[k];  // k > i: upper triangle, never used
-            int bad = 0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const double piv = readlane_d(d[j], j);
-                bad |= !(piv > 0.0);
-                const double r = rsq_nr(piv);
-                il[j] = r;
-                const double cj = i == j ? piv * r : d[j] * r;
-                d[j] = cj;
-#pragma unroll
-                for (int k = j + 1; k < 16; ++k) d[k] -= cj * readlane_d(cj, k);
-            }
-            if (kk == 0) {
-#pragma unroll
-                for (int m = 0; m < 16; ++m) LT[16 * m + i] = d[m];
-            }
-            wave_lds_sync();
-            // column i of Linv (lower): x[q] = Linv[q][i]; L[q][m] read as a broadcast
-            double x[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                double s = q == i ? 1.0 : 0.0;
-#pragma unroll
-                for (int m = 0; m < q; ++m) s -= LT[16 * m + q] * x[m];
-                x[q] = s * il[q];
-            }
-            // LB[m][c] = Linv[c][m]: lane m holds column m of Linv, i.e. Linv[c][m] = x[c]
-            if (kk == 0) {
-                double* dst = LB + 256 * J + 16 * i;
-#pragma unroll
-                for (int q = 0; q < 16; ++q) dst[q] = x[q];
-            }
+            const int bad = chol16_wave<false>(S + c0 * ls + c0, ls, LB + 256 * J, LT, lane);
             if (lane == 0) sh.chol_bad = bad;
         }
         __syncthreads();

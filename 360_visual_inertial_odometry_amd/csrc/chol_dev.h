@@ -1,0 +1,83 @@
+// chol_dev.h — wave-level pieces of the blocked LDS Cholesky shared by the window solver
+// (ba_kernel.hip, reduced camera system <= 96^2) and the global solver's diagonal blocks
+// (ba_global.hip, 64^2 tiles of the config-5 system).  Reduced solve of Ceres' Schur complement
+// (schur_complement_solver.cc:118-356: LLT of S); fixed operation order, no atomics.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace vio360 {
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+// 1/sqrt(p) to full double precision: hardware estimate + two Newton-Raphson steps
+__device__ __forceinline__ double rsq_nr(double p) {
+    double r = __builtin_amdgcn_rsq(p);
+    const double h = 0.5 * p;
+    r = r * fma(-h * r, r, 1.5);
+    r = r * fma(-h * r, r, 1.5);
+    return r;
+}
+
+// LDS writes of this wave visible to its own later reads (no workgroup barrier)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave factors the 16x16 SPD tile A (LDS, row stride ld, lower part read): lane i (mod 16) holds
+// row i, pivots and column entries are broadcast with v_readlane.  Outputs
+//   lbt[16 m + c] = Linv[c][m]   (L^-1 transposed, the B operand of the panel MFMAs)
+//   A            <- L (lower, zeros above) when WRITE_L
+// using lt[256] as scratch.  Returns nonzero (the same on every lane) if a pivot is not positive.
+template <bool WRITE_L>
+__device__ __forceinline__ int chol16_wave(double* A, int ld, double* lbt, double* lt, int lane) {
+    const int i = lane & 15, kk = lane >> 4;
+    double d[16], il[16];
+    const double* row = A + i * ld;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = row[k];  // k > i: upper triangle, never used
+    int bad = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const double piv = readlane_d(d[j], j);
+        bad |= !(piv > 0.0);
+        const double r = rsq_nr(piv);
+        il[j] = r;
+        const double cj = i == j ? piv * r : d[j] * r;
+        d[j] = cj;
+#pragma unroll
+        for (int k = j + 1; k < 16; ++k) d[k] -= cj * readlane_d(cj, k);
+    }
+    if (kk == 0) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) lt[16 * m + i] = d[m];
+    }
+    wave_lds_sync();
+    // column i of Linv (lower): x[q] = Linv[q][i]; L[q][m] read as an LDS broadcast
+    double x[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        double s = q == i ? 1.0 : 0.0;
+#pragma unroll
+        for (int m = 0; m < q; ++m) s -= lt[16 * m + q] * x[m];
+        x[q] = s * il[q];
+    }
+    if (kk == 0) {
+        double* dst = lbt + 16 * i;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) dst[q] = x[q];
+        if (WRITE_L) {
+            double* out = A + i * ld;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) out[m] = m <= i ? d[m] : 0.0;
+        }
+    }
+    return bad;
+}
+
+}  // namespace vio360

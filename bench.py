@@ -28,6 +28,42 @@ sys.path.insert(0, ROOT)
 FP64_PEAK = 78.6e12  # MI355X FP64 vector (= FP64 matrix) peak, AMD spec
 
 
+TRACKER_KERNELS = ("pyr_down_kernel", "lk_kernel", "ransac_prep_kernel", "ransac_hyp_kernel", "ransac_select_kernel",
+                   "gftt_reset_kernel", "gftt_max_kernel", "gftt_hist_kernel", "gftt_cand_kernel",
+                   "gftt_topk_compact_kernel", "gftt_select_kernel<false>", "gftt_select_kernel<true>",
+                   "disc_mask_kernel")
+
+
+def pmc_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/gpu_pmc.sh ->
+    tools/pmc_summary.py -> profiles/r*_pmc_traffic.json; reads corrected x2 for gfx950).  PMC counters
+    cannot be collected inside this process, so the newest committed summary of the same workload is
+    reported (None when absent)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        return json.load(f)["kernels"], os.path.relpath(files[-1], ROOT)
+
+
+def ba_traffic(args):
+    """PMC HBM bytes per ba_window_kernel launch (profiled on the default 256-window x 10-iteration step)."""
+    k, src = pmc_traffic()
+    if not k or "ba_window_kernel" not in k or args.windows != 256 or args.lm_iters != 10:
+        return None
+    return k["ba_window_kernel"]["hbm_bytes_per_launch"]
+
+
+def klt_traffic():
+    """PMC HBM bytes of one ERP-KLT pipeline run: per-launch bytes x launches per run (lk_kernel runs once)."""
+    k, src = pmc_traffic()
+    if not k or "lk_kernel" not in k:
+        return None
+    runs = k["lk_kernel"]["dispatches"]
+    return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items() if n in TRACKER_KERNELS) / runs
+
+
 def ba_flops_per_iter(prob):
     """SURVEY §8(d) counting convention for one LM iteration of one window."""
     K, L, N = prob.K, prob.L, prob.N
@@ -131,8 +167,9 @@ def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
             "peak": 8000.0,
             "unit": "GB/s",
             "frac": alg_bytes / (stage["total"] * 1e-3) / 8.0e12,
-            "traffic": None,
-            "note": "algorithmic 2 B/px (both u8 frames read once) over the whole pipeline's device time",
+            "traffic": klt_traffic(),
+            "note": "algorithmic 2 B/px (both u8 frames read once) over the whole pipeline's device time; "
+                    "traffic = PMC HBM bytes of one pipeline run (all tracker kernels, committed profile)",
         },
         "cpu_baseline": None,
     }
@@ -288,7 +325,7 @@ def main():
                 "peak": FP64_PEAK / 1e12,
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK,
-                "traffic": None,
+                "traffic": ba_traffic(args),
                 "kernel": "ba_window_kernel",
                 "kernel_avg_ms": kms,
                 "kernel_launches": kcount,
