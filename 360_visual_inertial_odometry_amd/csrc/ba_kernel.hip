@@ -1154,7 +1154,7 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
     double* red = sh.S;                    // [3][BA_THREADS] per-lane W^T-terms
     double* dls = sh.S + 3 * BA_THREADS;   // [LC][3] landmark steps of the chunk
     double* cps = sh.S + 6 * BA_THREADS;   // [LC][3] landmark candidates of the chunk
-    // software pipeline: observation index two chunks ahead, lane and slot data one chunk ahead
+    // software pipeline: observation index two chunks ahead, observation data one chunk ahead
     struct ObsD { double a6[6], pb[3], ra, rb; float u, v; int o, lv, out; };
     struct LmD { double sv[3], gv[3], vi[6], x[3]; int lv; };
     auto ld_o = [&](int l0n) -> int {
@@ -1193,18 +1193,18 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
         }
     };
     ObsD cur;
-    LmD lcur;
     int o_nn = ld_o(g.LC);
     ld_obs(0, ld_o(0), cur);
-    ld_lm(0, lcur);
     for (int l0 = 0; l0 < L; l0 += g.LC) {
+        // landmark-lane data of this chunk: issued here, consumed after the first barrier (a prefetch
+        // one chunk ahead would live across the candidate evaluation and spill)
+        LmD lcur;
+        ld_lm(l0, lcur);
         ObsD nxt;
-        LmD lnxt;
-        nxt.o = -1; nxt.lv = 0; lnxt.lv = 0;
+        nxt.o = -1; nxt.lv = 0;
         int o_n2 = -1;
         if (l0 + g.LC < L) {
             ld_obs(l0 + g.LC, o_nn, nxt);
-            ld_lm(l0 + g.LC, lnxt);
             o_n2 = ld_o(l0 + 2 * g.LC);
         }
         const bool lv = cur.o >= 0 && cur.lv;
@@ -1298,7 +1298,6 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
         }
         if (kProfWalk) prof_mark(sh, PF_BS_C);
         cur = nxt;
-        lcur = lnxt;
         o_nn = o_n2;
     }
     for (int f = threadIdx.x; f < nf; f += BA_THREADS)
