@@ -10,11 +10,13 @@
 //                        every 22x22 next-frame tile live in LDS; gradient/mismatch sums are exact
 //                        int64 wave reductions.
 //   ransac_*             RejectOutliersRotationRANSAC: one wavefront per hypothesis.
-//   gftt_*               cv::goodFeaturesToTrack(blockSize 3, Sobel 3): the min-eigenvalue map is
-//                        never written to HBM — pass 1 reduces its masked maximum, pass 2
-//                        recomputes it on a haloed LDS tile, applies THRESH_TOZERO + 3x3 dilate
-//                        NMS + mask and appends (response, address) keys; a radix sort and one
-//                        workgroup's greedy min-distance pass finish.
+//   gftt_*               cv::goodFeaturesToTrack(blockSize 3, Sobel 3): pass 1 computes the
+//                        min-eigenvalue map on LDS tiles (Sobel, 3x3 box, eigenvalue), writes it
+//                        (f32, W x H) and reduces its masked maximum; pass 2 reads a haloed tile of
+//                        the map back, applies THRESH_TOZERO + 3x3 dilate NMS + mask and appends
+//                        (response, address) keys; a top-K histogram cut, a sort and one
+//                        workgroup's greedy min-distance pass finish.  (Recomputing the map in
+//                        pass 2 cost more than its 2 x 4 B/px round trip through HBM / MALL.)
 // Float expressions follow tracker_oracle.c literally and the file is built with
 // -ffp-contract=off, so results are bitwise those of the oracle.
 #include <float.h>
@@ -67,6 +69,7 @@ __global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLeve
 // LK.  One wavefront per point.
 constexpr int LK_WAVES = 4;
 constexpr int LK_WIN_MAX = 21;
+constexpr int LK_NIT = (LK_WIN_MAX * LK_WIN_MAX + 63) / 64;  // patch pixels per lane
 constexpr int LK_T = LK_WIN_MAX + 3;  // prev tile (patch + 1 bilinear + 1 Scharr each side)
 constexpr int LK_D = LK_WIN_MAX + 1;  // derivative / next tile
 
@@ -77,14 +80,29 @@ struct LkShared {
     uint8_t Jr[LK_R * LK_R];                 // next-frame region (reflect-101 values), origin (rx0, ry0)
     uint8_t It[LK_T * LK_T];
     int16_t dx[LK_D * LK_D], dy[LK_D * LK_D];
-    int16_t Iw[LK_WIN_MAX * LK_WIN_MAX];
-    int16_t dIx[LK_WIN_MAX * LK_WIN_MAX], dIy[LK_WIN_MAX * LK_WIN_MAX];
 };
 
+// Wave sum of integer partials, exact while |sum| < 2^53: the partials are summed as doubles
+// (integer-valued, so every order gives the same exact value) with DPP row reductions (xor 1, xor 2,
+// half-row mirror, row mirror: VALU lane moves, no LDS crossbar) and the four row totals read out.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
 __device__ __forceinline__ long long wave_sum_i64(long long v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    double d = (double)v;
+    d += dpp_d<0xB1>(d);   // quad_perm [1,0,3,2]
+    d += dpp_d<0x4E>(d);   // quad_perm [2,3,0,1]
+    d += dpp_d<0x141>(d);  // row_half_mirror
+    d += dpp_d<0x140>(d);  // row_mirror: every lane holds its row's sum
+    return (long long)(((lane_d(d, 0) + lane_d(d, 16)) + lane_d(d, 32)) + lane_d(d, 48));
 }
 
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
@@ -177,20 +195,32 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
         float a = px - ipx, b = py - ipy;
         int w00, w01, w10, w11;
         lk_weights(a, b, w00, w01, w10, w11);
+        // the lane's patch pixels e = lane + 64 it: interpolated I and derivatives stay in registers
+        // for all iterations of the level; joff = offset of the pixel in the next-frame window (-1: none)
+        int joff[LK_NIT], iwv[LK_NIT], ixr[LK_NIT], iyr[LK_NIT];
         int sA11 = 0, sA12 = 0, sA22 = 0;  // per-lane partials fit int32 (<= 7 terms < 2^26 each)
-        for (int e = lane; e < np; e += 64) {
-            int y = e / win, x = e % win;
-            const uint8_t* t = &S.It[(y + 1) * T + x + 1];
-            int ival = DESCALE(t[0] * w00 + t[1] * w01 + t[T] * w10 + t[T + 1] * w11, 9);
-            int q = y * D + x;
-            int ixv = DESCALE(S.dx[q] * w00 + S.dx[q + 1] * w01 + S.dx[q + D] * w10 + S.dx[q + D + 1] * w11, 14);
-            int iyv = DESCALE(S.dy[q] * w00 + S.dy[q + 1] * w01 + S.dy[q + D] * w10 + S.dy[q + D + 1] * w11, 14);
-            S.Iw[e] = (int16_t)ival;
-            S.dIx[e] = (int16_t)ixv;
-            S.dIy[e] = (int16_t)iyv;
-            sA11 += ixv * ixv;
-            sA12 += ixv * iyv;
-            sA22 += iyv * iyv;
+#pragma unroll
+        for (int it = 0; it < LK_NIT; ++it) {
+            const int e = lane + 64 * it;
+            joff[it] = -1;
+            iwv[it] = ixr[it] = iyr[it] = 0;
+            if (e < np) {
+                const int y = e / win, x = e - (e / win) * win;
+                const uint8_t* t = &S.It[(y + 1) * T + x + 1];
+                const int ival = DESCALE(t[0] * w00 + t[1] * w01 + t[T] * w10 + t[T + 1] * w11, 9);
+                const int q = y * D + x;
+                const int ixv =
+                    DESCALE(S.dx[q] * w00 + S.dx[q + 1] * w01 + S.dx[q + D] * w10 + S.dx[q + D + 1] * w11, 14);
+                const int iyv =
+                    DESCALE(S.dy[q] * w00 + S.dy[q + 1] * w01 + S.dy[q + D] * w10 + S.dy[q + D + 1] * w11, 14);
+                iwv[it] = (int16_t)ival;
+                ixr[it] = (int16_t)ixv;
+                iyr[it] = (int16_t)iyv;
+                joff[it] = y * LK_R + x;
+                sA11 += ixv * ixv;
+                sA12 += ixv * iyv;
+                sA22 += iyv * iyv;
+            }
         }
         const long long tA11 = wave_sum_i64(sA11), tA12 = wave_sum_i64(sA12), tA22 = wave_sum_i64(sA22);
         const float A11 = (float)tA11 * FLT_SCALE, A12 = (float)tA12 * FLT_SCALE, A22 = (float)tA22 * FLT_SCALE;
@@ -215,12 +245,14 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
             lk_region(S.Jr, rx0, ry0, J, w, h, Lv.pitch, inx, iny, win, lane);
             const uint8_t* Jw = S.Jr + (iny - ry0) * LK_R + (inx - rx0);
             int ib1 = 0, ib2 = 0;  // per-lane partials fit int32 (<= 7 terms < 2^26 each)
-            for (int e = lane; e < np; e += 64) {
-                int y = e / win, x = e % win;
-                const uint8_t* t = &Jw[y * LK_R + x];
-                int diff = DESCALE(t[0] * w00 + t[1] * w01 + t[LK_R] * w10 + t[LK_R + 1] * w11, 9) - S.Iw[e];
-                ib1 += diff * S.dIx[e];
-                ib2 += diff * S.dIy[e];
+#pragma unroll
+            for (int it = 0; it < LK_NIT; ++it) {
+                if (joff[it] >= 0) {
+                    const uint8_t* t = Jw + joff[it];
+                    const int diff = DESCALE(t[0] * w00 + t[1] * w01 + t[LK_R] * w10 + t[LK_R + 1] * w11, 9) - iwv[it];
+                    ib1 += diff * ixr[it];
+                    ib2 += diff * iyr[it];
+                }
             }
             const float b1 = (float)wave_sum_i64(ib1) * FLT_SCALE, b2 = (float)wave_sum_i64(ib2) * FLT_SCALE;
             const float ddx = (A12 * b2 - A22 * b1) * Dt;
@@ -245,11 +277,14 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
                 lk_region(S.Jr, rx0, ry0, J, w, h, Lv.pitch, ix, iy, win, lane);
                 const uint8_t* Jw = S.Jr + (iy - ry0) * LK_R + (ix - rx0);
                 long long es = 0;
-                for (int e = lane; e < np; e += 64) {
-                    int y = e / win, x = e % win;
-                    const uint8_t* t = &Jw[y * LK_R + x];
-                    int diff = DESCALE(t[0] * w00 + t[1] * w01 + t[LK_R] * w10 + t[LK_R + 1] * w11, 9) - S.Iw[e];
-                    es += diff < 0 ? -diff : diff;
+#pragma unroll
+                for (int it = 0; it < LK_NIT; ++it) {
+                    if (joff[it] >= 0) {
+                        const uint8_t* t = Jw + joff[it];
+                        const int diff =
+                            DESCALE(t[0] * w00 + t[1] * w01 + t[LK_R] * w10 + t[LK_R + 1] * w11, 9) - iwv[it];
+                        es += diff < 0 ? -diff : diff;
+                    }
                 }
                 es = wave_sum_i64(es);
                 err = (float)es * (1.f / (32 * win * win));
@@ -699,9 +734,25 @@ __device__ void gf_eig_tile(const GfArgs& G, int ex0, int ey0, uint8_t (*src)[Gf
     }
     __syncthreads();
     const float scale = (float)(1.0 / 3060.0);
+    // interior tile: every Sobel neighbour of every cov position is inside the image, no reflection
+    const bool interior = sx0 >= 0 && sy0 >= 0 && sx0 + T::SW <= W && sy0 + T::SH <= H;
     // cov at positions (ex0-1+cx, ey0-1+cy): Sobel of reflect101 neighbours.  The tile holds
     // source rows/cols sy0.. with reflect applied per coordinate, so for a cov position p the
     // neighbours p±1 must be reflected relative to the image, not the tile: re-derive them.
+    if (interior) {
+        for (int e = threadIdx.x; e < T::CW * T::CH; e += 256) {
+            const int cy = e / T::CW, cx = e % T::CW;
+            const uint8_t* r0 = src[cy];
+            const uint8_t* r1 = src[cy + 1];
+            const uint8_t* r2 = src[cy + 2];
+            const int sx = (r0[cx + 2] - r0[cx]) + 2 * (r1[cx + 2] - r1[cx]) + (r2[cx + 2] - r2[cx]);
+            const int sy = (r2[cx] + 2 * r2[cx + 1] + r2[cx + 2]) - (r0[cx] + 2 * r0[cx + 1] + r0[cx + 2]);
+            const float dx = (float)sx * scale, dy = (float)sy * scale;
+            cov[cy][cx][0] = dx * dx;
+            cov[cy][cx][1] = dx * dy;
+            cov[cy][cx][2] = dy * dy;
+        }
+    } else
     for (int e = threadIdx.x; e < T::CW * T::CH; e += 256) {
         int cy = e / T::CW, cx = e % T::CW;
         int X = reflect101(ex0 - 1 + cx, W), Y = reflect101(ey0 - 1 + cy, H);
@@ -762,41 +813,63 @@ __device__ void gf_eig_tile(const GfArgs& G, int ex0, int ey0, uint8_t (*src)[Gf
     __syncthreads();
 }
 
-// Each workgroup walks GF_SUB tiles down the image (fewer, longer-lived workgroups; one global
-// atomic per workgroup instead of one per tile / wave).
+// Pass 1a: the min-eigenvalue map, independent of the mask (so it can run concurrently with LK /
+// RANSAC / the disc mask).  Each workgroup walks GF_SUB tiles down the image.
 constexpr int GF_SUB = 4;
-__global__ void __launch_bounds__(256) gftt_max_kernel(GfArgs G) {
+__global__ void __launch_bounds__(256) gftt_eig_kernel(GfArgs G) {
     using T = GfTile<2>;
     __shared__ uint8_t src[T::SH][T::SW + 4];
     __shared__ float cov[T::CH][T::CW][3];
     __shared__ float eig[T::EH][T::EW];
-    __shared__ uint32_t red[4];
-    uint32_t m = 0;  // ord(-inf-ish): any value beats 0
     for (int sub = 0; sub < GF_SUB; ++sub) {
         const int ex0 = blockIdx.x * GF_BX, ey0 = (blockIdx.y * GF_SUB + sub) * GF_BY;
         if (ey0 >= G.H) break;
         gf_eig_tile<2>(G, ex0, ey0, src, cov, eig);
         for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
-            int ey = e / T::EW, ex = e % T::EW;
-            int X = ex0 + ex, Y = ey0 + ey;
-            if (X < G.W && Y < G.H && gf_masked_in(G, X, Y)) m = max(m, ord_f32(eig[ey][ex]));
+            const int ey = e / T::EW, ex = e % T::EW;
+            const int X = ex0 + ex, Y = ey0 + ey;
+            if (X < G.W && Y < G.H) G.eig[(size_t)Y * G.W + X] = eig[ey][ex];
         }
         __syncthreads();  // eig / src are rewritten by the next tile
+    }
+}
+
+// Pass 1b: masked maximum of the map (minMaxLoc over the mask), streamed row by row; rows the
+// analytic polar mask removes are skipped.  One global atomic per workgroup.
+constexpr int GM_BLOCKS = 1024;
+__global__ void __launch_bounds__(256) gftt_max_kernel(GfArgs G) {
+    __shared__ uint32_t red[4];
+    uint32_t m = 0;  // ord(-inf-ish): any value beats 0
+    constexpr int U = 8;  // loads in flight per lane
+    for (int y = blockIdx.x; y < G.H; y += gridDim.x) {
+        if (!G.mask && (y < G.top_rows || y >= G.bottom_start)) continue;
+        const float* row = G.eig + (size_t)y * G.W;
+        for (int x0 = threadIdx.x; x0 < G.W; x0 += 256 * U) {
+            float v[U];
+            bool in[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int x = x0 + 256 * u;
+                in[u] = x < G.W && gf_masked_in(G, x, y);
+                v[u] = x < G.W ? row[x] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (in[u]) m = max(m, ord_f32(v[u]));
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t = max(max(red[0], red[1]), max(red[2], red[3]));
+        const uint32_t t = max(max(red[0], red[1]), max(red[2], red[3]));
         if (t) atomicMax(G.max_ord, t);
     }
 }
 
 __global__ void __launch_bounds__(256) gftt_cand_kernel(GfArgs G) {
-    using T = GfTile<3>;
-    __shared__ uint8_t src[T::SH][T::SW + 4];
-    __shared__ float cov[T::CH][T::CW][3];
+    using T = GfTile<3>;  // eig positions of the tile with a 1-pixel halo
     __shared__ float eig[T::EH][T::EW];
     __shared__ unsigned long long keys[GF_SUB * GF_BX * GF_BY];
     __shared__ unsigned int s_cnt, s_base;
@@ -809,10 +882,13 @@ __global__ void __launch_bounds__(256) gftt_cand_kernel(GfArgs G) {
     for (int sub = 0; sub < GF_SUB; ++sub) {
         const int ox = blockIdx.x * GF_BX, oy = (blockIdx.y * GF_SUB + sub) * GF_BY;
         if (oy >= G.H) break;
-        gf_eig_tile<3>(G, ox - 1, oy - 1, src, cov, eig);
+        // the map of pass 1 (positions outside the image read as 0: the dilation ignores them),
+        // thresholded to zero
         for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
-            int ey = e / T::EW, ex = e % T::EW;
-            if (!(eig[ey][ex] > thr)) eig[ey][ex] = 0.f;
+            const int ey = e / T::EW, ex = e % T::EW;
+            const int X = ox - 1 + ex, Y = oy - 1 + ey;
+            const float v = (X >= 0 && Y >= 0 && X < G.W && Y < G.H) ? G.eig[(size_t)Y * G.W + X] : 0.f;
+            eig[ey][ex] = v > thr ? v : 0.f;
         }
         __syncthreads();
         for (int e = threadIdx.x; e < GF_BX * GF_BY; e += 256) {
@@ -1229,9 +1305,15 @@ hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st) {
     hipLaunchKernelGGL(disc_mask_kernel, dim3(max_pts), dim3(128), 0, st, d);
     return hipGetLastError();
 }
+hipError_t launch_gftt_eig(const GfArgs& g, hipStream_t st) {
+    dim3 grd((g.W + GF_BX - 1) / GF_BX, (g.H + GF_BY * GF_SUB - 1) / (GF_BY * GF_SUB));
+    hipLaunchKernelGGL(gftt_eig_kernel, grd, dim3(256), 0, st, g);
+    return hipGetLastError();
+}
+// after the map (launch_gftt_eig, on this stream or joined into it): masked max, then candidates
 static hipError_t gftt_candidates(const GfArgs& g, hipStream_t st) {
     dim3 grd((g.W + GF_BX - 1) / GF_BX, (g.H + GF_BY * GF_SUB - 1) / (GF_BY * GF_SUB));
-    hipLaunchKernelGGL(gftt_max_kernel, grd, dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gftt_max_kernel, dim3(GM_BLOCKS), dim3(256), 0, st, g);
     hipLaunchKernelGGL(gftt_cand_kernel, grd, dim3(256), 0, st, g);
     return hipGetLastError();
 }
@@ -1275,7 +1357,7 @@ hipError_t launch_gftt_full(const GfArgs& g, unsigned int count, void* sort_tmp,
 }
 size_t gftt_sort_tmp_bytes(unsigned int cap) {
     size_t tb = 0;
-    hipcub::DeviceRadixSort::SortKeysDescending((void*)nullptr, tb, (unsigned long long*)nullptr,
+    (void)hipcub::DeviceRadixSort::SortKeysDescending((void*)nullptr, tb, (unsigned long long*)nullptr,
                                                 (unsigned long long*)nullptr, (int)cap, 0, 64, (hipStream_t)0);
     return tb;
 }

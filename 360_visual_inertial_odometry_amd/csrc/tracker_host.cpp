@@ -63,6 +63,7 @@ struct erp_tracker {
     int* d_scal = nullptr;
     // gftt
     unsigned long long *d_cand = nullptr, *d_cand_sorted = nullptr;
+    float* d_eig = nullptr;     // GFTT min-eigenvalue map (W x H f32)
     unsigned int cand_cap = 0;
     void* d_sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
@@ -80,6 +81,9 @@ struct erp_tracker {
     unsigned int topk_cap = 0;
     GfArgs last_gf{};           // arguments of the last enqueued GFTT (exact fallback)
     hipEvent_t ev[6] = {};
+    // the GFTT eigenvalue map runs on a side stream, overlapped with pyramids / LK / RANSAC
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     bool ran = false;
     std::vector<void*> allocs;
 };
@@ -103,6 +107,9 @@ void tracker_free(erp_tracker* t) {
     t->allocs.clear();
     for (auto& e : t->ev)
         if (e) (void)hipEventDestroy(e);
+    if (t->side) (void)hipStreamDestroy(t->side);
+    if (t->fork) (void)hipEventDestroy(t->fork);
+    if (t->join) (void)hipEventDestroy(t->join);
 }
 
 int ensure_iters(erp_tracker* t, int iters) {
@@ -122,6 +129,7 @@ int ensure_gftt(erp_tracker* t, double min_dist) {
         // NMS leaves at most one candidate per 2x2 block except on exact plateaus; W*H/4 (+slack)
         t->cand_cap = (unsigned int)std::min<size_t>((size_t)t->W * t->H / 4 + 4096, (size_t)1 << 26);
         if ((rc = dalloc(t, &t->d_cand, sizeof(unsigned long long) * t->cand_cap)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_eig, sizeof(float) * (size_t)t->W * t->H)) != VIO_OK) return rc;
         if ((rc = dalloc(t, &t->d_cand_sorted, sizeof(unsigned long long) * t->cand_cap)) != VIO_OK) return rc;
         t->sort_tmp_bytes = gftt_sort_tmp_bytes(t->cand_cap);
         if ((rc = dalloc(t, (char**)&t->d_sort_tmp, t->sort_tmp_bytes)) != VIO_OK) return rc;
@@ -171,6 +179,10 @@ int tracker_alloc(erp_tracker* t) {
     if ((rc = ensure_iters(t, 1024))) return rc;
     for (auto& e : t->ev)
         if (hipEventCreate(&e) != hipSuccess) return hip_fail(t->ctx, hipErrorUnknown, "hipEventCreate");
+    if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&t->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess)
+        return hip_fail(t->ctx, hipErrorUnknown, "side stream / events");
     return VIO_OK;
 }
 
@@ -243,8 +255,18 @@ RansacArgs ransac_args(erp_tracker* t, int n, int mode, int iters, uint32_t seed
     return r;
 }
 
+// GFTT arguments for the eigenvalue-map pass only
+GfArgs gf_map_args(const erp_tracker* t, const uint8_t* img, int pitch) {
+    GfArgs g;
+    std::memset(&g, 0, sizeof g);
+    g.img = img; g.W = t->W; g.H = t->H; g.pitch = pitch;
+    g.eig = t->d_eig;
+    return g;
+}
+
+// eig_ready: the map of `img` was already produced (launch_gftt_eig joined into the context stream)
 int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* mask, int mask_pitch, int max_corners,
-                 double quality, double min_dist, bool discs, int margin, float polar) {
+                 double quality, double min_dist, bool discs, int margin, float polar, bool eig_ready = false) {
     int rc = ensure_gftt(t, min_dist);
     if (rc) return rc;
     GfArgs g;
@@ -259,6 +281,7 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     g.disc_words = t->disc_words;
     g.quality = quality; g.min_dist = min_dist; g.max_corners = max_corners;
     g.max_ord = (uint32_t*)(t->d_scal + 2);
+    g.eig = t->d_eig;
     g.cand = t->d_cand; g.cand_sorted = t->d_cand_sorted;
     g.n_cand = (unsigned int*)(t->d_scal + 3);
     g.cand_cap = t->cand_cap;
@@ -286,6 +309,7 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     // scalars [2] max_ord [3] n_cand [4] n_out [6] n_top [7..8] cut [9] incomplete
     t->last_gf = g;
     hipError_t e = launch_gftt_reset(g, t->d_scal, t->ctx->stream);
+    if (e == hipSuccess && !eig_ready) e = launch_gftt_eig(g, t->ctx->stream);
     if (e == hipSuccess) e = launch_gftt(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
     if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt kernels");
     return VIO_OK;
@@ -398,9 +422,18 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         return VIO_EINVAL;
     }
     if ((rc = ensure_iters(t, std::max(p->ransac_iters, 1)))) return rc;
+    if ((rc = ensure_gftt(t, p->min_dist))) return rc;
     hipStream_t st = t->ctx->stream;
     const int n = t->n_pts;
     VIO_HIP(t->ctx, hipEventRecord(t->ev[0], st));
+    // the eigenvalue map of the current frame does not depend on tracking: side stream
+    VIO_HIP(t->ctx, hipEventRecord(t->fork, st));
+    VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->fork, 0));
+    {
+        hipError_t e = launch_gftt_eig(gf_map_args(t, t->lvl[1][0], t->lp[0]), t->side);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_eig_kernel");
+    }
+    VIO_HIP(t->ctx, hipEventRecord(t->join, t->side));
     if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK
     VIO_HIP(t->ctx, hipEventRecord(t->ev[2], st));
     RansacArgs r = ransac_args(t, n, 1, p->ransac_iters, p->ransac_seed, p->ransac_thresh_rad, p->polar_ratio,
@@ -427,8 +460,9 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         hipError_t e = launch_disc_mask(d, n, st);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "disc_mask_kernel");
     }
+    VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->join, 0));
     if ((rc = enqueue_gftt(t, t->lvl[1][0], t->lp[0], nullptr, 0, p->max_corners, p->quality, p->min_dist, true,
-                           p->boundary_margin, p->polar_ratio)))
+                           p->boundary_margin, p->polar_ratio, true)))
         return rc;
     VIO_HIP(t->ctx, hipEventRecord(t->ev[4], st));
     t->ran = true;

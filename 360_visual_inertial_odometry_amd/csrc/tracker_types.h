@@ -64,6 +64,7 @@ struct GfArgs {
     double quality, min_dist;
     int max_corners;
     uint32_t* max_ord;              // device scalar (ordered-int max of the masked eig map)
+    float* eig;                     // [H][W] min-eigenvalue map, written by pass 1, read by pass 2
     unsigned long long* cand;       // [cand_cap]
     unsigned long long* cand_sorted;
     unsigned int* n_cand;           // device scalar
@@ -100,7 +101,8 @@ hipError_t launch_lk(const LkArgs& a, hipStream_t st);
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st);
 hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st);
 // fast path (top-K) and the exact fallback over every candidate (used when `incomplete` is raised)
-hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st);
+hipError_t launch_gftt_eig(const GfArgs& g, hipStream_t st);  // the min-eigenvalue map (needs img, W, H, pitch, eig)
+hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st);  // after the map
 hipError_t launch_gftt_full(const GfArgs& g, unsigned int count, void* sort_tmp, size_t sort_tmp_bytes,
                             hipStream_t st);  // sorts the first `count` candidates (n_cand read back)
 hipError_t launch_gftt_reset(const GfArgs& g, int* scal, hipStream_t st);
