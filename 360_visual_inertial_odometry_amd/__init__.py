@@ -6,6 +6,7 @@ a GPU is missing every entry point raises.
 """
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
@@ -93,6 +94,7 @@ class Context:
         if rc != 0:
             raise VioError(f"vio_ctx_create failed ({rc}): {L.vio_ctx_last_error(None).decode()}")
         self.h = h
+        self._children = weakref.WeakSet()  # batches / trackers: closed before the context
 
     def check(self, rc, what):
         if rc != 0:
@@ -100,6 +102,11 @@ class Context:
 
     def close(self):
         if self.h:
+            for ch in list(self._children):  # the C-ABI requires children to go first
+                try:
+                    ch.close()
+                except Exception:
+                    pass
             lib().vio_ctx_destroy(self.h)
             self.h = None
 
@@ -192,6 +199,7 @@ class Tracker:
         h = C.c_void_p()
         ctx.check(lib().erp_tracker_create(ctx.h, W, H, max_points, max_corners, C.byref(h)), "erp_tracker_create")
         self.h = h
+        ctx._children.add(self)
         self.n = 0
 
     def upload(self, slot, img):
@@ -252,6 +260,7 @@ class Frontend:
         self.params = params or default_frontend_params()
         ctx.check(lib().erp_frontend_create(ctx.h, W, H, C.byref(self.params), C.byref(h)), "erp_frontend_create")
         self.h = h
+        ctx._children.add(self)
 
     def track(self, img):
         img = _u8img(img)
@@ -290,6 +299,7 @@ class BaBatch:
         h = C.c_void_p()
         ctx.check(lib().vio_ba_batch_create(ctx.h, self._P, n, C.byref(h)), "vio_ba_batch_create")
         self.h = h
+        ctx._children.add(self)
 
     def run(self):
         self.ctx.check(lib().vio_ba_batch_run(self.h), "vio_ba_batch_run")

@@ -60,7 +60,7 @@ struct BaPools {
     uint8_t* out_bad;            // [sum L] SetBad decisions
     int32_t* out_i32;            // per-window summary ints [n][8]
     double* out_sum;             // per-window summary doubles [n][4]
-    unsigned long long* prof;    // optional [n][16] per-phase shader clocks (diagnostics), may be null
+    unsigned long long* prof;    // optional [n][VIO_BA_PROF_SLOTS] per-phase shader clocks (diagnostics), may be null
     int route;                   // 0: ba_window_kernel solves every window; 1: it solves the PnP windows
                                  // only and the phase kernels (ba_phases.inc) the others
 };

@@ -48,6 +48,7 @@ extern "C" {
 typedef struct vio_ctx vio_ctx;
 
 int vio_ctx_create(int device, vio_ctx** out);
+/* destroy every batch / tracker / front-end created on the context first: they use its stream */
 void vio_ctx_destroy(vio_ctx* ctx);
 /* last error message of this context (or of the last failed vio_ctx_create when ctx==NULL) */
 const char* vio_ctx_last_error(const vio_ctx* ctx);

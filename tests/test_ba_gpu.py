@@ -145,6 +145,21 @@ def test_batched_equals_single_bitwise(vio, synth, gpu_ctx):
         assert batch[i]["final_cost"] == solo["final_cost"]
 
 
+def test_routes_agree(vio, synth, gpu_ctx):
+    """Batches above the phase-route size (32 non-PnP windows) run in the single-kernel solver, whose
+    fixed summation orders differ from the phase kernels': the same window agrees with its solo
+    (phase-route) result to roundoff."""
+    ws = [synth.config3(synth.SEED + i) for i in range(40)]
+    probs = [vio.BaProblem(w, variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1) for w in ws]
+    big = gpu_ctx.ba_solve(probs)
+    for i in (0, 17, 39):
+        solo = gpu_ctx.ba_solve([probs[i]])[0]
+        assert big[i]["iterations"] == solo["iterations"]
+        assert np.abs(big[i]["T_wb"] - solo["T_wb"]).max() <= 1e-7
+        assert np.abs(big[i]["lm_xyz"] - solo["lm_xyz"]).max() <= 1e-6
+        assert abs(big[i]["final_cost"] - solo["final_cost"]) <= 1e-8 * solo["final_cost"]
+
+
 def test_mixed_variant_batch(vio, gpu_ctx, all_cases):
     """One launch may mix variants and sizes (LocalBA, BA, VIBA, PnP)."""
     probs = [vio.BaProblem(w, variant=v) for _, w, v in all_cases]
