@@ -124,9 +124,20 @@ __device__ __forceinline__ void lk_region(uint8_t* Jr, int& rx0, int& ry0, const
     rx0 = ix - LK_MARGIN;
     ry0 = iy - LK_MARGIN;
     __builtin_amdgcn_wave_barrier();
-    for (int e = lane; e < LK_R * LK_R; e += 64) {
+    // every global load of the region is issued before the first LDS store (one memory round trip
+    // instead of one per 64 pixels)
+    constexpr int NR = (LK_R * LK_R + 63) / 64;
+    uint32_t v[NR];
+#pragma unroll
+    for (int it = 0; it < NR; ++it) {
+        const int e = lane + 64 * it;
         const int ty = e / LK_R, tx = e - ty * LK_R;
-        Jr[e] = J[(size_t)reflect101(ry0 + ty, h) * pitch + reflect101(rx0 + tx, w)];
+        v[it] = e < LK_R * LK_R ? J[(size_t)reflect101(ry0 + ty, h) * pitch + reflect101(rx0 + tx, w)] : 0u;
+    }
+#pragma unroll
+    for (int it = 0; it < NR; ++it) {
+        const int e = lane + 64 * it;
+        if (e < LK_R * LK_R) Jr[e] = (uint8_t)v[it];
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -166,9 +177,20 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
         }
         // stage the prev tile: rows ipy-1 .. ipy+win+1, cols ipx-1 .. ipx+win+1
         const int T = win + 3;
-        for (int e = lane; e < T * T; e += 64) {
-            int ty = e / T, tx = e % T;
-            S.It[e] = I[(size_t)reflect101(ipy - 1 + ty, h) * Lv.pitch + reflect101(ipx - 1 + tx, w)];
+        {
+            constexpr int NT = (LK_T * LK_T + 63) / 64;  // loads first, then the LDS stores
+            uint32_t v[NT];
+#pragma unroll
+            for (int it = 0; it < NT; ++it) {
+                const int e = lane + 64 * it;
+                const int ty = e / T, tx = e - (e / T) * T;
+                v[it] = e < T * T ? I[(size_t)reflect101(ipy - 1 + ty, h) * Lv.pitch + reflect101(ipx - 1 + tx, w)] : 0u;
+            }
+#pragma unroll
+            for (int it = 0; it < NT; ++it) {
+                const int e = lane + 64 * it;
+                if (e < T * T) S.It[e] = (uint8_t)v[it];
+            }
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
