@@ -750,9 +750,20 @@ __device__ void gf_eig_tile(const GfArgs& G, int ex0, int ey0, uint8_t (*src)[Gf
     using T = GfTile<HALO>;
     const int W = G.W, H = G.H;
     const int sx0 = ex0 - 2, sy0 = ey0 - 2;
-    for (int e = threadIdx.x; e < T::SW * T::SH; e += 256) {
-        int ty = e / T::SW, tx = e % T::SW;
-        src[ty][tx] = G.img[(size_t)reflect101(sy0 + ty, H) * G.pitch + reflect101(sx0 + tx, W)];
+    {
+        constexpr int NS = (T::SW * T::SH + 255) / 256;  // loads first, then the LDS stores
+        uint32_t v[NS];
+#pragma unroll
+        for (int it = 0; it < NS; ++it) {
+            const int e = threadIdx.x + 256 * it;
+            const int ty = e / T::SW, tx = e % T::SW;
+            v[it] = e < T::SW * T::SH ? G.img[(size_t)reflect101(sy0 + ty, H) * G.pitch + reflect101(sx0 + tx, W)] : 0u;
+        }
+#pragma unroll
+        for (int it = 0; it < NS; ++it) {
+            const int e = threadIdx.x + 256 * it;
+            if (e < T::SW * T::SH) src[e / T::SW][e % T::SW] = (uint8_t)v[it];
+        }
     }
     __syncthreads();
     const float scale = (float)(1.0 / 3060.0);
@@ -901,16 +912,31 @@ __global__ void __launch_bounds__(256) gftt_cand_kernel(GfArgs G) {
     double maxv = mo ? (double)unord_f32(mo) : 0.0;  // minMaxLoc over the mask, 0 when empty
     if (maxv < 0.0) maxv = 0.0;
     const float thr = (float)(maxv * G.quality);
+    // the map of pass 1 for all GF_SUB haloed sub-tiles, every load issued up front (positions
+    // outside the image read as 0: the dilation ignores them)
+    constexpr int NE = (T::EW * T::EH + 255) / 256;
+    float vmap[GF_SUB][NE];
+#pragma unroll
+    for (int sub = 0; sub < GF_SUB; ++sub)
+#pragma unroll
+        for (int it = 0; it < NE; ++it) {
+            const int e = threadIdx.x + 256 * it;
+            const int ey = e / T::EW, ex = e % T::EW;
+            const int X = blockIdx.x * GF_BX - 1 + ex, Y = (blockIdx.y * GF_SUB + sub) * GF_BY - 1 + ey;
+            vmap[sub][it] = (e < T::EW * T::EH && X >= 0 && Y >= 0 && X < G.W && Y < G.H)
+                                ? G.eig[(size_t)Y * G.W + X] : 0.f;
+        }
     for (int sub = 0; sub < GF_SUB; ++sub) {
         const int ox = blockIdx.x * GF_BX, oy = (blockIdx.y * GF_SUB + sub) * GF_BY;
         if (oy >= G.H) break;
-        // the map of pass 1 (positions outside the image read as 0: the dilation ignores them),
-        // thresholded to zero
-        for (int e = threadIdx.x; e < T::EW * T::EH; e += 256) {
-            const int ey = e / T::EW, ex = e % T::EW;
-            const int X = ox - 1 + ex, Y = oy - 1 + ey;
-            const float v = (X >= 0 && Y >= 0 && X < G.W && Y < G.H) ? G.eig[(size_t)Y * G.W + X] : 0.f;
-            eig[ey][ex] = v > thr ? v : 0.f;
+        // thresholded to zero (THRESH_TOZERO)
+#pragma unroll
+        for (int it = 0; it < NE; ++it) {
+            const int e = threadIdx.x + 256 * it;
+            if (e < T::EW * T::EH) {
+                const float v = vmap[sub][it];
+                eig[e / T::EW][e % T::EW] = v > thr ? v : 0.f;
+            }
         }
         __syncthreads();
         for (int e = threadIdx.x; e < GF_BX * GF_BY; e += 256) {
@@ -1241,23 +1267,30 @@ __global__ void __launch_bounds__(256) gftt_topk_compact_kernel(GfArgs G) {
     const unsigned int n = min(*G.n_cand, G.cand_cap);
     const unsigned int cut = (unsigned int)G.cut[0];
     const int lane = threadIdx.x & 63;
-    for (unsigned int i0 = blockIdx.x * 256; i0 < n; i0 += gridDim.x * 256) {  // wave-uniform trip count
-        const unsigned int i = i0 + threadIdx.x;
-        unsigned long long k = 0;
-        bool take = false;
-        if (i < n) {
-            k = G.cand[i];
-            take = (unsigned int)(k >> 52) >= cut;
+    constexpr int U = 4;  // candidate loads in flight per lane
+    const unsigned int stride = gridDim.x * 256;
+    for (unsigned int i0 = blockIdx.x * 256; i0 < n; i0 += U * stride) {  // wave-uniform trip count
+        unsigned long long kv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned int i = i0 + u * stride + threadIdx.x;
+            kv[u] = i < n ? G.cand[i] : 0ull;
         }
-        const unsigned long long bal = __ballot(take);  // one counter atomic per wave
-        if (!bal) continue;
-        const int leader = __ffsll((long long)bal) - 1;
-        unsigned int base = 0;
-        if (lane == leader) base = atomicAdd(G.n_top, (unsigned int)__popcll(bal));
-        base = __shfl(base, leader, 64);
-        if (take) {
-            const unsigned int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
-            if (pos < G.topk_cap) G.topk[pos] = k;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned int i = i0 + u * stride + threadIdx.x;
+            const unsigned long long k = kv[u];
+            const bool take = i < n && (unsigned int)(k >> 52) >= cut;
+            const unsigned long long bal = __ballot(take);  // one counter atomic per wave
+            if (!bal) continue;
+            const int leader = __ffsll((long long)bal) - 1;
+            unsigned int base = 0;
+            if (lane == leader) base = atomicAdd(G.n_top, (unsigned int)__popcll(bal));
+            base = __shfl(base, leader, 64);
+            if (take) {
+                const unsigned int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+                if (pos < G.topk_cap) G.topk[pos] = k;
+            }
         }
     }
 }
