@@ -123,6 +123,10 @@ int ensure_iters(erp_tracker* t, int iters) {
     return VIO_OK;
 }
 
+// the GFTT selection grid (3 slots x 4 B per min-distance cell) lives in LDS up to this size, next
+// to the selection kernel's ~14 KB of static LDS (config 1: 128 x 64 cells = 96 KB)
+constexpr size_t kSelectGridLds = 140 * 1024;
+
 int ensure_gftt(erp_tracker* t, double min_dist) {
     int rc;
     if (!t->d_cand) {
@@ -142,7 +146,7 @@ int ensure_gftt(erp_tracker* t, double min_dist) {
         int cell = (int)std::lrint(min_dist);
         int gw = (t->W + cell - 1) / cell, gh = (t->H + cell - 1) / cell;
         size_t bytes = (size_t)gw * gh * 3 * sizeof(uint32_t);
-        if (bytes > 96 * 1024 && bytes > t->grid_bytes) {
+        if (bytes > kSelectGridLds && bytes > t->grid_bytes) {
             if ((rc = dalloc(t, &t->d_grid, bytes)) != VIO_OK) return rc;
             t->grid_bytes = bytes;
         }
@@ -291,7 +295,7 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     g.gw = (t->W + g.cell - 1) / g.cell;
     g.gh = (t->H + g.cell - 1) / g.cell;
     size_t lds = (size_t)g.gw * g.gh * 3 * sizeof(uint32_t);
-    g.grid_global = lds > 96 * 1024 ? t->d_grid : nullptr;
+    g.grid_global = lds > kSelectGridLds ? t->d_grid : nullptr;
     g.corners = t->d_corners;
     g.n_out = t->d_scal + 4;
     if (!g.grid_global) {
