@@ -366,10 +366,20 @@ __global__ void __launch_bounds__(256) chol_diag_kernel(double* S, int n, int k,
     double* P = LT + 256;        // [4 waves][16][17] product scratch of the inverse
     __shared__ int bad_s;
     double* blk = S + (size_t)k * NB * n + (size_t)k * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += 256) {
-        const int r = e >> 6, c = e & 63;
-        T[r * TLD + c] = c <= r ? blk[(size_t)r * n + c] : 0.0;
-        X[r * TLD + c] = 0.0;
+    {
+        constexpr int PER = NB * NB / 256;  // loads first, then the LDS stores
+        double v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = threadIdx.x + 256 * u, r = e >> 6, c = e & 63;
+            v[u] = c <= r ? blk[(size_t)r * n + c] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = threadIdx.x + 256 * u, r = e >> 6, c = e & 63;
+            T[r * TLD + c] = v[u];
+            X[r * TLD + c] = 0.0;
+        }
     }
     __syncthreads();
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -461,6 +471,26 @@ __global__ void __launch_bounds__(256) chol_diag_kernel(double* S, int n, int k,
     }
 }
 
+// two 64x64 tiles into LDS: all 32 global loads of a lane are issued before the first LDS store
+// (one memory round trip instead of sixteen)
+__device__ __forceinline__ void stage_tiles(double (*As)[NB + 1], double (*Bs)[NB + 1], const double* A, size_t lda,
+                                            const double* B, size_t ldb) {
+    constexpr int PER = NB * NB / 256;
+    double va[PER], vb[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int e = threadIdx.x + 256 * u, r = e / NB, c = e % NB;
+        va[u] = A[(size_t)r * lda + c];
+        vb[u] = B[(size_t)r * ldb + c];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int e = threadIdx.x + 256 * u, r = e / NB, c = e % NB;
+        As[r][c] = va[u];
+        Bs[r][c] = vb[u];
+    }
+}
+
 // 64x64x64 tile product on MFMA f64: acc(wave's 32x32) += A(64xK) * B(64xK)^T from LDS
 // wave w: rows 32*(w>>1) .. +32, cols 32*(w&1) .. +32 ; 2x2 MFMA 16x16 tiles
 __device__ __forceinline__ void mfma_tile_ABt(const double (*As)[NB + 1], const double (*Bs)[NB + 1], d4 acc[2][2],
@@ -488,11 +518,7 @@ __global__ void __launch_bounds__(256) chol_trsm_kernel(double* S, int n, int k,
     const int i = k + 1 + blockIdx.x;
     double* blk = S + (size_t)i * NB * n + (size_t)k * NB;
     const double* Li = Linv + (size_t)k * NB * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += 256) {
-        int r = e / NB, c = e % NB;
-        As[r][c] = blk[(size_t)r * n + c];
-        Bs[r][c] = Li[e];
-    }
+    stage_tiles(As, Bs, blk, (size_t)n, Li, NB);
     __syncthreads();
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     d4 acc[2][2];
@@ -521,24 +547,35 @@ __global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k,
     const int i = k + 1 + ii, j = k + 1 + jj;
     const double* Aik = S + (size_t)i * NB * n + (size_t)k * NB;
     const double* Ajk = S + (size_t)j * NB * n + (size_t)k * NB;
-    for (int e = threadIdx.x; e < NB * NB; e += 256) {
-        int r = e / NB, c = e % NB;
-        As[r][c] = Aik[(size_t)r * n + c];
-        Bs[r][c] = Ajk[(size_t)r * n + c];
-    }
-    __syncthreads();
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r0 = 32 * (wid >> 1), c0 = 32 * (wid & 1);
+    double* C = S + (size_t)i * NB * n + (size_t)j * NB;
+    // the lane's 16 destination values are fetched first: their latency overlaps the staging and
+    // the MFMAs instead of following them
+    double cv[2][2][4];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                cv[ti][tj][q] = C[(size_t)r * n + c];
+            }
+    stage_tiles(As, Bs, Aik, (size_t)n, Ajk, (size_t)n);
+    __syncthreads();
     d4 acc[2][2];
     for (int a = 0; a < 2; ++a)
         for (int b = 0; b < 2; ++b) acc[a][b] = d4{0, 0, 0, 0};
     mfma_tile_ABt(As, Bs, acc, wid, lane);
-    double* C = S + (size_t)i * NB * n + (size_t)j * NB;
-    const int r0 = 32 * (wid >> 1), c0 = 32 * (wid & 1);
+#pragma unroll
     for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
         for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
             for (int q = 0; q < 4; ++q) {
-                int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
-                if (i != j || c <= r) C[(size_t)r * n + c] -= acc[ti][tj][q];
+                const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                if (i != j || c <= r) C[(size_t)r * n + c] = cv[ti][tj][q] - acc[ti][tj][q];
             }
 }
 
