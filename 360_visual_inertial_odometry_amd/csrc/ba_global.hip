@@ -595,11 +595,21 @@ __global__ void __launch_bounds__(256) trsv_fwd_kernel(const double* S, int n, i
     if (blockIdx.x == 0 && threadIdx.x < NB) y[k * NB + threadIdx.x] = yk[threadIdx.x];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const double ylane = yk[lane];
-    for (int r = (k + 1) * NB + blockIdx.x * 16 + wid; r < n && r < (k + 1) * NB + (blockIdx.x + 1) * 16; r += 4) {
-        double s = S[(size_t)r * n + (size_t)k * NB + lane] * ylane;
+    // the wave's four rows: loads first, then the four reductions
+    const int rb = (k + 1) * NB + blockIdx.x * 16 + wid, rend = min(n, (k + 1) * NB + (blockIdx.x + 1) * 16);
+    double sv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int r = rb + 4 * u;
+        sv[u] = r < rend ? S[(size_t)r * n + (size_t)k * NB + lane] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int r = rb + 4 * u;
+        double s = sv[u] * ylane;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        if (lane == 0) b[r] -= s;
+        if (lane == 0 && r < rend) b[r] -= s;
     }
 }
 
@@ -620,8 +630,13 @@ __global__ void __launch_bounds__(256) trsv_bwd_kernel(const double* S, int n, i
     const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + cl;
     double s = 0.0;
-    if (c < k * NB)
-        for (int q = g * 16; q < g * 16 + 16; ++q) s += S[(size_t)(k * NB + q) * n + c] * xk[q];
+    if (c < k * NB) {
+        double v[16];  // loads first, then the ordered sum
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = S[(size_t)(k * NB + g * 16 + u) * n + c];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u] * xk[g * 16 + u];
+    }
     part[g][cl] = s;
     __syncthreads();
     if (g == 0 && c < k * NB) y[c] -= (part[0][cl] + part[1][cl]) + (part[2][cl] + part[3][cl]);
