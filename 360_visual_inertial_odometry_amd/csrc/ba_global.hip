@@ -290,7 +290,21 @@ __global__ void __launch_bounds__(GT) gba_schur_kernel(GbaArgs A) {
     if (lane >= 36) return;
     const int i = lane / 6, j = lane % 6;
     double acc = 0.0;
-    for (int c = A.dest_ptr[d]; c < A.dest_ptr[d + 1]; ++c) {
+    const int cbeg = A.dest_ptr[d], cend = A.dest_ptr[d + 1];
+    int c = cbeg;
+    for (; c + 4 <= cend; c += 4) {  // four contributions' loads in flight, summed in order
+        double y[4][3], w[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double* Y = A.Yo + 18 * (size_t)A.contrib_a[c + u] + 3 * i;
+            const double* W = A.Wo + 18 * (size_t)A.contrib_b[c + u] + 3 * j;
+#pragma unroll
+            for (int e = 0; e < 3; ++e) { y[u][e] = Y[e]; w[u][e] = W[e]; }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += y[u][0] * w[u][0] + y[u][1] * w[u][1] + y[u][2] * w[u][2];
+    }
+    for (; c < cend; ++c) {
         const double* Y = A.Yo + 18 * (size_t)A.contrib_a[c] + 3 * i;
         const double* W = A.Wo + 18 * (size_t)A.contrib_b[c] + 3 * j;
         acc += Y[0] * W[0] + Y[1] * W[1] + Y[2] * W[2];
