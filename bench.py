@@ -28,8 +28,9 @@ sys.path.insert(0, ROOT)
 FP64_PEAK = 78.6e12  # MI355X FP64 vector (= FP64 matrix) peak, AMD spec
 
 
-TRACKER_KERNELS = ("pyr_down_kernel", "lk_kernel", "ransac_prep_kernel", "ransac_hyp_kernel", "ransac_select_kernel",
-                   "gftt_reset_kernel", "gftt_max_kernel", "gftt_hist_kernel", "gftt_cand_kernel",
+TRACKER_KERNELS = ("pyr_down_kernel", "lk_kernel", "ransac_prep_kernel", "ransac_sample_kernel", "ransac_hyp_kernel",
+                   "ransac_select_kernel", "gftt_reset_kernel", "gftt_eig_kernel", "gftt_max_kernel", "gftt_hist_kernel",
+                   "gftt_cand_kernel",
                    "gftt_topk_compact_kernel", "gftt_select_kernel<false>", "gftt_select_kernel<true>",
                    "disc_mask_kernel")
 
@@ -61,7 +62,8 @@ def klt_traffic():
     if not k or "lk_kernel" not in k:
         return None
     runs = k["lk_kernel"]["dispatches"]
-    return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items() if n in TRACKER_KERNELS) / runs
+    return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items()
+               if n in TRACKER_KERNELS or n.startswith("rocprim")) / runs  # rocprim: the top-K key sort
 
 
 def ba_flops_per_iter(prob):
