@@ -1492,13 +1492,88 @@ __device__ __forceinline__ void lm_solve(BaShared& sh, const WinCtx& c) {
     }
 }
 
+// ---- setup helpers: the lane's loads of several strides are issued before its stores (a loop of
+// dependent load -> store pairs costs one memory round trip per stride otherwise)
+constexpr int SETUP_U = 4;
+// dst[e] = src[e], e < n
+__device__ __forceinline__ void copy_strided(double* dst, const double* src, int n) {
+    for (int e0 = threadIdx.x; e0 < n; e0 += SETUP_U * BA_THREADS) {
+        double v[SETUP_U];
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int e = e0 + u * BA_THREADS;
+            v[u] = e < n ? src[e] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int e = e0 + u * BA_THREADS;
+            if (e < n) dst[e] = v[u];
+        }
+    }
+}
+// (landmark, keyframe) -> observation table (pairs are unique: host-checked); lk preset to -1
+__device__ __forceinline__ void fill_lk(int* lk, const int* obs_lm, const int* obs_kf, int N) {
+    for (int o0 = threadIdx.x; o0 < N; o0 += SETUP_U * BA_THREADS) {
+        int lm[SETUP_U], kf[SETUP_U];
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int o = o0 + u * BA_THREADS;
+            lm[u] = o < N ? obs_lm[o] : 0;
+            kf[u] = o < N ? obs_kf[o] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int o = o0 + u * BA_THREADS;
+            if (o < N) lk[16 * lm[u] + kf[u]] = o;
+        }
+    }
+}
+// fixed cost (program.cc:305-390): residual blocks whose pose and point are both constant, in the
+// lane's observation order; posef = the window's pose -> f-column table (LDS), pc / rcb its pose cache
+template <typename PC, typename RCB>
+__device__ __forceinline__ double fixed_cost(const WinCtx& c, const int* posef, const PC& pc, const RCB& rcb) {
+    const BaWin& w = *c.w;
+    const int N = w.N;
+    double fc = 0.0;
+    for (int o0 = threadIdx.x; o0 < N; o0 += SETUP_U * BA_THREADS) {
+        int kf[SETUP_U], lm[SETUP_U];
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int o = o0 + u * BA_THREADS;
+            kf[u] = o < N ? c.obs_kf[o] : 0;
+            lm[u] = o < N ? c.obs_lm[o] : 0;
+        }
+        unsigned fixed = 0;
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int o = o0 + u * BA_THREADS;
+            if (o < N && posef[kf[u]] < 0 && !c.lm_var[lm[u]]) fixed |= 1u << u;
+        }
+        for (int u = 0; u < SETUP_U; ++u) {  // rare: reload the observation
+            if (!((fixed >> u) & 1u)) continue;
+            const int o = o0 + u * BA_THREADS;
+            const int k = c.obs_kf[o], l = c.obs_lm[o];
+            double Pw[3] = {c.lm_xyz0[3 * l], c.lm_xyz0[3 * l + 1], c.lm_xyz0[3 * l + 2]};
+            double r[2], Jp[12], Jl[6];
+            bool jz;
+            if (factor_eval(pc[k], rcb[k], Pw, (double)c.obs_uv[2 * o], (double)c.obs_uv[2 * o + 1], w.cols, w.rows,
+                            w.Lw, false, w.is_pnp, false, r, Jp, Jl, jz) == 0) {
+                double cst, sc;
+                huber(w.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
+                fc += cst;
+            }
+        }
+    }
+    return fc;
+}
+
 // reset the free parameters of the window to their initial values
 __device__ __forceinline__ void init_params(BaShared& sh, const WinCtx& c, bool poses_only) {
     const BaWin& w = *c.w;
     double* ws = c.ws;
     for (int e = threadIdx.x; e < 6 * w.K; e += BA_THREADS) ws[c.L.x_pose + e] = 0.0;
     if (!poses_only) {
-        for (int e = threadIdx.x; e < 3 * w.L; e += BA_THREADS) ws[c.L.x_lm + e] = c.lm_xyz0[e];
+        copy_strided(ws + c.L.x_lm, c.lm_xyz0, 3 * w.L);
         for (int e = threadIdx.x; e < 3 * w.K; e += BA_THREADS) ws[c.L.x_vel + e] = w.is_vi ? c.vel0[e] : 0.0;
         for (int e = threadIdx.x; e < 6; e += BA_THREADS) ws[c.L.x_bias + e] = e < 3 ? w.bg0[e] : w.ba0[e - 3];
     }
@@ -1571,8 +1646,7 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
         int* lk = reinterpret_cast<int*>(c.ws + c.L.lk);
         for (int e = threadIdx.x; e < 16 * L; e += BA_THREADS) lk[e] = -1;
         __syncthreads();
-        for (int o = threadIdx.x; o < N; o += BA_THREADS)
-            lk[16 * c.obs_lm[o] + c.obs_kf[o]] = o;
+        fill_lk(lk, c.obs_lm, c.obs_kf, N);
     }
     init_params(sh, c, false);
 
@@ -1580,20 +1654,7 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
     {
         pose_cache(sh, c, c.ws + c.L.x_pose);
         __syncthreads();
-        double fc = 0.0;
-        for (int o = threadIdx.x; o < N; o += BA_THREADS) {
-            int k = c.obs_kf[o], l = c.obs_lm[o];
-            if (w.pose_f[k] >= 0 || c.lm_var[l]) continue;
-            double Pw[3] = {c.lm_xyz0[3 * l], c.lm_xyz0[3 * l + 1], c.lm_xyz0[3 * l + 2]};
-            double r[2], Jp[12], Jl[6];
-            bool jz;
-            if (factor_eval(sh.pc[k], sh.Rcb_raw[k], Pw, (double)c.obs_uv[2 * o], (double)c.obs_uv[2 * o + 1], w.cols,
-                            w.rows, w.Lw, false, w.is_pnp, false, r, Jp, Jl, jz) == 0) {
-                double cst, sc;
-                huber(w.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
-                fc += cst;
-            }
-        }
+        const double fc = fixed_cost(c, sh.posef, sh.pc, sh.Rcb_raw);
         double fct = block_sum(fc, sh.red);
         if (threadIdx.x == 0) sh.st.fixed_cost = fct;
         __syncthreads();
