@@ -988,6 +988,7 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
     __shared__ int s_good[GS_THREADS];
     __shared__ unsigned int s_idx[GS_THREADS];  // the batch's candidate addresses
     __shared__ unsigned int s_sv[GS_THREADS];   // survivors of the pre-filter, batch order: y << 16 | x
+    __shared__ int s_cell[GS_THREADS];          // their grid cells (yc * gw + xc)
     __shared__ unsigned long long s_conf[GS_THREADS][GS_THREADS / 64];
     __shared__ int s_wcnt[GS_THREADS / 64];
     __shared__ unsigned long long s_am[GS_THREADS / 64];  // accepted survivors of the batch
@@ -1062,6 +1063,7 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
                 x = (int)(idx % G.W);
                 y = (int)(idx / G.W);
                 s_sv[rank] = ((unsigned int)y << 16) | (unsigned int)x;
+                s_cell[rank] = (y / cell) * G.gw + x / cell;
             }
             __syncthreads();
             if (good) {
@@ -1143,21 +1145,20 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
                 const int kk = nacc_before + before;
                 G.corners[2 * kk] = (float)x;
                 G.corners[2 * kk + 1] = (float)y;
-                const int xc = x / cell, yc = y / cell;
+                const int mycell = s_cell[rank];
                 int i_cell = 0, m_cell = 0;
                 for (int r = 0; r < nsv; ++r) {
                     if (!((s_am[r >> 6] >> (r & 63)) & 1ull)) continue;
-                    const int xr = (int)(s_sv[r] & 0xffffu), yr = (int)(s_sv[r] >> 16);
-                    if (xr / cell == xc && yr / cell == yc) {
+                    if (s_cell[r] == mycell) {
                         if (r < rank) ++i_cell;
                         ++m_cell;
                     }
                 }
-                uint32_t* cellp = &grid[(yc * G.gw + xc) * GS_SLOTS];
+                uint32_t* cellp = &grid[mycell * GS_SLOTS];
                 int e0 = 0;
                 while (e0 < GS_SLOTS && cellp[e0] != 0xffffffffu) ++e0;  // entries from earlier batches
                 const int slot = min(e0 + i_cell, GS_SLOTS - 1);
-                if (e0 + i_cell < GS_SLOTS - 1 || i_cell == m_cell - 1) s_slot_val[rank] = ((uint32_t)y << 16) | (uint32_t)x, s_slot_idx[rank] = (yc * G.gw + xc) * GS_SLOTS + slot;
+                if (e0 + i_cell < GS_SLOTS - 1 || i_cell == m_cell - 1) s_slot_val[rank] = ((uint32_t)y << 16) | (uint32_t)x, s_slot_idx[rank] = mycell * GS_SLOTS + slot;
                 else s_slot_idx[rank] = -1;
             }
             __syncthreads();
