@@ -239,47 +239,76 @@ __device__ __noinline__ void imu_eval(const vio_preint& p, const double* sqi, co
 }
 
 // sqrt information of an IMU factor (Factors.cpp:1309-1323): chol((cov9 + 1e-8 I)^-1)^T, or I
-__device__ __noinline__ void imu_sqrt_info(const vio_preint& p, double* out) {
-    double M[9][18];
-    for (int i = 0; i < 9; ++i)
-        for (int j = 0; j < 18; ++j)
-            M[i][j] = j < 9 ? (double)p.cov9[9 * i + j] + (i == j ? 1e-8 : 0.0) : (j - 9 == i ? 1.0 : 0.0);
+// InertialFactorFixedGravity ctor (Factors.cpp:1310-1323): sqrt-information = chol((cov + 1e-8 I)^-1)^T,
+// identity when the inverse or its Cholesky fails.  One whole wave per factor: Gauss-Jordan with
+// partial pivoting on [Sigma | I] with lane j < 18 holding column j (9 rows in registers, pivot row
+// and multipliers broadcast by v_readlane), then the Cholesky of the inverse with lane i < 9 holding
+// row i.  Every matrix element goes through the same operations in the same order as the serial
+// elimination (oracle/ba_oracle.c), so the result is the same; nothing is dynamically indexed.
+__device__ __noinline__ void imu_sqrt_info_wave(const vio_preint& p, double* out) {
+    const int lane = threadIdx.x & 63;
+    const int j = lane < 18 ? lane : 17;
+    double m[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) m[i] = j < 9 ? (double)p.cov9[9 * i + j] + (i == j ? 1e-8 : 0.0) : (j - 9 == i ? 1.0 : 0.0);
     bool ok = true;
-    for (int c = 0; c < 9 && ok; ++c) {
-        int piv = c;
+#pragma unroll
+    for (int c = 0; c < 9; ++c) {
+        if (!ok) break;
+        // pivot row: the largest |M[r][c]|, r >= c, first one on ties (lane c scans its column)
+        int pv = c;
+        double bv = fabs(m[c]), pval = m[c];
+#pragma unroll
         for (int rr = c + 1; rr < 9; ++rr)
-            if (fabs(M[rr][c]) > fabs(M[piv][c])) piv = rr;
-        if (M[piv][c] == 0.0) { ok = false; break; }
-        if (piv != c)
-            for (int j = 0; j < 18; ++j) { double t = M[c][j]; M[c][j] = M[piv][j]; M[piv][j] = t; }
-        double iv = 1.0 / M[c][c];
-        for (int j = 0; j < 18; ++j) M[c][j] *= iv;
+            if (fabs(m[rr]) > bv) { bv = fabs(m[rr]); pv = rr; pval = m[rr]; }
+        const int piv = __builtin_amdgcn_readlane(pv, c);
+        if (readlane_d(pval, c) == 0.0) { ok = false; break; }
+#pragma unroll
+        for (int rr = c + 1; rr < 9; ++rr)
+            if (rr == piv) { const double t = m[c]; m[c] = m[rr]; m[rr] = t; }
+        const double iv = 1.0 / readlane_d(m[c], c);
+        m[c] *= iv;
+#pragma unroll
         for (int rr = 0; rr < 9; ++rr) {
             if (rr == c) continue;
-            double f = M[rr][c];
+            const double f = readlane_d(m[rr], c);
             if (f == 0.0) continue;
-            for (int j = 0; j < 18; ++j) M[rr][j] -= f * M[c][j];
+            m[rr] -= f * m[c];
         }
     }
-    double Lm[81];
+    // row i of the inverse into lane i: Inv[i][k] = M[i][9 + k] (lane 9 + k, register i)
+    double r[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        r[k] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const double v = readlane_d(m[i], 9 + k);
+            if (lane == i) r[k] = v;
+        }
+    }
     if (ok) {
-        for (int i = 0; i < 9; ++i)
-            for (int j = 0; j < 9; ++j) Lm[9 * i + j] = M[i][9 + j];
-        for (int j = 0; j < 9 && ok; ++j) {
-            double d = Lm[9 * j + j];
-            for (int k = 0; k < j; ++k) d -= Lm[9 * j + k] * Lm[9 * j + k];
-            if (!(d > 0.0)) { ok = false; break; }
-            d = sqrt(d);
-            Lm[9 * j + j] = d;
-            for (int i = j + 1; i < 9; ++i) {
-                double s = Lm[9 * i + j];
-                for (int k = 0; k < j; ++k) s -= Lm[9 * i + k] * Lm[9 * j + k];
-                Lm[9 * i + j] = s / d;
-            }
+#pragma unroll
+        for (int c = 0; c < 9; ++c) {
+            double d = r[c];  // meaningful on lane c: L[c][c] - sum_k L[c][k]^2
+#pragma unroll
+            for (int k = 0; k < c; ++k) d -= r[k] * r[k];
+            const double dc = readlane_d(d, c);
+            if (!(dc > 0.0)) { ok = false; break; }
+            const double sd = sqrt(dc);
+            double s = r[c];
+#pragma unroll
+            for (int k = 0; k < c; ++k) s -= r[k] * readlane_d(r[k], c);
+            if (lane == c) r[c] = sd;
+            else if (lane > c && lane < 9) r[c] = s / sd;
         }
     }
-    for (int i = 0; i < 9; ++i)
-        for (int j = 0; j < 9; ++j) out[9 * i + j] = ok ? (j >= i ? Lm[9 * j + i] : 0.0) : (i == j ? 1.0 : 0.0);
+    // out (row-major, upper) = L^T: lane jj writes column jj, out[i][jj] = L[jj][i] for i <= jj
+    if (lane < 9) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+            out[9 * i + lane] = ok ? (i <= lane ? r[i] : 0.0) : (i == lane ? 1.0 : 0.0);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1628,10 +1657,11 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
                 polar3(pr + 12, sh.pinit[k] + 12);
                 for (int i = 0; i < 3; ++i) sh.pinit[k][21 + i] = pr[21 + i];
                 for (int i = 0; i < 9; ++i) sh.Rcb_raw[k][i] = pr[12 + i];
-            } else if (job == 2) {
-                if (w.is_vi && k >= 1 && c.preint_valid[k]) imu_sqrt_info(c.preint[k], c.sqi + 81 * k);
             }
         }
+        if (job >= 2 && w.is_vi)  // whole waves 2 and 3, one IMU factor at a time each
+            for (int kk = 1 + (job - 2); kk < K; kk += 2)
+                if (c.preint_valid[kk]) imu_sqrt_info_wave(c.preint[kk], c.sqi + 81 * kk);
     }
     for (int o = threadIdx.x; o < N; o += BA_THREADS) c.outlier[o] = 0;
     for (int k = threadIdx.x; k < BA_KMAX; k += BA_THREADS) {
