@@ -1366,14 +1366,90 @@ __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
     prof_mark(sh, PF_CAND);
 }
 
+// ---- setup helpers: the lane's loads of several strides are issued before its stores (a loop of
+// dependent load -> store pairs costs one memory round trip per stride otherwise)
+constexpr int SETUP_U = 4;
+// dst[e] = src[e], e < n, by NT threads
+template <int NT = BA_THREADS>
+__device__ __forceinline__ void copy_strided(double* dst, const double* src, int n) {
+    for (int e0 = threadIdx.x; e0 < n; e0 += SETUP_U * NT) {
+        double v[SETUP_U];
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int e = e0 + u * NT;
+            v[u] = e < n ? src[e] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int e = e0 + u * NT;
+            if (e < n) dst[e] = v[u];
+        }
+    }
+}
+// (landmark, keyframe) -> observation table (pairs are unique: host-checked); lk preset to -1
+__device__ __forceinline__ void fill_lk(int* lk, const int* obs_lm, const int* obs_kf, int N) {
+    for (int o0 = threadIdx.x; o0 < N; o0 += SETUP_U * BA_THREADS) {
+        int lm[SETUP_U], kf[SETUP_U];
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int o = o0 + u * BA_THREADS;
+            lm[u] = o < N ? obs_lm[o] : 0;
+            kf[u] = o < N ? obs_kf[o] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int o = o0 + u * BA_THREADS;
+            if (o < N) lk[16 * lm[u] + kf[u]] = o;
+        }
+    }
+}
+// fixed cost (program.cc:305-390): residual blocks whose pose and point are both constant, in the
+// lane's observation order; posef = the window's pose -> f-column table (LDS), pc / rcb its pose cache
+template <typename PC, typename RCB>
+__device__ __forceinline__ double fixed_cost(const WinCtx& c, const int* posef, const PC& pc, const RCB& rcb) {
+    const BaWin& w = *c.w;
+    const int N = w.N;
+    double fc = 0.0;
+    for (int o0 = threadIdx.x; o0 < N; o0 += SETUP_U * BA_THREADS) {
+        int kf[SETUP_U], lm[SETUP_U];
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int o = o0 + u * BA_THREADS;
+            kf[u] = o < N ? c.obs_kf[o] : 0;
+            lm[u] = o < N ? c.obs_lm[o] : 0;
+        }
+        unsigned fixed = 0;
+#pragma unroll
+        for (int u = 0; u < SETUP_U; ++u) {
+            const int o = o0 + u * BA_THREADS;
+            if (o < N && posef[kf[u]] < 0 && !c.lm_var[lm[u]]) fixed |= 1u << u;
+        }
+        for (int u = 0; u < SETUP_U; ++u) {  // rare: reload the observation
+            if (!((fixed >> u) & 1u)) continue;
+            const int o = o0 + u * BA_THREADS;
+            const int k = c.obs_kf[o], l = c.obs_lm[o];
+            double Pw[3] = {c.lm_xyz0[3 * l], c.lm_xyz0[3 * l + 1], c.lm_xyz0[3 * l + 2]};
+            double r[2], Jp[12], Jl[6];
+            bool jz;
+            if (factor_eval(pc[k], rcb[k], Pw, (double)c.obs_uv[2 * o], (double)c.obs_uv[2 * o + 1], w.cols, w.rows,
+                            w.Lw, false, w.is_pnp, false, r, Jp, Jl, jz) == 0) {
+                double cst, sc;
+                huber(w.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
+                fc += cst;
+            }
+        }
+    }
+    return fc;
+}
+
 __device__ __forceinline__ void accept_candidate(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;
     double* ws = c.ws;
     const int K = w.K, L = w.L;
-    for (int e = threadIdx.x; e < 6 * K; e += BA_THREADS) ws[c.L.x_pose + e] = ws[c.L.c_pose + e];
-    for (int e = threadIdx.x; e < 3 * L; e += BA_THREADS) ws[c.L.x_lm + e] = ws[c.L.c_lm + e];
-    for (int e = threadIdx.x; e < 3 * K; e += BA_THREADS) ws[c.L.x_vel + e] = ws[c.L.c_vel + e];
-    for (int e = threadIdx.x; e < 6; e += BA_THREADS) ws[c.L.x_bias + e] = ws[c.L.c_bias + e];
+    copy_strided(ws + c.L.x_pose, ws + c.L.c_pose, 6 * K);
+    copy_strided(ws + c.L.x_lm, ws + c.L.c_lm, 3 * L);
+    copy_strided(ws + c.L.x_vel, ws + c.L.c_vel, 3 * K);
+    copy_strided(ws + c.L.x_bias, ws + c.L.c_bias, 6);
     __syncthreads();
 }
 
@@ -1519,81 +1595,6 @@ __device__ __forceinline__ void lm_solve(BaShared& sh, const WinCtx& c) {
             __syncthreads();
         }
     }
-}
-
-// ---- setup helpers: the lane's loads of several strides are issued before its stores (a loop of
-// dependent load -> store pairs costs one memory round trip per stride otherwise)
-constexpr int SETUP_U = 4;
-// dst[e] = src[e], e < n
-__device__ __forceinline__ void copy_strided(double* dst, const double* src, int n) {
-    for (int e0 = threadIdx.x; e0 < n; e0 += SETUP_U * BA_THREADS) {
-        double v[SETUP_U];
-#pragma unroll
-        for (int u = 0; u < SETUP_U; ++u) {
-            const int e = e0 + u * BA_THREADS;
-            v[u] = e < n ? src[e] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < SETUP_U; ++u) {
-            const int e = e0 + u * BA_THREADS;
-            if (e < n) dst[e] = v[u];
-        }
-    }
-}
-// (landmark, keyframe) -> observation table (pairs are unique: host-checked); lk preset to -1
-__device__ __forceinline__ void fill_lk(int* lk, const int* obs_lm, const int* obs_kf, int N) {
-    for (int o0 = threadIdx.x; o0 < N; o0 += SETUP_U * BA_THREADS) {
-        int lm[SETUP_U], kf[SETUP_U];
-#pragma unroll
-        for (int u = 0; u < SETUP_U; ++u) {
-            const int o = o0 + u * BA_THREADS;
-            lm[u] = o < N ? obs_lm[o] : 0;
-            kf[u] = o < N ? obs_kf[o] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < SETUP_U; ++u) {
-            const int o = o0 + u * BA_THREADS;
-            if (o < N) lk[16 * lm[u] + kf[u]] = o;
-        }
-    }
-}
-// fixed cost (program.cc:305-390): residual blocks whose pose and point are both constant, in the
-// lane's observation order; posef = the window's pose -> f-column table (LDS), pc / rcb its pose cache
-template <typename PC, typename RCB>
-__device__ __forceinline__ double fixed_cost(const WinCtx& c, const int* posef, const PC& pc, const RCB& rcb) {
-    const BaWin& w = *c.w;
-    const int N = w.N;
-    double fc = 0.0;
-    for (int o0 = threadIdx.x; o0 < N; o0 += SETUP_U * BA_THREADS) {
-        int kf[SETUP_U], lm[SETUP_U];
-#pragma unroll
-        for (int u = 0; u < SETUP_U; ++u) {
-            const int o = o0 + u * BA_THREADS;
-            kf[u] = o < N ? c.obs_kf[o] : 0;
-            lm[u] = o < N ? c.obs_lm[o] : 0;
-        }
-        unsigned fixed = 0;
-#pragma unroll
-        for (int u = 0; u < SETUP_U; ++u) {
-            const int o = o0 + u * BA_THREADS;
-            if (o < N && posef[kf[u]] < 0 && !c.lm_var[lm[u]]) fixed |= 1u << u;
-        }
-        for (int u = 0; u < SETUP_U; ++u) {  // rare: reload the observation
-            if (!((fixed >> u) & 1u)) continue;
-            const int o = o0 + u * BA_THREADS;
-            const int k = c.obs_kf[o], l = c.obs_lm[o];
-            double Pw[3] = {c.lm_xyz0[3 * l], c.lm_xyz0[3 * l + 1], c.lm_xyz0[3 * l + 2]};
-            double r[2], Jp[12], Jl[6];
-            bool jz;
-            if (factor_eval(pc[k], rcb[k], Pw, (double)c.obs_uv[2 * o], (double)c.obs_uv[2 * o + 1], w.cols, w.rows,
-                            w.Lw, false, w.is_pnp, false, r, Jp, Jl, jz) == 0) {
-                double cst, sc;
-                huber(w.huber, r[0] * r[0] + r[1] * r[1], cst, sc);
-                fc += cst;
-            }
-        }
-    }
-    return fc;
 }
 
 // reset the free parameters of the window to their initial values
