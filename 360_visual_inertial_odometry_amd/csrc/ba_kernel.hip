@@ -238,7 +238,6 @@ __device__ __noinline__ void imu_eval(const vio_preint& p, const double* sqi, co
         }
 }
 
-// sqrt information of an IMU factor (Factors.cpp:1309-1323): chol((cov9 + 1e-8 I)^-1)^T, or I
 // InertialFactorFixedGravity ctor (Factors.cpp:1310-1323): sqrt-information = chol((cov + 1e-8 I)^-1)^T,
 // identity when the inverse or its Cholesky fails.  One whole wave per factor: Gauss-Jordan with
 // partial pivoting on [Sigma | I] with lane j < 18 holding column j (9 rows in registers, pivot row
