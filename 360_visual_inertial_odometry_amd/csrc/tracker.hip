@@ -452,28 +452,21 @@ __device__ void ransac_sample_seq(const RansacArgs& R, Mt19937& g, int n) {
         R.samples[3 * it + 2] = got[2];
     }
 }
-__global__ void __launch_bounds__(RS_THREADS) ransac_sample_kernel(RansacArgs R) {
+// the first RS_RAW tempered outputs of mt19937(seed): seeding recurrence, RS_BLOCKS twists of the
+// 624-word state (three dependency-free phases each) and tempering.  Depends on the seed only, so
+// the tracker pipeline runs it on its side stream while the frames are processed.
+__global__ void __launch_bounds__(RS_THREADS) ransac_raw_kernel(uint32_t seed, uint32_t* raw) {
     __shared__ uint32_t mt[624];
-    __shared__ uint32_t acc[RS_RAW];    // accepted draws (compacted), in stream order
-    __shared__ uint8_t len3[RS_RAW];    // 1: a hypothesis starting at draw p consumes exactly 3 draws
-    __shared__ int wsum[RS_THREADS / 64];
-    __shared__ int s_m, s_fallback;
-    const int n = *R.n_good;
-    if (n < 3 || R.iters <= 0) return;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x;
     if (tid == 0) {  // seeding recurrence (sequential, 623 steps)
-        uint32_t v = R.seed;
+        uint32_t v = seed;
         mt[0] = v;
         for (int i = 1; i < 624; ++i) {
             v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)i;
             mt[i] = v;
         }
-        s_m = 0;
-        s_fallback = 0;
     }
     __syncthreads();
-    const uint32_t range = (uint32_t)n;
-    const uint32_t thr = (uint32_t)(-range) % range;
     for (int blk = 0; blk < RS_BLOCKS; ++blk) {
         // twist: phases [0,227) [227,454) [454,624)
         const int lo[3] = {0, 227, 454}, hi[3] = {227, 454, 624};
@@ -488,15 +481,43 @@ __global__ void __launch_bounds__(RS_THREADS) ransac_sample_kernel(RansacArgs R)
             if (i < hi[ph]) mt[i] = nv;
             __syncthreads();
         }
-        // temper + accept test + compaction (stream order)
-        int accepted = 0;
-        uint32_t val = 0;
         if (tid < 624) {
             uint32_t y = mt[tid];
             y ^= y >> 11;
             y ^= (y << 7) & 0x9d2c5680u;
             y ^= (y << 15) & 0xefc60000u;
             y ^= y >> 18;
+            raw[624 * blk + tid] = y;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(RS_THREADS) ransac_sample_kernel(RansacArgs R) {
+    __shared__ uint32_t acc[RS_RAW];    // accepted draws (compacted), in stream order
+    __shared__ uint8_t len3[RS_RAW];    // 1: a hypothesis starting at draw p consumes exactly 3 draws
+    __shared__ int wsum[RS_THREADS / 64];
+    __shared__ int s_m, s_fallback;
+    const int n = *R.n_good;
+    if (n < 3 || R.iters <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) {
+        s_m = 0;
+        s_fallback = 0;
+    }
+    // the lane's tempered words of every block, loads in flight together
+    uint32_t yw[RS_BLOCKS];
+#pragma unroll
+    for (int blk = 0; blk < RS_BLOCKS; ++blk) yw[blk] = tid < 624 ? R.raw[624 * blk + tid] : 0u;
+    __syncthreads();
+    const uint32_t range = (uint32_t)n;
+    const uint32_t thr = (uint32_t)(-range) % range;
+#pragma unroll
+    for (int blk = 0; blk < RS_BLOCKS; ++blk) {
+        // accept test + compaction (stream order)
+        int accepted = 0;
+        uint32_t val = 0;
+        if (tid < 624) {
+            const uint32_t y = yw[blk];
             const uint64_t prod = (uint64_t)y * range;
             const uint32_t low = (uint32_t)prod;
             accepted = !(low < range && low < thr);
@@ -1347,6 +1368,11 @@ hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int fra
 hipError_t launch_lk(const LkArgs& a, hipStream_t st) {
     if (a.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(lk_kernel, dim3((a.n + LK_WAVES - 1) / LK_WAVES), dim3(64 * LK_WAVES), 0, st, a);
+    return hipGetLastError();
+}
+size_t ransac_raw_words() { return RS_RAW; }
+hipError_t launch_ransac_raw(uint32_t seed, uint32_t* raw, hipStream_t st) {
+    hipLaunchKernelGGL(ransac_raw_kernel, dim3(1), dim3(RS_THREADS), 0, st, seed, raw);
     return hipGetLastError();
 }
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st) {

@@ -63,6 +63,7 @@ struct erp_tracker {
     int* d_scal = nullptr;
     // gftt
     unsigned long long *d_cand = nullptr, *d_cand_sorted = nullptr;
+    uint32_t* d_raw = nullptr;  // tempered mt19937 words of the RANSAC seed (side stream)
     float* d_eig = nullptr;     // GFTT min-eigenvalue map (W x H f32)
     unsigned int cand_cap = 0;
     void* d_sort_tmp = nullptr;
@@ -83,7 +84,7 @@ struct erp_tracker {
     hipEvent_t ev[6] = {};
     // the GFTT eigenvalue map runs on a side stream, overlapped with pyramids / LK / RANSAC
     hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, raw_done = nullptr;
     bool ran = false;
     std::vector<void*> allocs;
 };
@@ -110,6 +111,7 @@ void tracker_free(erp_tracker* t) {
     if (t->side) (void)hipStreamDestroy(t->side);
     if (t->fork) (void)hipEventDestroy(t->fork);
     if (t->join) (void)hipEventDestroy(t->join);
+    if (t->raw_done) (void)hipEventDestroy(t->raw_done);
 }
 
 int ensure_iters(erp_tracker* t, int iters) {
@@ -181,11 +183,13 @@ int tracker_alloc(erp_tracker* t) {
     t->disc_words = (t->W + 31) / 32;
     if ((rc = dalloc(t, &t->d_disc, sizeof(uint32_t) * t->disc_words * t->H))) return rc;
     if ((rc = ensure_iters(t, 1024))) return rc;
+    if ((rc = dalloc(t, &t->d_raw, sizeof(uint32_t) * ransac_raw_words()))) return rc;
     for (auto& e : t->ev)
         if (hipEventCreate(&e) != hipSuccess) return hip_fail(t->ctx, hipErrorUnknown, "hipEventCreate");
     if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&t->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&t->raw_done, hipEventDisableTiming) != hipSuccess)
         return hip_fail(t->ctx, hipErrorUnknown, "side stream / events");
     return VIO_OK;
 }
@@ -255,6 +259,7 @@ RansacArgs ransac_args(erp_tracker* t, int n, int mode, int iters, uint32_t seed
     r.gidx = t->d_gidx; r.n_good = t->d_scal + 0;
     r.b0 = t->d_b0; r.b1 = t->d_b1;
     r.samples = t->d_samples; r.iters = iters; r.seed = seed; r.thresh = thr;
+    r.raw = t->d_raw;
     r.count = t->d_count; r.kept = t->d_kept; r.n_in = t->d_scal + 1;
     return r;
 }
@@ -433,8 +438,11 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
     // the eigenvalue map of the current frame does not depend on tracking: side stream
     VIO_HIP(t->ctx, hipEventRecord(t->fork, st));
     VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->fork, 0));
-    {
-        hipError_t e = launch_gftt_eig(gf_map_args(t, t->lvl[1][0], t->lp[0]), t->side);
+    {  // the RANSAC draws' raw stream depends on the seed only; then the eigenvalue map
+        hipError_t e = launch_ransac_raw(p->ransac_seed, t->d_raw, t->side);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac_raw_kernel");
+        VIO_HIP(t->ctx, hipEventRecord(t->raw_done, t->side));
+        e = launch_gftt_eig(gf_map_args(t, t->lvl[1][0], t->lp[0]), t->side);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_eig_kernel");
     }
     VIO_HIP(t->ctx, hipEventRecord(t->join, t->side));
@@ -443,6 +451,7 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
     RansacArgs r = ransac_args(t, n, 1, p->ransac_iters, p->ransac_seed, p->ransac_thresh_rad, p->polar_ratio,
                                p->boundary_margin, t->d_pts, t->d_next);
     if (n > 0) {
+        VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->raw_done, 0));
         hipError_t e = launch_ransac(r, true, st);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac kernels");
     } else {

@@ -44,6 +44,7 @@ struct RansacArgs {
     float* b0;             // [n][3] bearings of the compacted points
     float* b1;
     int32_t* samples;      // [iters][3]
+    const uint32_t* raw;   // [RS_RAW] tempered mt19937 words of `seed` (ransac_raw_kernel)
     int iters;
     uint32_t seed;
     float thresh;
@@ -98,6 +99,10 @@ struct DiscArgs {
 
 hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int frames, hipStream_t st);
 hipError_t launch_lk(const LkArgs& a, hipStream_t st);
+// the tempered mt19937 stream of a seed (independent of the points: may run on another stream)
+hipError_t launch_ransac_raw(uint32_t seed, uint32_t* raw, hipStream_t st);
+size_t ransac_raw_words();
+// gen_samples: hypotheses drawn on device from r.raw (launch_ransac_raw of r.seed must precede)
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st);
 hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st);
 // fast path (top-K) and the exact fallback over every candidate (used when `incomplete` is raised)
