@@ -28,7 +28,7 @@ EXPORTS = [
     "erp_tracker_upload", "erp_tracker_device_frame", "erp_tracker_swap", "erp_tracker_set_points",
     "erp_tracker_run", "erp_tracker_sync", "erp_tracker_download", "erp_tracker_stage_ms",
     "erp_tracker_destroy", "erp_frontend_create", "erp_frontend_track", "erp_frontend_features",
-    "erp_frontend_stats", "erp_frontend_destroy",
+    "erp_frontend_stats", "erp_frontend_destroy", "vio_imu_preintegrate", "vio_imu_preintegrate_kernel_ms",
 ]
 
 
@@ -80,6 +80,9 @@ def lib():
     L.erp_frontend_features.argtypes = [vp, vp, vp, vp, vp, C.c_int]
     L.erp_frontend_stats.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.erp_frontend_destroy.argtypes = [vp]
+    L.vio_imu_preintegrate.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, vp, vp, C.POINTER(abi.VioImuNoise), vp,
+                                       vp, vp]
+    L.vio_imu_preintegrate_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
     _lib = L
     return L
 
@@ -127,6 +130,20 @@ class Context:
         return [o.result() for o in outs]
 
 
+    # ---- IMU preintegration ----
+    def imu_preintegrate(self, samples, t_start, t_end, gyro_bias=None, accel_bias=None, noise=None):
+        """IMUPreintegrator::Preintegrate for every interval [t_start[i], t_end[i]) in one launch.
+
+        samples: (M, 7) [t, ax, ay, az, gx, gy, gz] rows sorted by t (or vio_imu_data records).
+        Returns (records dict of (n, ...) arrays, valid (n,) u8, cov_bias_diag (n, 6) f32)."""
+        return _imu_call(lambda *a: lib().vio_imu_preintegrate(self.h, *a), self.check, samples, t_start, t_end,
+                         gyro_bias, accel_bias, noise)
+
+    def imu_kernel_ms(self):
+        ms = C.c_double()
+        self.check(lib().vio_imu_preintegrate_kernel_ms(self.h, C.byref(ms)), "vio_imu_preintegrate_kernel_ms")
+        return ms.value
+
     # ---- ERP feature tracking ----
     def klt_track(self, prev, curr, pts, params=None):
         """cv::calcOpticalFlowPyrLK as FeatureTracker::TrackOpticalFlow calls it -> (next, status, err)."""
@@ -166,6 +183,28 @@ class Context:
         self.check(lib().erp_rot_ransac(self.h, _p(p0), _p(p1), n, W, H, _p(samples), len(samples) // 3,
                                         float(thr), _p(mask), C.byref(nin)), "erp_rot_ransac")
         return mask, nin.value
+
+
+def _imu_call(fn, check, samples, t_start, t_end, gyro_bias, accel_bias, noise):
+    """Marshal one vio_imu_preintegrate-shaped call (shared by the HIP path and the test oracle)."""
+    imu = samples if getattr(samples, "dtype", None) == abi.IMU_DTYPE else abi.imu_array(samples)
+    imu = np.ascontiguousarray(imu)
+    t0 = np.ascontiguousarray(t_start, dtype=np.float64).reshape(-1)
+    t1 = np.ascontiguousarray(t_end, dtype=np.float64).reshape(-1)
+    if t0.shape != t1.shape:
+        raise ValueError("t_start / t_end sizes differ")
+    n = len(t0)
+    bg = None if gyro_bias is None else np.ascontiguousarray(np.broadcast_to(np.asarray(gyro_bias, np.float32), (n, 3)))
+    ba = None if accel_bias is None else np.ascontiguousarray(np.broadcast_to(np.asarray(accel_bias, np.float32), (n, 3)))
+    out = (abi.VioPreint * max(n, 1))()
+    valid = np.zeros(max(n, 1), np.uint8)
+    cov_bias = np.zeros((max(n, 1), 6), np.float32)
+    nz = abi.imu_noise(noise)
+    rc = fn(_p(imu), len(imu), _p(t0), _p(t1), n, None if bg is None else _p(bg), None if ba is None else _p(ba),
+            C.byref(nz), C.cast(out, C.c_void_p), _p(valid), _p(cov_bias))
+    check(rc, "vio_imu_preintegrate")
+    rec = abi.preint_records(out)
+    return {k: v[:n] for k, v in rec.items()}, valid[:n], cov_bias[:n]
 
 
 def _u8img(a):

@@ -237,3 +237,56 @@ class BaOutput:
             "num_inliers": s.num_inliers, "num_outliers": s.num_outliers, "num_bad_lm": s.num_bad_lm,
             "initial_cost": s.initial_cost, "final_cost": s.final_cost, "fixed_cost": s.fixed_cost,
         }
+
+
+# ---------------------------------------------------------------------------------------------
+# IMU preintegration (vio_imu_preintegrate)
+class VioImuData(C.Structure):
+    """IMUData (src/processing/Estimator.h:32-36)."""
+    _fields_ = [("timestamp", C.c_double), ("ax", C.c_float), ("ay", C.c_float), ("az", C.c_float),
+                ("gx", C.c_float), ("gy", C.c_float), ("gz", C.c_float)]
+
+
+class VioImuNoise(C.Structure):
+    _fields_ = [("gyro_noise", C.c_float), ("accel_noise", C.c_float), ("gyro_bias_noise", C.c_float),
+                ("accel_bias_noise", C.c_float)]
+
+
+IMU_DTYPE = np.dtype({"names": ["timestamp", "ax", "ay", "az", "gx", "gy", "gz"],
+                      "formats": ["<f8"] + ["<f4"] * 6, "offsets": [0, 8, 12, 16, 20, 24, 28],
+                      "itemsize": C.sizeof(VioImuData)})
+PREINT_FIELDS = (("delta_R", (3, 3)), ("delta_V", (3,)), ("delta_P", (3,)), ("J_Rg", (3, 3)), ("J_Vg", (3, 3)),
+                 ("J_Va", (3, 3)), ("J_Pg", (3, 3)), ("J_Pa", (3, 3)), ("cov9", (9, 9)), ("gyro_bias", (3,)),
+                 ("accel_bias", (3,)))
+
+
+def imu_array(samples):
+    """(M, 7) array of [t, ax, ay, az, gx, gy, gz] (synth.imu_samples layout) -> vio_imu_data records."""
+    s = np.asarray(samples, dtype=np.float64).reshape(-1, 7)
+    out = np.zeros(len(s), IMU_DTYPE)
+    out["timestamp"] = s[:, 0]
+    for k, name in enumerate(("ax", "ay", "az", "gx", "gy", "gz")):
+        out[name] = s[:, 1 + k].astype(np.float32)
+    return out
+
+
+def imu_noise(noise=None):
+    """VioImuNoise from a (gyro, accel, gyro_bias, accel_bias) tuple; None = the reference defaults."""
+    if noise is None:
+        noise = (1.0e-4, 1.0e-3, 1.0e-6, 1.0e-5)
+    return VioImuNoise(*[float(x) for x in noise])
+
+
+def preint_records(out):
+    """(VioPreint * n) -> dict of stacked numpy arrays (n, ...) keyed by the IMUPreintegration fields."""
+    n = len(out)
+    flat = np.frombuffer(out, dtype=np.uint8).reshape(n, C.sizeof(VioPreint)) if n else np.zeros((0, C.sizeof(VioPreint)), np.uint8)
+    res = {}
+    for name, shape in PREINT_FIELDS:
+        off = getattr(VioPreint, name).offset
+        cnt = int(np.prod(shape))
+        res[name] = flat[:, off:off + 4 * cnt].copy().view(np.float32).reshape((n,) + shape)
+    off = VioPreint.dt_total.offset
+    res["dt_total"] = flat[:, off:off + 8].copy().view(np.float64).reshape(n)
+    return res
+

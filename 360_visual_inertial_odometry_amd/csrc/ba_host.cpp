@@ -468,6 +468,8 @@ void vio_ctx_destroy(vio_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     for (void* p : ctx->bufs)
         if (p) (void)hipFree(p);
+    for (hipEvent_t e : ctx->imu_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

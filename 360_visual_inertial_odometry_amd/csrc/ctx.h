@@ -14,6 +14,9 @@ struct vio_ctx {
     // grow-only device buffers keyed by slot
     std::vector<void*> bufs;
     std::vector<size_t> caps;
+    // IMU preintegration kernel timing (created on first use)
+    hipEvent_t imu_ev[2] = {nullptr, nullptr};
+    float imu_ms = -1.f;
 };
 
 namespace vio360 {
@@ -22,6 +25,8 @@ void set_error(vio_ctx* ctx, const std::string& msg);
 int hip_fail(vio_ctx* ctx, hipError_t e, const char* what);
 // device buffer of at least `bytes` for slot `slot` (contents undefined); nullptr on failure
 void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes);
+// scratch slots owned by vio_imu_preintegrate
+enum { kSlotImuData = 8, kSlotImuIntervals = 9, kSlotImuOut = 10 };
 
 #define VIO_HIP(ctx, expr)                                  \
     do {                                                    \

@@ -1,0 +1,324 @@
+// imu_preint.hip — IMU preintegration on device, the producer of the
+// InertialFactorFixedGravity inputs (vio_preint).
+//
+// Reference: IMUPreintegrator::Preintegrate / IntegrateMeasurement / UpdateCovariance
+// (src/processing/IMUPreintegrator.cpp:143-274), Rodrigues / RightJacobian / SkewSymmetric
+// (:313-356).  All arithmetic is f32 as in the reference (Eigen::Matrix3f); dt_total is the f64
+// accumulator of f32 steps.  Compiled with -ffp-contract=off so every expression rounds as written:
+// 3x3 products sum k = 0, 1, 2 in order, scalar factors are applied after the product, sin / cos of
+// the rotation angle are the correctly rounded f32 values (f64 evaluation rounded once), which is
+// what oracle/imu_oracle.c computes — the parity test is bitwise.
+//
+// Layout: one lane per interval (a keyframe pair).  An interval is a strictly sequential chain of
+// ~50 steps at 200 Hz / 4 Hz keyframes, so the parallelism is across intervals (every window of a
+// batch, every keyframe pair); the state (ΔR, ΔV, ΔP, five 3x3 Jacobians, the 9x9 covariance and
+// the bias-walk diagonal: 147 floats) lives in registers.  The 9x9 sandwich A·C·Aᵀ + B·N·Bᵀ of
+// UpdateCovariance is evaluated on its non-zero pattern only (A = I + dt·E₆₃, B non-zero in
+// columns 3..5); the dropped terms are exact zeros, so the result equals the dense product
+// summed in index order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ctx.h"
+
+using namespace vio360;
+
+namespace {
+
+struct ImuInterval {
+    double t0, t1;
+    float bg[3], ba[3];
+};
+
+struct ImuArgs {
+    const vio_imu_data* imu;
+    int n_imu;
+    const ImuInterval* iv;
+    int n;
+    vio_imu_noise noise;
+    vio_preint* out;
+    float* cov_bias;   // n*6
+    uint8_t* valid;    // n
+};
+
+__device__ __forceinline__ void mm3(const float* A, const float* B, float* C) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) C[3 * i + j] = (A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j]) + A[3 * i + 2] * B[6 + j];
+}
+
+// Aᵀ·B
+__device__ __forceinline__ void mtm3(const float* A, const float* B, float* C) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) C[3 * i + j] = (A[i] * B[j] + A[3 + i] * B[3 + j]) + A[6 + i] * B[6 + j];
+}
+
+__device__ __forceinline__ void mv3(const float* A, const float* v, float* o) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[i] = (A[3 * i] * v[0] + A[3 * i + 1] * v[1]) + A[3 * i + 2] * v[2];
+}
+
+__device__ __forceinline__ void skew3(const float* v, float* S) {
+    S[0] = 0.f;   S[1] = -v[2]; S[2] = v[1];
+    S[3] = v[2];  S[4] = 0.f;   S[5] = -v[0];
+    S[6] = -v[1]; S[7] = v[0];  S[8] = 0.f;
+}
+
+// Rodrigues (:321-336) and RightJacobian (:338-354) of the same ω·dt
+__device__ __forceinline__ void rodrigues_jr(const float* w, float* R, float* Jr) {
+    // sqrtf is correctly rounded here; __fsqrt_rn is not on this toolchain (tools/probe/imu_math_probe.hip:
+    // 15 % of 1M arguments differ from the IEEE result)
+    const float th = sqrtf((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2]);
+    if (th < 1e-6f) {
+        float S[9];
+        skew3(w, S);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const float id = (i % 4 == 0) ? 1.f : 0.f;
+            R[i] = id + S[i];
+            Jr[i] = id - 0.5f * S[i];
+        }
+        return;
+    }
+    const float ax[3] = {w[0] / th, w[1] / th, w[2] / th};
+    float K[9], KK[9];
+    skew3(ax, K);
+    mm3(K, K, KK);
+    const float s = (float)sin((double)th), c = (float)cos((double)th);
+    const float a = 1.f - c, b = (1.f - c) / th, d = (th - s) / th;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const float id = (i % 4 == 0) ? 1.f : 0.f;
+        R[i] = (id + s * K[i]) + a * KK[i];
+        Jr[i] = (id - b * K[i]) + d * KK[i];
+    }
+}
+
+__global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const ImuInterval iv = a.iv[i];
+    // filtered range [lo, hi): first timestamp >= t0, first timestamp >= t1 (sorted input)
+    int lo = 0, hi = a.n_imu;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (a.imu[m].timestamp < iv.t0) lo = m + 1; else hi = m;
+    }
+    int e = lo;
+    hi = a.n_imu;
+    while (e < hi) {
+        const int m = (e + hi) >> 1;
+        if (a.imu[m].timestamp < iv.t1) e = m + 1; else hi = m;
+    }
+    const int cnt = e - lo;
+    vio_preint* o = a.out + i;
+    if (cnt <= 0) {  // Preintegrate returns nullptr (:165-169)
+        float* of = reinterpret_cast<float*>(o);
+        for (int k = 0; k < (int)(sizeof(vio_preint) / sizeof(float)); ++k) of[k] = 0.f;
+        for (int k = 0; k < 6; ++k) a.cov_bias[6 * i + k] = 0.f;
+        a.valid[i] = 0;
+        return;
+    }
+    const float gn2 = a.noise.gyro_noise * a.noise.gyro_noise;   // Nga(0..2) never reaches cov9: B's
+    (void)gn2;                                                    // columns 0..2 are zero (:259-263)
+    const float an2 = a.noise.accel_noise * a.noise.accel_noise;
+    const float gbn2 = a.noise.gyro_bias_noise * a.noise.gyro_bias_noise;
+    const float abn2 = a.noise.accel_bias_noise * a.noise.accel_bias_noise;
+
+    float dR[9] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f};
+    float dV[3] = {0.f, 0.f, 0.f}, dP[3] = {0.f, 0.f, 0.f};
+    float JRg[9], JVg[9], JVa[9], JPg[9], JPa[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) JRg[k] = JVg[k] = JVa[k] = JPg[k] = JPa[k] = 0.f;
+    float C[81];
+#pragma unroll
+    for (int k = 0; k < 81; ++k) C[k] = 0.f;
+    float walk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    double dt_total = 0.0;
+
+    double t_prev = a.imu[lo].timestamp;
+    for (int s = 0; s < cnt; ++s) {
+        const vio_imu_data m = a.imu[lo + s];
+        float dt;
+        if (s == 0) dt = cnt > 1 ? (float)(a.imu[lo + 1].timestamp - m.timestamp) : 0.002f;
+        else dt = (float)(m.timestamp - t_prev);
+        t_prev = m.timestamp;
+        dt = fmaxf(0.0005f, fminf(dt, 0.02f));
+
+        // IntegrateMeasurement (:195-236)
+        const float gyr[3] = {m.gx - iv.bg[0], m.gy - iv.bg[1], m.gz - iv.bg[2]};
+        const float acc[3] = {m.ax - iv.ba[0], m.ay - iv.ba[1], m.az - iv.ba[2]};
+        const float wdt[3] = {gyr[0] * dt, gyr[1] * dt, gyr[2] * dt};
+        float dRi[9], Jr[9], T[9], S[9], U[9];
+        rodrigues_jr(wdt, dRi, Jr);
+        mtm3(dRi, Jr, T);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) JRg[k] = -T[k] * dt;
+        skew3(acc, S);
+        mm3(JVa, S, T);
+        mm3(T, JRg, U);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) JVg[k] = JVg[k] + U[k];
+        mm3(JPa, S, T);
+        mm3(T, JRg, U);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) JPg[k] = (JPg[k] + U[k]) + JVg[k] * dt;
+        float Racc[3];
+        mv3(dR, acc, Racc);  // old ΔR
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            JVa[k] = JVa[k] + dR[k] * dt;
+            JPa[k] = (JPa[k] + JVa[k] * dt) + ((0.5f * dR[k]) * dt) * dt;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float v_old = dV[k];
+            dV[k] = v_old + Racc[k] * dt;
+            dP[k] = dP[k] + (v_old * dt + ((0.5f * Racc[k]) * dt) * dt);
+        }
+        mm3(dR, dRi, T);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) dR[k] = T[k];
+
+        // UpdateCovariance (:238-274) with the updated ΔR.  A·C: rows 6..8 += dt·rows 3..5
+#pragma unroll
+        for (int r = 6; r < 9; ++r)
+#pragma unroll
+            for (int c = 0; c < 9; ++c) C[9 * r + c] = dt * C[9 * (r - 3) + c] + C[9 * r + c];
+        // (A·C)·Aᵀ: columns 6..8 += dt·columns 3..5
+#pragma unroll
+        for (int r = 0; r < 9; ++r)
+#pragma unroll
+            for (int c = 6; c < 9; ++c) C[9 * r + c] = C[9 * r + c - 3] * dt + C[9 * r + c];
+        // B·N·Bᵀ on rows / columns 3..8: B(3+r, 3+c) = ΔR·dt, B(6+r, 3+c) = ((0.5·ΔR)·dt)·dt
+        float Bm[18];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            Bm[k] = dR[k] * dt;
+            Bm[9 + k] = ((0.5f * dR[k]) * dt) * dt;
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            const float M0 = Bm[3 * r] * an2, M1 = Bm[3 * r + 1] * an2, M2 = Bm[3 * r + 2] * an2;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                const float p = (M0 * Bm[3 * c] + M1 * Bm[3 * c + 1]) + M2 * Bm[3 * c + 2];
+                C[9 * (3 + r) + 3 + c] = C[9 * (3 + r) + 3 + c] + p;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            walk[k] = walk[k] + gbn2 * dt;
+            walk[3 + k] = walk[3 + k] + abn2 * dt;
+        }
+        dt_total += (double)dt;
+    }
+
+    for (int k = 0; k < 9; ++k) {
+        o->delta_R[k] = dR[k];
+        o->J_Rg[k] = JRg[k];
+        o->J_Vg[k] = JVg[k];
+        o->J_Va[k] = JVa[k];
+        o->J_Pg[k] = JPg[k];
+        o->J_Pa[k] = JPa[k];
+    }
+    for (int k = 0; k < 3; ++k) {
+        o->delta_V[k] = dV[k];
+        o->delta_P[k] = dP[k];
+        o->gyro_bias[k] = iv.bg[k];
+        o->accel_bias[k] = iv.ba[k];
+    }
+    for (int k = 0; k < 81; ++k) o->cov9[k] = C[k];
+    o->_pad[0] = o->_pad[1] = 0.f;
+    o->dt_total = dt_total;
+    for (int k = 0; k < 6; ++k) a.cov_bias[6 * i + k] = walk[k];
+    a.valid[i] = 1;
+}
+
+size_t align_up(size_t v, size_t al) { return (v + al - 1) / al * al; }
+
+}  // namespace
+
+extern "C" int vio_imu_preintegrate(vio_ctx* ctx, const vio_imu_data* imu, int n_imu, const double* t_start,
+                                    const double* t_end, int n, const float* gyro_bias, const float* accel_bias,
+                                    const vio_imu_noise* noise, vio_preint* out, uint8_t* valid,
+                                    float* cov_bias_diag) {
+    if (!ctx || n < 0 || n_imu < 0 || (n > 0 && (!t_start || !t_end || !out || !valid)) || (n_imu > 0 && !imu))
+        return VIO_EINVAL;
+    for (int k = 1; k < n_imu; ++k)
+        if (!(imu[k].timestamp >= imu[k - 1].timestamp)) {
+            set_error(ctx, "vio_imu_preintegrate: IMU samples not sorted by timestamp");
+            return VIO_EINVAL;
+        }
+    if (n == 0) return VIO_OK;
+    if (n_imu == 0) {  // Preintegrate: empty measurement list → nullptr (:148-151)
+        std::memset(out, 0, sizeof(vio_preint) * (size_t)n);
+        std::memset(valid, 0, (size_t)n);
+        if (cov_bias_diag) std::memset(cov_bias_diag, 0, sizeof(float) * 6 * (size_t)n);
+        return VIO_OK;
+    }
+    std::vector<ImuInterval> iv(n);
+    for (int i = 0; i < n; ++i) {
+        iv[i].t0 = t_start[i];
+        iv[i].t1 = t_end[i];
+        for (int k = 0; k < 3; ++k) {
+            iv[i].bg[k] = gyro_bias ? gyro_bias[3 * i + k] : 0.f;
+            iv[i].ba[k] = accel_bias ? accel_bias[3 * i + k] : 0.f;
+        }
+    }
+    const size_t b_pre = align_up(sizeof(vio_preint) * (size_t)n, 256);
+    const size_t b_cov = align_up(sizeof(float) * 6 * (size_t)n, 256);
+    const size_t b_val = align_up((size_t)n, 256);
+    auto* d_imu = static_cast<vio_imu_data*>(ctx_buffer(ctx, kSlotImuData, sizeof(vio_imu_data) * (size_t)n_imu));
+    auto* d_iv = static_cast<ImuInterval*>(ctx_buffer(ctx, kSlotImuIntervals, sizeof(ImuInterval) * (size_t)n));
+    auto* d_out = static_cast<char*>(ctx_buffer(ctx, kSlotImuOut, b_pre + b_cov + b_val));
+    if (!d_imu || !d_iv || !d_out) {
+        set_error(ctx, "vio_imu_preintegrate: device allocation failed");
+        return VIO_ENOMEM;
+    }
+    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    for (hipEvent_t& ev : ctx->imu_ev)
+        if (!ev) VIO_HIP(ctx, hipEventCreate(&ev));
+    hipStream_t st = ctx->stream;
+    VIO_HIP(ctx, hipMemcpyAsync(d_imu, imu, sizeof(vio_imu_data) * (size_t)n_imu, hipMemcpyHostToDevice, st));
+    VIO_HIP(ctx, hipMemcpyAsync(d_iv, iv.data(), sizeof(ImuInterval) * (size_t)n, hipMemcpyHostToDevice, st));
+    ImuArgs a;
+    a.imu = d_imu;
+    a.n_imu = n_imu;
+    a.iv = d_iv;
+    a.n = n;
+    a.noise = noise ? *noise : vio_imu_noise{1.0e-4f, 1.0e-3f, 1.0e-6f, 1.0e-5f};
+    a.out = reinterpret_cast<vio_preint*>(d_out);
+    a.cov_bias = reinterpret_cast<float*>(d_out + b_pre);
+    a.valid = reinterpret_cast<uint8_t*>(d_out + b_pre + b_cov);
+    VIO_HIP(ctx, hipEventRecord(ctx->imu_ev[0], st));
+    hipLaunchKernelGGL(imu_preint_kernel, dim3((n + 63) / 64), dim3(64), 0, st, a);
+    VIO_HIP(ctx, hipGetLastError());
+    VIO_HIP(ctx, hipEventRecord(ctx->imu_ev[1], st));
+    VIO_HIP(ctx, hipMemcpyAsync(out, a.out, sizeof(vio_preint) * (size_t)n, hipMemcpyDeviceToHost, st));
+    VIO_HIP(ctx, hipMemcpyAsync(valid, a.valid, (size_t)n, hipMemcpyDeviceToHost, st));
+    if (cov_bias_diag)
+        VIO_HIP(ctx, hipMemcpyAsync(cov_bias_diag, a.cov_bias, sizeof(float) * 6 * (size_t)n, hipMemcpyDeviceToHost, st));
+    VIO_HIP(ctx, hipStreamSynchronize(st));
+    float ms = -1.f;
+    VIO_HIP(ctx, hipEventElapsedTime(&ms, ctx->imu_ev[0], ctx->imu_ev[1]));
+    ctx->imu_ms = ms;
+    return VIO_OK;
+}
+
+extern "C" int vio_imu_preintegrate_kernel_ms(vio_ctx* ctx, double* ms) {
+    if (!ctx || !ms) return VIO_EINVAL;
+    if (ctx->imu_ms < 0.f) {
+        set_error(ctx, "vio_imu_preintegrate_kernel_ms: no preintegration has run on this context");
+        return VIO_EINVAL;
+    }
+    *ms = ctx->imu_ms;
+    return VIO_OK;
+}

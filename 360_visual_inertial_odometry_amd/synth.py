@@ -266,7 +266,7 @@ def make_window(K=10, L=200, seed=SEED, W=ERP_W, H=ERP_H, noise_px=0.5, rot_sigm
             preint.append(preintegrate(samples, KF_DT * (i - 1), KF_DT * i))
         v_true = np.array([traj_vel(KF_DT * i) for i in range(K)])
         w.update({
-            "preint": preint, "gravity": gravity,
+            "preint": preint, "gravity": gravity, "imu_samples": samples,
             "vel": (v_true + rng.normal(0, 0.05, v_true.shape)).astype(np.float32).astype(np.float64),
             "bg": np.zeros(3), "ba": np.zeros(3), "vel_true": v_true,
         })

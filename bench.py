@@ -222,6 +222,56 @@ def global_ba_bench(vio, synth, ctx, lm_iters):
     }
 
 
+def imu_bench(vio, ctx, steps, cpu_seconds, want_cpu):
+    """IMU preintegration (the producer of the VIBA factors) for config 4's 256 windows
+    x 9 keyframe intervals = 2304 intervals of 50 samples (200 Hz IMU, 4 Hz keyframes) over one
+    sorted 576 s stream (synthetic samples).  value = intervals per second of device kernel time."""
+    rate, kf_dt, n_int = 200.0, 0.25, 256 * 9
+    rng = np.random.default_rng(11)
+    m = int(n_int * kf_dt * rate) + 1
+    s = np.zeros((m, 7))
+    s[:, 0] = np.arange(m) / rate
+    tt = s[:, 0]
+    s[:, 1:4] = np.stack([0.3 * np.sin(tt), 0.2 * np.cos(0.7 * tt), 9.81 + 0.1 * np.sin(2 * tt)], 1) + rng.normal(0, 1e-2, (m, 3))
+    s[:, 4:7] = np.array([0.01, -0.02, 0.14]) + rng.normal(0, 1e-3, (m, 3))
+    imu = vio.abi.imu_array(s)
+    t0 = kf_dt * np.arange(n_int)
+    t1 = t0 + kf_dt
+    for _ in range(3):
+        ctx.imu_preintegrate(imu, t0, t1)
+    kms, t_start = [], time.perf_counter()
+    for _ in range(steps):
+        rec, valid, _ = ctx.imu_preintegrate(imu, t0, t1)
+        kms.append(ctx.imu_kernel_ms())
+    wall = (time.perf_counter() - t_start) / steps
+    assert valid.all()
+    k_ms = float(np.mean(kms))
+    alg_bytes = m * 32 + n_int * (16 + 24 + C.sizeof(vio.abi.VioPreint) + 24 + 1)
+    out = {
+        "metric": "IMU preintegration intervals/s (256 windows x 9 KF intervals, 50 samples each)",
+        "value": n_int / (k_ms * 1e-3),
+        "unit": "intervals/s",
+        "kernel_ms": k_ms,
+        "wall_ms_per_call": wall * 1e3,
+        "note": "value over the HIP-event kernel time; wall includes the 3.7 MB sample upload and result download",
+        "roofline": {"bound": "latency", "achieved": alg_bytes / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                     "frac": alg_bytes / (k_ms * 1e-3) / 8.0e12, "traffic": None,
+                     "note": "one lane per interval: a 50-step dependent f32 chain; 2304 lanes = 36 waves"},
+        "cpu_baseline": None,
+    }
+    if want_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        reps, t_start = 0, time.perf_counter()
+        while time.perf_counter() - t_start < cpu_seconds:
+            oracle_lib.imu_preintegrate(vio, imu, t0, t1)
+            reps += 1
+        cpu_s = (time.perf_counter() - t_start) / reps
+        out["cpu_baseline"] = {"value": n_int / cpu_s, "unit": "intervals/s", "cores": 1, "kind": "port",
+                               "sample": f"{reps} x 2304 intervals through oracle/imu_oracle.c (1 thread)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -234,6 +284,7 @@ def main():
     ap.add_argument("--no-klt", action="store_true")
     ap.add_argument("--klt-steps", type=int, default=20)
     ap.add_argument("--no-global", action="store_true")
+    ap.add_argument("--no-imu", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -300,6 +351,8 @@ def main():
         gba = None if args.no_global else global_ba_bench(vio, synth, ctx, args.lm_iters)
         klt = None if args.no_klt else klt_bench(vio, synth, ctx, args.klt_steps, 3, args.cpu_seconds,
                                                  not args.no_cpu_baseline and world == 1)
+        imu = None if args.no_imu else imu_bench(vio, ctx, 20, min(args.cpu_seconds, 3.0),
+                                                 not args.no_cpu_baseline and world == 1)
         single_ips = args.lm_iters / single_wall
         out = {
             "metric": "sliding-window BA iters/sec (10KF x 500pts)",
@@ -343,6 +396,7 @@ def main():
             "cpu_baseline": cpu,
             "erp_klt": klt,
             "global_ba": gba,
+            "imu_preint": imu,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -285,6 +285,38 @@ int erp_frontend_features(erp_frontend* f, int32_t* ids, float* xy, int32_t* tra
 int erp_frontend_stats(erp_frontend* f, int* num_tracked, int* num_detected);
 void erp_frontend_destroy(erp_frontend* f);
 
+/* ------------------------------------------------------------------------------------------ */
+/* IMU preintegration: the producer of vio_preint, on device.                   */
+
+/* IMUData (src/processing/Estimator.h:32-36) */
+typedef struct {
+    double timestamp;         /* seconds */
+    float ax, ay, az;         /* m/s^2 */
+    float gx, gy, gz;         /* rad/s */
+} vio_imu_data;
+
+/* IMUPreintegrator noise densities (IMUPreintegrator.cpp:64-67 defaults 1e-4, 1e-3, 1e-6, 1e-5;
+   SetNoiseParameters :131-140) */
+typedef struct {
+    float gyro_noise, accel_noise, gyro_bias_noise, accel_bias_noise;
+} vio_imu_noise;
+
+/*
+ * IMUPreintegrator::Preintegrate (src/processing/IMUPreintegrator.cpp:143-193, with
+ * IntegrateMeasurement :195-236 and UpdateCovariance :238-274) for n intervals in one launch:
+ * interval i integrates the samples with t_start[i] <= timestamp < t_end[i] under the biases
+ * gyro_bias[3i..], accel_bias[3i..] (the preintegrator's m_gyro_bias / m_accel_bias; NULL = 0).
+ * imu[] must be sorted by non-decreasing timestamp (VIO_EINVAL otherwise).  valid[i] = 0 where
+ * the reference returns nullptr (no sample in range; out[i] is then zeroed).  cov_bias_diag
+ * (n*6, may be NULL) receives covariance(9..14, 9..14)'s diagonal, the random-walk block.
+ * noise NULL = the reference defaults.  Blocking; out / valid / cov_bias_diag are host buffers.
+ */
+int vio_imu_preintegrate(vio_ctx* ctx, const vio_imu_data* imu, int n_imu, const double* t_start,
+                         const double* t_end, int n, const float* gyro_bias, const float* accel_bias,
+                         const vio_imu_noise* noise, vio_preint* out, uint8_t* valid, float* cov_bias_diag);
+/* device time (ms) of the last vio_imu_preintegrate kernel on this context (HIP events) */
+int vio_imu_preintegrate_kernel_ms(vio_ctx* ctx, double* ms);
+
 #ifdef __cplusplus
 }
 #endif

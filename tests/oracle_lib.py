@@ -22,6 +22,8 @@ def load():
         subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
     L = C.CDLL(so)
     L.oracle_ba_solve.argtypes = [C.c_void_p, C.c_void_p]
+    vp = C.c_void_p
+    L.oracle_imu_preintegrate.argtypes = [vp, C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -34,6 +36,16 @@ def ba_solve(vio, prob):
     if rc != 0:
         raise RuntimeError(f"oracle_ba_solve rc={rc}")
     return O.result()
+
+
+def imu_preintegrate(vio, samples, t_start, t_end, gyro_bias=None, accel_bias=None, noise=None):
+    """oracle/imu_oracle.c through the same marshalling as Context.imu_preintegrate."""
+    L = load()
+
+    def check(rc, what):
+        if rc != 0:
+            raise RuntimeError(f"oracle {what} rc={rc}")
+    return vio._imu_call(L.oracle_imu_preintegrate, check, samples, t_start, t_end, gyro_bias, accel_bias, noise)
 
 
 def _p(a):

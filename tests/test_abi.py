@@ -40,6 +40,8 @@ STRUCTS = {
                                         "max_iterations", "fixed_iterations", "num_rounds"]),
     "vio_ba_summary": ("VioBaSummary", ["success", "num_bad_lm", "initial_cost", "fixed_cost"]),
     "vio_ba_output": ("VioBaOutput", ["T_wb", "lm_xyz", "obs_outlier", "summary"]),
+    "vio_imu_data": ("VioImuData", ["timestamp", "ax", "az", "gx", "gz"]),
+    "vio_imu_noise": ("VioImuNoise", ["gyro_noise", "accel_bias_noise"]),
     "erp_klt_params": ("ErpKltParams", ["win", "max_level", "epsilon", "min_eig_threshold"]),
     "erp_tracker_params": ("ErpTrackerParams", ["ransac_iters", "ransac_seed", "quality", "min_dist",
                                                 "boundary_margin", "polar_ratio"]),
