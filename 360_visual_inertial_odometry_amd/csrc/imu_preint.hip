@@ -9,10 +9,11 @@
 // the rotation angle are the correctly rounded f32 values (f64 evaluation rounded once), which is
 // what oracle/imu_oracle.c computes — the parity test is bitwise.
 //
-// Layout: one lane per interval (a keyframe pair).  An interval is a strictly sequential chain of
+// Layout: nine lanes per interval (a keyframe pair).  An interval is a strictly sequential chain of
 // ~50 steps at 200 Hz / 4 Hz keyframes, so the parallelism is across intervals (every window of a
-// batch, every keyframe pair); the state (ΔR, ΔV, ΔP, five 3x3 Jacobians, the 9x9 covariance and
-// the bias-walk diagonal: 147 floats) lives in registers.  The 9x9 sandwich A·C·Aᵀ + B·N·Bᵀ of
+// batch, every keyframe pair) and, inside one, across the covariance: each lane owns one position
+// of the 3x3-block structure of the 9x9 covariance (9 entries), the ΔR / ΔV / ΔP / Jacobian chain
+// is evaluated by all nine; everything stays in registers.  The 9x9 sandwich A·C·Aᵀ + B·N·Bᵀ of
 // UpdateCovariance is evaluated on its non-zero pattern only (A = I + dt·E₆₃, B non-zero in
 // columns 3..5); the dropped terms are exact zeros, so the result equals the dense product
 // summed in index order.
@@ -28,6 +29,9 @@
 using namespace vio360;
 
 namespace {
+
+constexpr int kLanesPerInterval = 9;
+constexpr int kIntervalsPerBlock = 64 / kLanesPerInterval;  // 7
 
 struct ImuInterval {
     double t0, t1;
@@ -102,8 +106,15 @@ __device__ __forceinline__ void rodrigues_jr(const float* w, float* R, float* Jr
 }
 
 __global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
+    // 9 lanes per interval (7 intervals per wave, lane 63 idle); lane q = 3·bi + bj owns the
+    // covariance entries C(bi + 3·u, bj + 3·v), u, v = 0..2 — the closure of UpdateCovariance's
+    // dependencies (row block 2 += dt·row block 1, column block 2 += dt·column block 1, B·N·Bᵀ on
+    // blocks 1..2), so the lanes never exchange data.  The 3x3 chain (ΔR, ΔV, ΔP, Jacobians) is
+    // evaluated redundantly by the 9 lanes; lane 0 writes it.
+    const int g = threadIdx.x / kLanesPerInterval, q = threadIdx.x % kLanesPerInterval;
+    const int i = blockIdx.x * kIntervalsPerBlock + g;
+    if (g >= kIntervalsPerBlock || i >= a.n) return;
+    const int bi = q / 3, bj = q % 3;
     const ImuInterval iv = a.iv[i];
     // filtered range [lo, hi): first timestamp >= t0, first timestamp >= t1 (sorted input)
     int lo = 0, hi = a.n_imu;
@@ -120,10 +131,12 @@ __global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
     const int cnt = e - lo;
     vio_preint* o = a.out + i;
     if (cnt <= 0) {  // Preintegrate returns nullptr (:165-169)
-        float* of = reinterpret_cast<float*>(o);
-        for (int k = 0; k < (int)(sizeof(vio_preint) / sizeof(float)); ++k) of[k] = 0.f;
-        for (int k = 0; k < 6; ++k) a.cov_bias[6 * i + k] = 0.f;
-        a.valid[i] = 0;
+        if (q == 0) {
+            float* of = reinterpret_cast<float*>(o);
+            for (int k = 0; k < (int)(sizeof(vio_preint) / sizeof(float)); ++k) of[k] = 0.f;
+            for (int k = 0; k < 6; ++k) a.cov_bias[6 * i + k] = 0.f;
+            a.valid[i] = 0;
+        }
         return;
     }
     const float gn2 = a.noise.gyro_noise * a.noise.gyro_noise;   // Nga(0..2) never reaches cov9: B's
@@ -137,17 +150,21 @@ __global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
     float JRg[9], JVg[9], JVa[9], JPg[9], JPa[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) JRg[k] = JVg[k] = JVa[k] = JPg[k] = JPa[k] = 0.f;
-    float C[81];
+    float C[9];  // C[3u + v] = cov(bi + 3u, bj + 3v)
 #pragma unroll
-    for (int k = 0; k < 81; ++k) C[k] = 0.f;
+    for (int k = 0; k < 9; ++k) C[k] = 0.f;
     float walk[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     double dt_total = 0.0;
 
+    // samples s and s+1 in registers, s+2 loaded at the top of step s (its latency hides behind the
+    // step's arithmetic instead of stalling the next step)
     double t_prev = a.imu[lo].timestamp;
+    vio_imu_data m = a.imu[lo];
+    vio_imu_data m_next = a.imu[lo + (cnt > 1 ? 1 : 0)];
     for (int s = 0; s < cnt; ++s) {
-        const vio_imu_data m = a.imu[lo + s];
+        const vio_imu_data m_pre = a.imu[lo + min(s + 2, cnt - 1)];
         float dt;
-        if (s == 0) dt = cnt > 1 ? (float)(a.imu[lo + 1].timestamp - m.timestamp) : 0.002f;
+        if (s == 0) dt = cnt > 1 ? (float)(m_next.timestamp - m.timestamp) : 0.002f;
         else dt = (float)(m.timestamp - t_prev);
         t_prev = m.timestamp;
         dt = fmaxf(0.0005f, fminf(dt, 0.02f));
@@ -187,30 +204,32 @@ __global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
 #pragma unroll
         for (int k = 0; k < 9; ++k) dR[k] = T[k];
 
-        // UpdateCovariance (:238-274) with the updated ΔR.  A·C: rows 6..8 += dt·rows 3..5
+        // UpdateCovariance (:238-274) with the updated ΔR.  A·C: row block 2 += dt·row block 1
 #pragma unroll
-        for (int r = 6; r < 9; ++r)
+        for (int v = 0; v < 3; ++v) C[6 + v] = dt * C[3 + v] + C[6 + v];
+        // (A·C)·Aᵀ: column block 2 += dt·column block 1
 #pragma unroll
-            for (int c = 0; c < 9; ++c) C[9 * r + c] = dt * C[9 * (r - 3) + c] + C[9 * r + c];
-        // (A·C)·Aᵀ: columns 6..8 += dt·columns 3..5
+        for (int u = 0; u < 3; ++u) C[3 * u + 2] = C[3 * u + 1] * dt + C[3 * u + 2];
+        // B·N·Bᵀ on blocks 1..2: B(3+r, 3+c) = ΔR·dt, B(6+r, 3+c) = ((0.5·ΔR)·dt)·dt.  The lane needs
+        // B rows bi (block 1), 3+bi (block 2) and bj, 3+bj; ΔR rows picked by selects (a per-lane
+        // index into a register array would become a waterfall loop)
+        float Bi[2][3], Bj[2][3];
 #pragma unroll
-        for (int r = 0; r < 9; ++r)
-#pragma unroll
-            for (int c = 6; c < 9; ++c) C[9 * r + c] = C[9 * r + c - 3] * dt + C[9 * r + c];
-        // B·N·Bᵀ on rows / columns 3..8: B(3+r, 3+c) = ΔR·dt, B(6+r, 3+c) = ((0.5·ΔR)·dt)·dt
-        float Bm[18];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            Bm[k] = dR[k] * dt;
-            Bm[9 + k] = ((0.5f * dR[k]) * dt) * dt;
+        for (int k = 0; k < 3; ++k) {
+            const float ri = bi == 0 ? dR[k] : (bi == 1 ? dR[3 + k] : dR[6 + k]);
+            const float rj = bj == 0 ? dR[k] : (bj == 1 ? dR[3 + k] : dR[6 + k]);
+            Bi[0][k] = ri * dt;
+            Bi[1][k] = ((0.5f * ri) * dt) * dt;
+            Bj[0][k] = rj * dt;
+            Bj[1][k] = ((0.5f * rj) * dt) * dt;
         }
 #pragma unroll
-        for (int r = 0; r < 6; ++r) {
-            const float M0 = Bm[3 * r] * an2, M1 = Bm[3 * r + 1] * an2, M2 = Bm[3 * r + 2] * an2;
+        for (int u = 1; u < 3; ++u) {
+            const float M0 = Bi[u - 1][0] * an2, M1 = Bi[u - 1][1] * an2, M2 = Bi[u - 1][2] * an2;
 #pragma unroll
-            for (int c = 0; c < 6; ++c) {
-                const float p = (M0 * Bm[3 * c] + M1 * Bm[3 * c + 1]) + M2 * Bm[3 * c + 2];
-                C[9 * (3 + r) + 3 + c] = C[9 * (3 + r) + 3 + c] + p;
+            for (int v = 1; v < 3; ++v) {
+                const float p = (M0 * Bj[v - 1][0] + M1 * Bj[v - 1][1]) + M2 * Bj[v - 1][2];
+                C[3 * u + v] = C[3 * u + v] + p;
             }
         }
 #pragma unroll
@@ -219,8 +238,15 @@ __global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
             walk[3 + k] = walk[3 + k] + abn2 * dt;
         }
         dt_total += (double)dt;
+        m = m_next;
+        m_next = m_pre;
     }
 
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) o->cov9[9 * (bi + 3 * u) + bj + 3 * v] = C[3 * u + v];
+    if (q != 0) return;
     for (int k = 0; k < 9; ++k) {
         o->delta_R[k] = dR[k];
         o->J_Rg[k] = JRg[k];
@@ -235,7 +261,6 @@ __global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
         o->gyro_bias[k] = iv.bg[k];
         o->accel_bias[k] = iv.ba[k];
     }
-    for (int k = 0; k < 81; ++k) o->cov9[k] = C[k];
     o->_pad[0] = o->_pad[1] = 0.f;
     o->dt_total = dt_total;
     for (int k = 0; k < 6; ++k) a.cov_bias[6 * i + k] = walk[k];
@@ -299,7 +324,7 @@ extern "C" int vio_imu_preintegrate(vio_ctx* ctx, const vio_imu_data* imu, int n
     a.cov_bias = reinterpret_cast<float*>(d_out + b_pre);
     a.valid = reinterpret_cast<uint8_t*>(d_out + b_pre + b_cov);
     VIO_HIP(ctx, hipEventRecord(ctx->imu_ev[0], st));
-    hipLaunchKernelGGL(imu_preint_kernel, dim3((n + 63) / 64), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(imu_preint_kernel, dim3((n + kIntervalsPerBlock - 1) / kIntervalsPerBlock), dim3(64), 0, st, a);
     VIO_HIP(ctx, hipGetLastError());
     VIO_HIP(ctx, hipEventRecord(ctx->imu_ev[1], st));
     VIO_HIP(ctx, hipMemcpyAsync(out, a.out, sizeof(vio_preint) * (size_t)n, hipMemcpyDeviceToHost, st));
