@@ -29,6 +29,7 @@ EXPORTS = [
     "erp_tracker_run", "erp_tracker_sync", "erp_tracker_download", "erp_tracker_stage_ms",
     "erp_tracker_destroy", "erp_frontend_create", "erp_frontend_track", "erp_frontend_features",
     "erp_frontend_stats", "erp_frontend_destroy", "vio_imu_preintegrate", "vio_imu_preintegrate_kernel_ms",
+    "vio_triangulate", "vio_triangulate_device", "vio_triangulate_kernel_ms",
 ]
 
 
@@ -83,6 +84,9 @@ def lib():
     L.vio_imu_preintegrate.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, vp, vp, C.POINTER(abi.VioImuNoise), vp,
                                        vp, vp]
     L.vio_imu_preintegrate_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    L.vio_triangulate.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp]
+    L.vio_triangulate_device.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp]
+    L.vio_triangulate_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
     _lib = L
     return L
 
@@ -142,6 +146,34 @@ class Context:
     def imu_kernel_ms(self):
         ms = C.c_double()
         self.check(lib().vio_imu_preintegrate_kernel_ms(self.h, C.byref(ms)), "vio_imu_preintegrate_kernel_ms")
+        return ms.value
+
+    # ---- two-view triangulation ----
+    def triangulate(self, T_cw, pairs, bearings, width):
+        """Estimator::TriangulateSinglePoint for n candidates: T_cw (m,4,4) world-to-camera f32,
+        pairs (n,2) pose indices, bearings (n,6) = (b1, b2).  Returns (points (n,3) f32,
+        valid (n,) u8, pixel_err (n,2) f32)."""
+        T = np.ascontiguousarray(T_cw, dtype=np.float32).reshape(-1, 16)
+        P = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
+        B = np.ascontiguousarray(bearings, dtype=np.float32).reshape(-1, 6)
+        if len(P) != len(B):
+            raise ValueError("pairs / bearings sizes differ")
+        n = len(P)
+        X = np.zeros((max(n, 1), 3), np.float32)
+        V = np.zeros(max(n, 1), np.uint8)
+        E = np.zeros((max(n, 1), 2), np.float32)
+        self.check(lib().vio_triangulate(self.h, _p(T), len(T), _p(P), _p(B), n, int(width), _p(X), _p(V), _p(E)),
+                   "vio_triangulate")
+        return X[:n], V[:n], E[:n]
+
+    def triangulate_device(self, T_ptr, n_poses, pair_ptr, bear_ptr, n, width, x_ptr, valid_ptr, err_ptr=None):
+        """vio_triangulate_device on raw device pointers (ints), async on the context stream."""
+        self.check(lib().vio_triangulate_device(self.h, T_ptr, n_poses, pair_ptr, bear_ptr, n, int(width), x_ptr,
+                                                valid_ptr, err_ptr), "vio_triangulate_device")
+
+    def triangulate_kernel_ms(self):
+        ms = C.c_double()
+        self.check(lib().vio_triangulate_kernel_ms(self.h, C.byref(ms)), "vio_triangulate_kernel_ms")
         return ms.value
 
     # ---- ERP feature tracking ----

@@ -470,6 +470,8 @@ void vio_ctx_destroy(vio_ctx* ctx) {
         if (p) (void)hipFree(p);
     for (hipEvent_t e : ctx->imu_ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->tri_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -17,6 +17,8 @@ struct vio_ctx {
     // IMU preintegration kernel timing (created on first use)
     hipEvent_t imu_ev[2] = {nullptr, nullptr};
     float imu_ms = -1.f;
+    // triangulation kernel timing (created on first use)
+    hipEvent_t tri_ev[2] = {nullptr, nullptr};
 };
 
 namespace vio360 {
@@ -27,6 +29,8 @@ int hip_fail(vio_ctx* ctx, hipError_t e, const char* what);
 void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes);
 // scratch slots owned by vio_imu_preintegrate
 enum { kSlotImuData = 8, kSlotImuIntervals = 9, kSlotImuOut = 10 };
+// scratch slots owned by vio_triangulate
+enum { kSlotTriIn = 11, kSlotTriOut = 12 };
 
 #define VIO_HIP(ctx, expr)                                  \
     do {                                                    \

@@ -317,6 +317,29 @@ int vio_imu_preintegrate(vio_ctx* ctx, const vio_imu_data* imu, int n_imu, const
 /* device time (ms) of the last vio_imu_preintegrate kernel on this context (HIP events) */
 int vio_imu_preintegrate_kernel_ms(vio_ctx* ctx, double* ms);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Two-view triangulation: Estimator::TriangulateSinglePoint                   */
+/* (src/processing/Estimator.cpp:1082-1137) for n candidates in one launch.                   */
+
+/*
+ * T_cw: n_poses world-to-camera transforms, 4x4 row-major f32 (the reference's
+ * kf->GetTwc().inverse(), Estimator.cpp:1163-1164).  Candidate i triangulates bearings
+ * bearings[6i..6i+2] (in camera pose_pair[2i]) and bearings[6i+3..6i+5] (in camera pose_pair[2i+1])
+ * (Feature::GetBearing, unit f32).  points: 3n f32; valid[i] = TriangulateSinglePoint's return
+ * (|v(3)| >= 1e-10 and a finite point); pixel_err (2n, may be NULL) = the reprojection angle errors
+ * in pixels TriangulateNewMapPoints computes (:1233-1248) with `width` = GetWidth().  Blocking; host
+ * buffers.  The 4x4 SVD is an f64 one-sided Jacobi on the f32-built A (reference: Eigen's f32
+ * JacobiSVD; the null vector is unique up to sign, which the division cancels).
+ */
+int vio_triangulate(vio_ctx* ctx, const float* T_cw, int n_poses, const int32_t* pose_pair, const float* bearings,
+                    int n, int width, float* points, uint8_t* valid, float* pixel_err);
+/* the same on DEVICE buffers, asynchronous on the context stream (no validation of pose_pair) */
+int vio_triangulate_device(vio_ctx* ctx, const float* T_cw, int n_poses, const int32_t* pose_pair,
+                           const float* bearings, int n, int width, float* points, uint8_t* valid,
+                           float* pixel_err);
+/* device time (ms) of the last triangulation kernel on this context (waits for it) */
+int vio_triangulate_kernel_ms(vio_ctx* ctx, double* ms);
+
 #ifdef __cplusplus
 }
 #endif
