@@ -26,9 +26,7 @@
 
 #include "ctx.h"
 
-using namespace vio360;
-
-namespace {
+namespace vio360 {
 
 constexpr int kLanesPerInterval = 9;
 constexpr int kIntervalsPerBlock = 64 / kLanesPerInterval;  // 7
@@ -267,9 +265,11 @@ __global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
     a.valid[i] = 1;
 }
 
-size_t align_up(size_t v, size_t al) { return (v + al - 1) / al * al; }
+static size_t align_up(size_t v, size_t al) { return (v + al - 1) / al * al; }
 
-}  // namespace
+}  // namespace vio360
+
+using namespace vio360;
 
 extern "C" int vio_imu_preintegrate(vio_ctx* ctx, const vio_imu_data* imu, int n_imu, const double* t_start,
                                     const double* t_end, int n, const float* gyro_bias, const float* accel_bias,

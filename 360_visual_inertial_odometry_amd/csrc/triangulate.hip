@@ -24,9 +24,7 @@
 
 #include "ctx.h"
 
-using namespace vio360;
-
-namespace {
+namespace vio360 {
 
 constexpr int kMaxSweeps = 12;
 
@@ -141,7 +139,9 @@ __global__ __launch_bounds__(256) void triangulate_kernel(TriArgs a) {
     }
 }
 
-}  // namespace
+}  // namespace vio360
+
+using namespace vio360;
 
 extern "C" int vio_triangulate_device(vio_ctx* ctx, const float* T_cw, int n_poses, const int32_t* pose_pair,
                                       const float* bearings, int n, int width, float* points, uint8_t* valid,

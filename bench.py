@@ -30,7 +30,7 @@ FP64_PEAK = 78.6e12  # MI355X FP64 vector (= FP64 matrix) peak, AMD spec (SURVEY
 
 TRACKER_KERNELS = ("pyr_down_kernel", "lk_kernel", "ransac_prep_kernel", "ransac_sample_kernel", "ransac_hyp_kernel",
                    "ransac_select_kernel", "gftt_reset_kernel", "gftt_eig_kernel", "gftt_max_kernel", "gftt_hist_kernel",
-                   "gftt_cand_kernel",
+                   "gftt_cand_kernel", "gftt_cut_kernel", "ransac_raw_kernel",
                    "gftt_topk_compact_kernel", "gftt_select_kernel<false>", "gftt_select_kernel<true>",
                    "disc_mask_kernel")
 
@@ -64,6 +64,14 @@ def klt_traffic():
     runs = k["lk_kernel"]["dispatches"]
     return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items()
                if n in TRACKER_KERNELS or n.startswith("rocprim")) / runs  # rocprim: the top-K key sort
+
+
+def kernel_traffic(name):
+    """PMC HBM bytes per launch of one kernel from the committed summary (None when absent)."""
+    k, src = pmc_traffic()
+    if not k or name not in k:
+        return None
+    return k[name]["hbm_bytes_per_launch"]
 
 
 def ba_flops_per_iter(prob):
@@ -255,7 +263,7 @@ def imu_bench(vio, ctx, steps, cpu_seconds, want_cpu):
         "wall_ms_per_call": wall * 1e3,
         "note": "value over the HIP-event kernel time; wall includes the 3.7 MB sample upload and result download",
         "roofline": {"bound": "latency", "achieved": alg_bytes / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": alg_bytes / (k_ms * 1e-3) / 8.0e12, "traffic": None,
+                     "frac": alg_bytes / (k_ms * 1e-3) / 8.0e12, "traffic": kernel_traffic("imu_preint_kernel"),
                      "note": "one lane per interval: a 50-step dependent f32 chain; 2304 lanes = 36 waves"},
         "cpu_baseline": None,
     }
@@ -306,7 +314,7 @@ def tri_bench(vio, ctx, steps, want_cpu):
         "unit": "candidates/s",
         "kernel_ms": k_ms,
         "roofline": {"bound": "hbm", "achieved": alg_bytes / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": alg_bytes / (k_ms * 1e-3) / 8.0e12, "traffic": None,
+                     "frac": alg_bytes / (k_ms * 1e-3) / 8.0e12, "traffic": kernel_traffic("triangulate_kernel"),
                      "note": "53 B per candidate in/out (poses L2-resident); the f64 one-sided Jacobi "
                              "(~2 kFLOP per candidate) is the actual limiter"},
         "cpu_baseline": None,

@@ -28,7 +28,7 @@ def load(pass_dir, counter):
 
 
 def short(name):
-    base = name.split("(")[0]
+    base = name.replace("(anonymous namespace)::", "").split("(")[0]
     return base.replace("void ", "").replace("vio360::", "").strip()
 
 
