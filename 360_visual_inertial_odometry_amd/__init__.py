@@ -28,7 +28,8 @@ EXPORTS = [
     "erp_tracker_upload", "erp_tracker_device_frame", "erp_tracker_swap", "erp_tracker_set_points",
     "erp_tracker_run", "erp_tracker_sync", "erp_tracker_download", "erp_tracker_stage_ms",
     "erp_tracker_destroy", "erp_frontend_create", "erp_frontend_track", "erp_frontend_features",
-    "erp_frontend_stats", "erp_frontend_destroy", "vio_imu_preintegrate", "vio_imu_preintegrate_kernel_ms",
+    "erp_frontend_stats", "erp_frontend_destroy", "vio_imu_preintegrate", "vio_imu_preintegrate_kernel_ms", "vio_imu_preintegrate_device",
+    "vio_ba_batch_set_preint",
     "vio_triangulate", "vio_triangulate_device", "vio_triangulate_kernel_ms",
 ]
 
@@ -84,6 +85,9 @@ def lib():
     L.vio_imu_preintegrate.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, vp, vp, C.POINTER(abi.VioImuNoise), vp,
                                        vp, vp]
     L.vio_imu_preintegrate_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    L.vio_imu_preintegrate_device.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, vp, vp, C.POINTER(abi.VioImuNoise),
+                                              vp, vp, vp]
+    L.vio_ba_batch_set_preint.argtypes = [vp, vp, C.c_int, C.c_int]
     L.vio_triangulate.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp]
     L.vio_triangulate_device.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp]
     L.vio_triangulate_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
@@ -142,6 +146,14 @@ class Context:
         Returns (records dict of (n, ...) arrays, valid (n,) u8, cov_bias_diag (n, 6) f32)."""
         return _imu_call(lambda *a: lib().vio_imu_preintegrate(self.h, *a), self.check, samples, t_start, t_end,
                          gyro_bias, accel_bias, noise)
+
+    def imu_preintegrate_device(self, imu_ptr, n_imu, t0_ptr, t1_ptr, n, out_ptr, valid_ptr, cov_bias_ptr,
+                                gyro_bias_ptr=None, accel_bias_ptr=None, noise=None):
+        """vio_imu_preintegrate_device on raw device pointers (ints), async on the context stream."""
+        nz = abi.imu_noise(noise)
+        self.check(lib().vio_imu_preintegrate_device(self.h, imu_ptr, n_imu, t0_ptr, t1_ptr, n, gyro_bias_ptr,
+                                                     accel_bias_ptr, C.byref(nz), out_ptr, valid_ptr, cov_bias_ptr),
+                   "vio_imu_preintegrate_device")
 
     def imu_kernel_ms(self):
         ms = C.c_double()
@@ -377,6 +389,12 @@ class BaBatch:
 
     def sync(self):
         self.ctx.check(lib().vio_ba_batch_sync(self.h), "vio_ba_batch_sync")
+
+    def set_preint(self, src, count, on_device=False):
+        """vio_ba_batch_set_preint: src = (VioPreint * count) host array or a device pointer (int)."""
+        ptr = src if on_device else C.cast(src, C.c_void_p)
+        self.ctx.check(lib().vio_ba_batch_set_preint(self.h, ptr, int(count), 1 if on_device else 0),
+                       "vio_ba_batch_set_preint")
 
     def kernel_ms(self):
         ms, cnt = C.c_double(), C.c_int()

@@ -512,6 +512,26 @@ int vio_ba_batch_run(vio_ba_batch* b) {
     return launch(ctx, b->dev, true);
 }
 
+int vio_ba_batch_set_preint(vio_ba_batch* b, const vio_preint* src, int count, int on_device) {
+    if (!b || (count > 0 && !src)) return VIO_EINVAL;
+    vio_ctx* ctx = b->ctx;
+    Packed& pk = b->dev.pk;
+    if (count != (int)pk.preint.size()) {
+        set_error(ctx, "vio_ba_batch_set_preint: count must be the batch's total keyframe count");
+        return VIO_EINVAL;
+    }
+    if (count == 0) return VIO_OK;
+    const size_t bytes = sizeof(vio_preint) * (size_t)count;
+    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    if (on_device) {
+        VIO_HIP(ctx, hipMemcpyAsync((void*)b->dev.P.preint, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+        std::memcpy(pk.preint.data(), src, bytes);  // the staging copy outlives the async upload
+        VIO_HIP(ctx, hipMemcpyAsync((void*)b->dev.P.preint, pk.preint.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+    }
+    return VIO_OK;
+}
+
 int vio_ba_batch_sync(vio_ba_batch* b) {
     if (!b) return VIO_EINVAL;
     VIO_HIP(b->ctx, hipStreamSynchronize(b->ctx->stream));

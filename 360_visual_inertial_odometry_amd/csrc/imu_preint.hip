@@ -31,7 +31,7 @@ namespace vio360 {
 constexpr int kLanesPerInterval = 9;
 constexpr int kIntervalsPerBlock = 64 / kLanesPerInterval;  // 7
 
-struct ImuInterval {
+struct ImuInterval {  // one interval's inputs, in registers
     double t0, t1;
     float bg[3], ba[3];
 };
@@ -39,7 +39,10 @@ struct ImuInterval {
 struct ImuArgs {
     const vio_imu_data* imu;
     int n_imu;
-    const ImuInterval* iv;
+    const double* t0;  // n
+    const double* t1;  // n
+    const float* bg;   // n*3 or null (= 0)
+    const float* ba;   // n*3 or null (= 0)
     int n;
     vio_imu_noise noise;
     vio_preint* out;
@@ -113,7 +116,14 @@ __global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
     const int i = blockIdx.x * kIntervalsPerBlock + g;
     if (g >= kIntervalsPerBlock || i >= a.n) return;
     const int bi = q / 3, bj = q % 3;
-    const ImuInterval iv = a.iv[i];
+    ImuInterval iv;
+    iv.t0 = a.t0[i];
+    iv.t1 = a.t1[i];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        iv.bg[k] = a.bg ? a.bg[3 * i + k] : 0.f;
+        iv.ba[k] = a.ba ? a.ba[3 * i + k] : 0.f;
+    }
     // filtered range [lo, hi): first timestamp >= t0, first timestamp >= t1 (sorted input)
     int lo = 0, hi = a.n_imu;
     while (lo < hi) {
@@ -271,6 +281,34 @@ static size_t align_up(size_t v, size_t al) { return (v + al - 1) / al * al; }
 
 using namespace vio360;
 
+static int launch_preint(vio_ctx* ctx, const ImuArgs& a) {
+    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    for (hipEvent_t& ev : ctx->imu_ev)
+        if (!ev) VIO_HIP(ctx, hipEventCreate(&ev));
+    VIO_HIP(ctx, hipEventRecord(ctx->imu_ev[0], ctx->stream));
+    hipLaunchKernelGGL(imu_preint_kernel, dim3((a.n + kIntervalsPerBlock - 1) / kIntervalsPerBlock), dim3(64), 0,
+                       ctx->stream, a);
+    VIO_HIP(ctx, hipGetLastError());
+    VIO_HIP(ctx, hipEventRecord(ctx->imu_ev[1], ctx->stream));
+    ctx->imu_ms = 0.f;  // resolved by vio_imu_preintegrate_kernel_ms
+    return VIO_OK;
+}
+
+static const vio_imu_noise kDefaultNoise = {1.0e-4f, 1.0e-3f, 1.0e-6f, 1.0e-5f};
+
+extern "C" int vio_imu_preintegrate_device(vio_ctx* ctx, const vio_imu_data* imu, int n_imu, const double* t_start,
+                                           const double* t_end, int n, const float* gyro_bias,
+                                           const float* accel_bias, const vio_imu_noise* noise, vio_preint* out,
+                                           uint8_t* valid, float* cov_bias_diag) {
+    if (!ctx || n < 0 || n_imu < 0 || (n > 0 && (!t_start || !t_end || !out || !valid || !cov_bias_diag)) ||
+        (n_imu > 0 && !imu))
+        return VIO_EINVAL;
+    if (n == 0) return VIO_OK;
+    ImuArgs a{imu, n_imu, t_start, t_end, gyro_bias, accel_bias, n, noise ? *noise : kDefaultNoise, out,
+              cov_bias_diag, valid};
+    return launch_preint(ctx, a);
+}
+
 extern "C" int vio_imu_preintegrate(vio_ctx* ctx, const vio_imu_data* imu, int n_imu, const double* t_start,
                                     const double* t_end, int n, const float* gyro_bias, const float* accel_bias,
                                     const vio_imu_noise* noise, vio_preint* out, uint8_t* valid,
@@ -289,61 +327,58 @@ extern "C" int vio_imu_preintegrate(vio_ctx* ctx, const vio_imu_data* imu, int n
         if (cov_bias_diag) std::memset(cov_bias_diag, 0, sizeof(float) * 6 * (size_t)n);
         return VIO_OK;
     }
-    std::vector<ImuInterval> iv(n);
-    for (int i = 0; i < n; ++i) {
-        iv[i].t0 = t_start[i];
-        iv[i].t1 = t_end[i];
-        for (int k = 0; k < 3; ++k) {
-            iv[i].bg[k] = gyro_bias ? gyro_bias[3 * i + k] : 0.f;
-            iv[i].ba[k] = accel_bias ? accel_bias[3 * i + k] : 0.f;
-        }
-    }
+    const size_t b_t = align_up(sizeof(double) * (size_t)n, 256), b_b = align_up(sizeof(float) * 3 * (size_t)n, 256);
     const size_t b_pre = align_up(sizeof(vio_preint) * (size_t)n, 256);
     const size_t b_cov = align_up(sizeof(float) * 6 * (size_t)n, 256);
     const size_t b_val = align_up((size_t)n, 256);
     auto* d_imu = static_cast<vio_imu_data*>(ctx_buffer(ctx, kSlotImuData, sizeof(vio_imu_data) * (size_t)n_imu));
-    auto* d_iv = static_cast<ImuInterval*>(ctx_buffer(ctx, kSlotImuIntervals, sizeof(ImuInterval) * (size_t)n));
+    auto* d_iv = static_cast<char*>(ctx_buffer(ctx, kSlotImuIntervals, 2 * b_t + 2 * b_b));
     auto* d_out = static_cast<char*>(ctx_buffer(ctx, kSlotImuOut, b_pre + b_cov + b_val));
     if (!d_imu || !d_iv || !d_out) {
         set_error(ctx, "vio_imu_preintegrate: device allocation failed");
         return VIO_ENOMEM;
     }
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
-    for (hipEvent_t& ev : ctx->imu_ev)
-        if (!ev) VIO_HIP(ctx, hipEventCreate(&ev));
     hipStream_t st = ctx->stream;
+    VIO_HIP(ctx, hipSetDevice(ctx->device));
     VIO_HIP(ctx, hipMemcpyAsync(d_imu, imu, sizeof(vio_imu_data) * (size_t)n_imu, hipMemcpyHostToDevice, st));
-    VIO_HIP(ctx, hipMemcpyAsync(d_iv, iv.data(), sizeof(ImuInterval) * (size_t)n, hipMemcpyHostToDevice, st));
     ImuArgs a;
     a.imu = d_imu;
     a.n_imu = n_imu;
-    a.iv = d_iv;
+    a.t0 = reinterpret_cast<const double*>(d_iv);
+    a.t1 = reinterpret_cast<const double*>(d_iv + b_t);
+    a.bg = gyro_bias ? reinterpret_cast<const float*>(d_iv + 2 * b_t) : nullptr;
+    a.ba = accel_bias ? reinterpret_cast<const float*>(d_iv + 2 * b_t + b_b) : nullptr;
+    VIO_HIP(ctx, hipMemcpyAsync(d_iv, t_start, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, st));
+    VIO_HIP(ctx, hipMemcpyAsync(d_iv + b_t, t_end, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, st));
+    if (gyro_bias)
+        VIO_HIP(ctx, hipMemcpyAsync(d_iv + 2 * b_t, gyro_bias, sizeof(float) * 3 * (size_t)n, hipMemcpyHostToDevice, st));
+    if (accel_bias)
+        VIO_HIP(ctx, hipMemcpyAsync(d_iv + 2 * b_t + b_b, accel_bias, sizeof(float) * 3 * (size_t)n,
+                                    hipMemcpyHostToDevice, st));
     a.n = n;
-    a.noise = noise ? *noise : vio_imu_noise{1.0e-4f, 1.0e-3f, 1.0e-6f, 1.0e-5f};
+    a.noise = noise ? *noise : kDefaultNoise;
     a.out = reinterpret_cast<vio_preint*>(d_out);
     a.cov_bias = reinterpret_cast<float*>(d_out + b_pre);
     a.valid = reinterpret_cast<uint8_t*>(d_out + b_pre + b_cov);
-    VIO_HIP(ctx, hipEventRecord(ctx->imu_ev[0], st));
-    hipLaunchKernelGGL(imu_preint_kernel, dim3((n + kIntervalsPerBlock - 1) / kIntervalsPerBlock), dim3(64), 0, st, a);
-    VIO_HIP(ctx, hipGetLastError());
-    VIO_HIP(ctx, hipEventRecord(ctx->imu_ev[1], st));
+    int rc = launch_preint(ctx, a);
+    if (rc) return rc;
     VIO_HIP(ctx, hipMemcpyAsync(out, a.out, sizeof(vio_preint) * (size_t)n, hipMemcpyDeviceToHost, st));
     VIO_HIP(ctx, hipMemcpyAsync(valid, a.valid, (size_t)n, hipMemcpyDeviceToHost, st));
     if (cov_bias_diag)
         VIO_HIP(ctx, hipMemcpyAsync(cov_bias_diag, a.cov_bias, sizeof(float) * 6 * (size_t)n, hipMemcpyDeviceToHost, st));
     VIO_HIP(ctx, hipStreamSynchronize(st));
-    float ms = -1.f;
-    VIO_HIP(ctx, hipEventElapsedTime(&ms, ctx->imu_ev[0], ctx->imu_ev[1]));
-    ctx->imu_ms = ms;
     return VIO_OK;
 }
 
 extern "C" int vio_imu_preintegrate_kernel_ms(vio_ctx* ctx, double* ms) {
     if (!ctx || !ms) return VIO_EINVAL;
-    if (ctx->imu_ms < 0.f) {
+    if (ctx->imu_ms < 0.f || !ctx->imu_ev[1]) {
         set_error(ctx, "vio_imu_preintegrate_kernel_ms: no preintegration has run on this context");
         return VIO_EINVAL;
     }
-    *ms = ctx->imu_ms;
+    float f = 0.f;
+    VIO_HIP(ctx, hipEventSynchronize(ctx->imu_ev[1]));
+    VIO_HIP(ctx, hipEventElapsedTime(&f, ctx->imu_ev[0], ctx->imu_ev[1]));
+    *ms = f;
     return VIO_OK;
 }

@@ -171,6 +171,12 @@ typedef struct vio_ba_batch vio_ba_batch;
 int vio_ba_batch_create(vio_ctx* ctx, const vio_ba_problem* probs, int n, vio_ba_batch** out);
 int vio_ba_batch_run(vio_ba_batch* b);          /* async on the context stream */
 int vio_ba_batch_sync(vio_ba_batch* b);
+/* replace the IMU preintegrations of a VIO_BA_VI batch before the next run: src holds the batch's
+   total keyframe count of entries, window after window in creation order (entry k of a window links
+   keyframe k-1 -> k; entry 0 unused), from host (on_device = 0) or device memory (on_device = 1,
+   e.g. the output of vio_imu_preintegrate_device).  The validity pattern given at creation stays
+   in force.  Async on the context stream. */
+int vio_ba_batch_set_preint(vio_ba_batch* b, const vio_preint* src, int count, int on_device);
 int vio_ba_batch_download(vio_ba_batch* b, vio_ba_output* outs);
 /* average device time (ms) of the solver kernel over the runs since the last reset */
 int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count);
@@ -314,7 +320,12 @@ typedef struct {
 int vio_imu_preintegrate(vio_ctx* ctx, const vio_imu_data* imu, int n_imu, const double* t_start,
                          const double* t_end, int n, const float* gyro_bias, const float* accel_bias,
                          const vio_imu_noise* noise, vio_preint* out, uint8_t* valid, float* cov_bias_diag);
-/* device time (ms) of the last vio_imu_preintegrate kernel on this context (HIP events) */
+/* the same on DEVICE buffers (imu, t_start, t_end, biases, out, valid, cov_bias_diag — the last is
+   required here), asynchronous on the context stream; imu must be sorted (not checked) */
+int vio_imu_preintegrate_device(vio_ctx* ctx, const vio_imu_data* imu, int n_imu, const double* t_start,
+                                const double* t_end, int n, const float* gyro_bias, const float* accel_bias,
+                                const vio_imu_noise* noise, vio_preint* out, uint8_t* valid, float* cov_bias_diag);
+/* device time (ms) of the last vio_imu_preintegrate[_device] kernel on this context (waits for it) */
 int vio_imu_preintegrate_kernel_ms(vio_ctx* ctx, double* ms);
 
 /* ------------------------------------------------------------------------------------------ */

@@ -3,6 +3,13 @@ import sys
 
 import pytest
 
+# torch bundles its own HIP runtime: load it before libvio360.so so that both resolve to the same
+# libamdhip64 (loaded the other way round, torch's lazy CUDA init finds no device)
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))

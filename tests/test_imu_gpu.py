@@ -4,6 +4,8 @@ Both evaluate IMUPreintegrator::Preintegrate (src/processing/IMUPreintegrator.cp
 with the same expression order, no FMA contraction and correctly rounded sin / cos, so every f32
 field and dt_total must be identical (compared with ==, so ±0 agree).
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -101,3 +103,71 @@ def test_device_preintegration_feeds_viba(vio, synth, ctx):
     assert g["success"] == o["success"] == 1
     assert np.abs(g["T_wb"][:, :3, 3] - o["T_wb"][:, :3, 3]).max() <= 1e-4
     assert np.abs(g["lm_xyz"] - o["lm_xyz"]).max() <= 1e-3
+
+
+def _as_dicts(rec, K):
+    return [None] + [{"delta_R": rec["delta_R"][k], "delta_V": rec["delta_V"][k], "delta_P": rec["delta_P"][k],
+                      "J_Rg": rec["J_Rg"][k], "J_Vg": rec["J_Vg"][k], "J_Va": rec["J_Va"][k],
+                      "J_Pg": rec["J_Pg"][k], "J_Pa": rec["J_Pa"][k], "cov": np.pad(rec["cov9"][k], ((0, 6), (0, 6))),
+                      "gyro_bias": rec["gyro_bias"][k], "accel_bias": rec["accel_bias"][k],
+                      "dt_total": float(rec["dt_total"][k])} for k in range(1, K)]
+
+
+def test_device_preintegration_chain_into_batch(vio, synth, ctx):
+    """vio_imu_preintegrate_device writes each window's factors straight into device memory,
+    vio_ba_batch_set_preint moves them into a VIBA batch (no host round trip); the solve is bitwise
+    the solve of a batch created with the same factors from the host."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    K, nw = 10, 4
+    ws = [synth.make_window(K=K, L=60, seed=20251230 + w, imu=True) for w in range(nw)]
+    t0 = np.r_[-1.0, synth.KF_DT * np.arange(K - 1)]  # entry 0: empty range -> invalid, unused
+    t1 = np.r_[-1.0, synth.KF_DT * np.arange(1, K)]
+    sz = C.sizeof(vio.abi.VioPreint)
+    d_out = torch.zeros(nw * K * sz, dtype=torch.uint8, device=dev)
+    d_valid = torch.zeros(nw * K, dtype=torch.uint8, device=dev)
+    d_cov = torch.zeros(nw * K * 6, dtype=torch.float32, device=dev)
+    d_t0 = torch.from_numpy(t0).to(dev)
+    d_t1 = torch.from_numpy(t1).to(dev)
+    keep = []
+    host_recs = []
+    for w, win in enumerate(ws):
+        imu = vio.abi.imu_array(win["imu_samples"])
+        d_imu = torch.from_numpy(imu.view(np.uint8).copy()).to(dev)
+        keep.append(d_imu)
+        torch.cuda.synchronize()
+        ctx.imu_preintegrate_device(d_imu.data_ptr(), len(imu), d_t0.data_ptr(), d_t1.data_ptr(), K,
+                                    d_out.data_ptr() + w * K * sz, d_valid.data_ptr() + w * K,
+                                    d_cov.data_ptr() + w * K * 24)
+        ctx.imu_kernel_ms()  # waits
+        rec, valid, _ = ctx.imu_preintegrate(imu, t0, t1)
+        assert valid.tolist() == [0] + [1] * (K - 1)
+        host_recs.append(rec)
+    raw = d_out.cpu().numpy()
+    for w in range(nw):  # the device buffer is bitwise the host entry's output
+        got = vio.abi.preint_records((vio.abi.VioPreint * K).from_buffer_copy(raw[w * K * sz:(w + 1) * K * sz].tobytes()))
+        for k in got:
+            assert np.array_equal(got[k], host_recs[w][k]), k
+    # batch A: created from the numpy-restated factors, then overwritten on device
+    pa = [vio.BaProblem(win, variant=vio.VIO_BA_VI) for win in ws]
+    A = vio.BaBatch(ctx, pa)
+    A.set_preint(d_out.data_ptr(), nw * K, on_device=True)
+    A.run()
+    A.sync()
+    ra = A.download()
+    # batch B: created directly from the same factors
+    for w, win in enumerate(ws):
+        win["preint"] = _as_dicts(host_recs[w], K)
+    pb = [vio.BaProblem(win, variant=vio.VIO_BA_VI) for win in ws]
+    B = vio.BaBatch(ctx, pb)
+    B.run()
+    B.sync()
+    rb = B.download()
+    for a, b in zip(ra, rb):
+        assert a["success"] == b["success"] == 1
+        assert np.array_equal(a["T_wb"], b["T_wb"]) and np.array_equal(a["lm_xyz"], b["lm_xyz"])
+        assert a["final_cost"] == b["final_cost"]
+    A.close()
+    B.close()
+    with pytest.raises(vio.VioError):
+        vio.BaBatch(ctx, pb[:1]).set_preint(d_out.data_ptr(), 3, on_device=True)
