@@ -31,6 +31,8 @@ EXPORTS = [
     "erp_frontend_stats", "erp_frontend_destroy", "vio_imu_preintegrate", "vio_imu_preintegrate_kernel_ms", "vio_imu_preintegrate_device",
     "vio_ba_batch_set_preint",
     "vio_triangulate", "vio_triangulate_device", "vio_triangulate_kernel_ms",
+    "vio_load_camera_timestamps", "vio_load_imu_csv", "erp_resize_area", "erp_resize_area_device",
+    "erp_resize_area_kernel_ms",
 ]
 
 
@@ -91,6 +93,11 @@ def lib():
     L.vio_triangulate.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp]
     L.vio_triangulate_device.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp]
     L.vio_triangulate_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    L.vio_load_camera_timestamps.argtypes = [C.c_char_p, vp, C.c_int, C.POINTER(C.c_int)]
+    L.vio_load_imu_csv.argtypes = [C.c_char_p, vp, C.c_int, C.POINTER(C.c_int)]
+    L.erp_resize_area.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int]
+    L.erp_resize_area_device.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int]
+    L.erp_resize_area_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
     _lib = L
     return L
 
@@ -188,6 +195,24 @@ class Context:
         self.check(lib().vio_triangulate_kernel_ms(self.h, C.byref(ms)), "vio_triangulate_kernel_ms")
         return ms.value
 
+    # ---- frame preprocessing ----
+    def resize_area(self, img, dW, dH):
+        """cv::resize(..., INTER_AREA) of a u8 frame to (dW, dH), integer factors (app/main.cpp:203)."""
+        a = _u8img(img)
+        H, W = a.shape
+        out = np.zeros((dH, dW), np.uint8)
+        self.check(lib().erp_resize_area(self.h, _p(a), W, H, a.strides[0], _p(out), dW, dH, dW), "erp_resize_area")
+        return out
+
+    def resize_area_device(self, src_ptr, W, H, stride, n_frames, dst_ptr, dW, dH, dst_stride):
+        self.check(lib().erp_resize_area_device(self.h, src_ptr, W, H, stride, n_frames, dst_ptr, dW, dH, dst_stride),
+                   "erp_resize_area_device")
+
+    def resize_kernel_ms(self):
+        ms = C.c_double()
+        self.check(lib().erp_resize_area_kernel_ms(self.h, C.byref(ms)), "erp_resize_area_kernel_ms")
+        return ms.value
+
     # ---- ERP feature tracking ----
     def klt_track(self, prev, curr, pts, params=None):
         """cv::calcOpticalFlowPyrLK as FeatureTracker::TrackOpticalFlow calls it -> (next, status, err)."""
@@ -227,6 +252,28 @@ class Context:
         self.check(lib().erp_rot_ransac(self.h, _p(p0), _p(p1), n, W, H, _p(samples), len(samples) // 3,
                                         float(thr), _p(mask), C.byref(nin)), "erp_rot_ransac")
         return mask, nin.value
+
+
+def load_camera_timestamps(path):
+    """LoadCameraTimestamps (app/main.cpp:30-48) through the C-ABI: (n,) f64."""
+    L, n = lib(), C.c_int()
+    rc = L.vio_load_camera_timestamps(os.fsencode(path), None, 0, C.byref(n))
+    if rc:
+        raise VioError(f"vio_load_camera_timestamps({path}) failed ({rc})")
+    out = np.zeros(max(n.value, 1), np.float64)
+    L.vio_load_camera_timestamps(os.fsencode(path), _p(out), n.value, C.byref(n))
+    return out[:n.value]
+
+
+def load_imu_csv(path):
+    """LoadIMUData (app/main.cpp:50-90) through the C-ABI: vio_imu_data records (abi.IMU_DTYPE)."""
+    L, n = lib(), C.c_int()
+    rc = L.vio_load_imu_csv(os.fsencode(path), None, 0, C.byref(n))
+    if rc:
+        raise VioError(f"vio_load_imu_csv({path}) failed ({rc})")
+    out = np.zeros(max(n.value, 1), abi.IMU_DTYPE)
+    L.vio_load_imu_csv(os.fsencode(path), _p(out), n.value, C.byref(n))
+    return out[:n.value]
 
 
 def _imu_call(fn, check, samples, t_start, t_end, gyro_bias, accel_bias, noise):

@@ -19,6 +19,8 @@ struct vio_ctx {
     float imu_ms = -1.f;
     // triangulation kernel timing (created on first use)
     hipEvent_t tri_ev[2] = {nullptr, nullptr};
+    // INTER_AREA resize kernel timing (created on first use)
+    hipEvent_t rsz_ev[2] = {nullptr, nullptr};
 };
 
 namespace vio360 {
@@ -31,6 +33,8 @@ void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes);
 enum { kSlotImuData = 8, kSlotImuIntervals = 9, kSlotImuOut = 10 };
 // scratch slots owned by vio_triangulate
 enum { kSlotTriIn = 11, kSlotTriOut = 12 };
+// scratch slots owned by erp_resize_area
+enum { kSlotResizeSrc = 13, kSlotResizeDst = 14 };
 
 #define VIO_HIP(ctx, expr)                                  \
     do {                                                    \

@@ -333,6 +333,36 @@ def tri_bench(vio, ctx, steps, want_cpu):
     return out
 
 
+def resize_bench(vio, ctx, steps):
+    """SURVEY §8 f3: cv::resize INTER_AREA of the frames (app/main.cpp:203), 3840x1920 -> 960x480,
+    64 device-resident frames per launch (synthetic noise frames).  HBM-bound: value = source Mpx/s."""
+    import torch
+    n, W, H, dW, dH = 64, 3840, 1920, 960, 480
+    dev = torch.device("cuda", torch.cuda.current_device())
+    src = torch.randint(0, 256, (n, H, W), dtype=torch.uint8, device=dev)
+    dst = torch.empty((n, dH, dW), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    args = (src.data_ptr(), W, H, W, n, dst.data_ptr(), dW, dH, dW)
+    for _ in range(3):
+        ctx.resize_area_device(*args)
+        ctx.resize_kernel_ms()
+    kms = []
+    for _ in range(steps):
+        ctx.resize_area_device(*args)
+        kms.append(ctx.resize_kernel_ms())
+    k_ms = float(np.mean(kms))
+    alg = n * (W * H + dW * dH)
+    return {
+        "metric": "INTER_AREA frame resize Mpx/s (3840x1920 -> 960x480, 64 frames per launch)",
+        "value": n * W * H / (k_ms * 1e-3) / 1e6,
+        "unit": "Mpx/s",
+        "kernel_ms": k_ms,
+        "roofline": {"bound": "hbm", "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                     "frac": alg / (k_ms * 1e-3) / 8.0e12, "traffic": kernel_traffic("resize_area4_kernel"),
+                     "note": "1 + 1/16 B per source pixel (read once, written at 1/16)"},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -347,6 +377,7 @@ def main():
     ap.add_argument("--no-global", action="store_true")
     ap.add_argument("--no-imu", action="store_true")
     ap.add_argument("--no-tri", action="store_true")
+    ap.add_argument("--no-resize", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -416,6 +447,7 @@ def main():
         imu = None if args.no_imu else imu_bench(vio, ctx, 20, min(args.cpu_seconds, 3.0),
                                                  not args.no_cpu_baseline and world == 1)
         tri = None if args.no_tri else tri_bench(vio, ctx, 20, not args.no_cpu_baseline and world == 1)
+        rsz = None if args.no_resize else resize_bench(vio, ctx, 20)
         single_ips = args.lm_iters / single_wall
         out = {
             "metric": "sliding-window BA iters/sec (10KF x 500pts)",
@@ -461,6 +493,7 @@ def main():
             "global_ba": gba,
             "imu_preint": imu,
             "triangulation": tri,
+            "frame_resize": rsz,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

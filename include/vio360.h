@@ -351,6 +351,27 @@ int vio_triangulate_device(vio_ctx* ctx, const float* T_cw, int n_poses, const i
 /* device time (ms) of the last triangulation kernel on this context (waits for it) */
 int vio_triangulate_kernel_ms(vio_ctx* ctx, double* ms);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Dataset formats and frame preprocessing, app/main.cpp:30-119, 199-204.        */
+
+/* LoadCameraTimestamps (app/main.cpp:30-48): one double per line.  Writes min(cap, count) values,
+   *n = count (call with cap = 0 to size the buffer).  VIO_EINVAL if the file cannot be opened. */
+int vio_load_camera_timestamps(const char* path, double* out, int cap, int* n);
+/* LoadIMUData (app/main.cpp:50-90): header line, then "t,ax,ay,az,gx,gy,gz" rows; malformed rows
+   are skipped exactly as the reference skips them.  Same sizing convention. */
+int vio_load_imu_csv(const char* path, vio_imu_data* out, int cap, int* n);
+
+/* cv::resize(img, img, Size(dW, dH), 0, 0, INTER_AREA) of a u8 grayscale frame (app/main.cpp:203),
+   integer downscale factors only (W % dW == 0, H % dH == 0; else VIO_ENOSYS).  Blocking; host buffers. */
+int erp_resize_area(vio_ctx* ctx, const uint8_t* src, int W, int H, int stride, uint8_t* dst, int dW, int dH,
+                    int dst_stride);
+/* the same for n_frames DEVICE frames (frame f at src + f*stride*H, dst + f*dst_stride*dH), async on
+   the context stream */
+int erp_resize_area_device(vio_ctx* ctx, const uint8_t* src, int W, int H, int stride, int n_frames, uint8_t* dst,
+                           int dW, int dH, int dst_stride);
+/* device time (ms) of the last resize kernel on this context (waits for it) */
+int erp_resize_area_kernel_ms(vio_ctx* ctx, double* ms);
+
 #ifdef __cplusplus
 }
 #endif
