@@ -10,8 +10,8 @@
 // (oracle/resize_oracle.py) and the GPU matches it bitwise.
 //
 // Roofline: HBM-bound streaming, 1 + 1/(fx·fy) bytes per source pixel.  The factor-4 fast path gives
-// each lane 4 output pixels: four 16-byte row loads (one 16x4 source block), no LDS; the grid covers
-// (output row, 4-pixel group, frame).
+// each lane 4 output pixels on two output rows: eight 16-byte non-temporal row loads (two 16x4
+// source blocks), no LDS; the grid covers (output row pair, 4-pixel group, frame).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -19,6 +19,8 @@
 #include "ctx.h"
 
 namespace vio360 {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 struct ResizeArgs {
     const uint8_t* src;
@@ -40,29 +42,34 @@ __device__ __forceinline__ int sum_bytes4(uint32_t w) {
     return (int)(w & 0xff) + (int)((w >> 8) & 0xff) + (int)((w >> 16) & 0xff) + (int)(w >> 24);
 }
 
-// fx = fy = 4, dst width a multiple of 4 and 16-byte aligned source rows: lane -> 4 output pixels
+// fx = fy = 4, dst width a multiple of 4, dst height even and 16-byte aligned source rows: lane ->
+// 4 output pixels on each of two output rows (eight 16-byte streaming loads in flight per lane)
 __global__ __launch_bounds__(256) void resize_area4_kernel(ResizeArgs a) {
     const int groups = a.dW >> 2;
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
+    const int y0 = 2 * blockIdx.y;
     const int f = blockIdx.z;
     if (g >= groups) return;
-    const uint8_t* s = a.src + f * a.frame_bytes_src + (long long)(4 * y) * a.stride + 16 * g;
-    uint4 r[4];
+    const uint8_t* s = a.src + f * a.frame_bytes_src + (long long)(4 * y0) * a.stride + 16 * g;
+    u32x4 r[8];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = *reinterpret_cast<const uint4*>(s + (long long)k * a.stride);
-    uint32_t out = 0;
+    for (int k = 0; k < 8; ++k) r[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + (long long)k * a.stride));
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        int sum = 0;
+    for (int h = 0; h < 2; ++h) {
+        uint32_t out = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t w = c == 0 ? r[k].x : (c == 1 ? r[k].y : (c == 2 ? r[k].z : r[k].w));
-            sum += sum_bytes4(w);
+        for (int c = 0; c < 4; ++c) {
+            int sum = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const u32x4 v = r[4 * h + k];
+                const uint32_t w = c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+                sum += sum_bytes4(w);
+            }
+            out |= (uint32_t)area_round(sum, a.scale) << (8 * c);
         }
-        out |= (uint32_t)area_round(sum, a.scale) << (8 * c);
+        *reinterpret_cast<uint32_t*>(a.dst + f * a.frame_bytes_dst + (long long)(y0 + h) * a.dstride + 4 * g) = out;
     }
-    *reinterpret_cast<uint32_t*>(a.dst + f * a.frame_bytes_dst + (long long)y * a.dstride + 4 * g) = out;
 }
 
 // any integer factors: lane -> 1 output pixel
@@ -117,11 +124,12 @@ extern "C" int erp_resize_area_device(vio_ctx* ctx, const uint8_t* src, int W, i
     for (hipEvent_t& ev : ctx->rsz_ev)
         if (!ev) VIO_HIP(ctx, hipEventCreate(&ev));
     VIO_HIP(ctx, hipEventRecord(ctx->rsz_ev[0], ctx->stream));
-    const bool fast = a.fx == 4 && a.fy == 4 && dW % 4 == 0 && stride % 16 == 0 && dst_stride % 4 == 0 &&
+    const bool fast = a.fx == 4 && a.fy == 4 && dW % 4 == 0 && dH % 2 == 0 && stride % 16 == 0 && dst_stride % 4 == 0 &&
                       (reinterpret_cast<uintptr_t>(src) & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 3) == 0;
     if (fast) {
         const int groups = dW / 4;
-        hipLaunchKernelGGL(resize_area4_kernel, dim3((groups + 255) / 256, dH, n_frames), dim3(256), 0, ctx->stream, a);
+        hipLaunchKernelGGL(resize_area4_kernel, dim3((groups + 255) / 256, dH / 2, n_frames), dim3(256), 0, ctx->stream,
+                           a);
     } else {
         hipLaunchKernelGGL(resize_area_kernel, dim3((dW + 255) / 256, dH, n_frames), dim3(256), 0, ctx->stream, a);
     }
