@@ -70,6 +70,17 @@ __device__ __forceinline__ void mv3(const float* A, const float* v, float* o) {
     for (int i = 0; i < 3; ++i) o[i] = (A[3 * i] * v[0] + A[3 * i + 1] * v[1]) + A[3 * i + 2] * v[2];
 }
 
+// A·[v]× with [v]×'s zero entries dropped from the k-ordered sums: adding an exact ±0 leaves every
+// non-zero sum unchanged, so this equals mm3(A, skew(v)) (up to the sign of an exactly zero entry)
+__device__ __forceinline__ void mm3_skew(const float* A, const float* v, float* C) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        C[3 * i + 0] = A[3 * i + 1] * v[2] + A[3 * i + 2] * -v[1];
+        C[3 * i + 1] = A[3 * i + 0] * -v[2] + A[3 * i + 2] * v[0];
+        C[3 * i + 2] = A[3 * i + 0] * v[1] + A[3 * i + 1] * -v[0];
+    }
+}
+
 __device__ __forceinline__ void skew3(const float* v, float* S) {
     S[0] = 0.f;   S[1] = -v[2]; S[2] = v[1];
     S[3] = v[2];  S[4] = 0.f;   S[5] = -v[0];
@@ -95,7 +106,7 @@ __device__ __forceinline__ void rodrigues_jr(const float* w, float* R, float* Jr
     const float ax[3] = {w[0] / th, w[1] / th, w[2] / th};
     float K[9], KK[9];
     skew3(ax, K);
-    mm3(K, K, KK);
+    mm3_skew(K, ax, KK);
     const float s = (float)sin((double)th), c = (float)cos((double)th);
     const float a = 1.f - c, b = (1.f - c) / th, d = (th - s) / th;
 #pragma unroll
@@ -181,17 +192,16 @@ __global__ __launch_bounds__(64) void imu_preint_kernel(ImuArgs a) {
         const float gyr[3] = {m.gx - iv.bg[0], m.gy - iv.bg[1], m.gz - iv.bg[2]};
         const float acc[3] = {m.ax - iv.ba[0], m.ay - iv.ba[1], m.az - iv.ba[2]};
         const float wdt[3] = {gyr[0] * dt, gyr[1] * dt, gyr[2] * dt};
-        float dRi[9], Jr[9], T[9], S[9], U[9];
+        float dRi[9], Jr[9], T[9], U[9];
         rodrigues_jr(wdt, dRi, Jr);
         mtm3(dRi, Jr, T);
 #pragma unroll
         for (int k = 0; k < 9; ++k) JRg[k] = -T[k] * dt;
-        skew3(acc, S);
-        mm3(JVa, S, T);
+        mm3_skew(JVa, acc, T);
         mm3(T, JRg, U);
 #pragma unroll
         for (int k = 0; k < 9; ++k) JVg[k] = JVg[k] + U[k];
-        mm3(JPa, S, T);
+        mm3_skew(JPa, acc, T);
         mm3(T, JRg, U);
 #pragma unroll
         for (int k = 0; k < 9; ++k) JPg[k] = (JPg[k] + U[k]) + JVg[k] * dt;

@@ -69,3 +69,5 @@ for nwin in (1, 256):
         res = b.download()[0]
         o = oracle(probs[0])
         print("fixed10 parity", cmp(o, res))
+    b.close()
+ctx.close()  # explicit: HIP objects must not outlive the runtime's own teardown at interpreter exit
