@@ -32,7 +32,7 @@ EXPORTS = [
     "vio_ba_batch_set_preint",
     "vio_triangulate", "vio_triangulate_device", "vio_triangulate_kernel_ms",
     "vio_load_camera_timestamps", "vio_load_imu_csv", "erp_resize_area", "erp_resize_area_device",
-    "erp_resize_area_kernel_ms",
+    "erp_resize_area_kernel_ms", "erp_tracker_upload_resized",
 ]
 
 
@@ -98,6 +98,7 @@ def lib():
     L.erp_resize_area.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int]
     L.erp_resize_area_device.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int]
     L.erp_resize_area_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    L.erp_tracker_upload_resized.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int]
     _lib = L
     return L
 
@@ -335,6 +336,13 @@ class Tracker:
     def upload(self, slot, img):
         img = _u8img(img)
         self.ctx.check(lib().erp_tracker_upload(self.h, slot, _p(img), img.shape[1]), "erp_tracker_upload")
+
+    def upload_resized(self, slot, img):
+        """erp_tracker_upload_resized: a camera-resolution frame, INTER_AREA-resized on the device."""
+        img = _u8img(img)
+        H, W = img.shape
+        self.ctx.check(lib().erp_tracker_upload_resized(self.h, slot, _p(img), W, H, img.strides[0]),
+                       "erp_tracker_upload_resized")
 
     def swap(self):
         self.ctx.check(lib().erp_tracker_swap(self.h), "erp_tracker_swap")

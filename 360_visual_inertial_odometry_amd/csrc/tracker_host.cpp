@@ -398,6 +398,20 @@ int erp_tracker_upload(erp_tracker* t, int slot, const uint8_t* img, int stride)
     return upload_frame(t, slot, img, stride);
 }
 
+int erp_tracker_upload_resized(erp_tracker* t, int slot, const uint8_t* img, int W, int H, int stride) {
+    if (!t || slot < 0 || slot > 1 || !img || W <= 0 || H <= 0 || stride < W) return VIO_EINVAL;
+    if (W == t->W && H == t->H) return upload_frame(t, slot, img, stride);
+    vio_ctx* ctx = t->ctx;
+    const int sp = (W + 15) & ~15;  // 16-byte rows: the resize fast path
+    uint8_t* d_src = static_cast<uint8_t*>(ctx_buffer(ctx, kSlotResizeSrc, (size_t)sp * H));
+    if (!d_src) {
+        set_error(ctx, "erp_tracker_upload_resized: device allocation failed");
+        return VIO_ENOMEM;
+    }
+    VIO_HIP(ctx, hipMemcpy2DAsync(d_src, sp, img, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
+    return erp_resize_area_device(ctx, d_src, W, H, sp, 1, t->lvl[slot][0], t->W, t->H, t->lp[0]);
+}
+
 int erp_tracker_device_frame(erp_tracker* t, int slot, uint8_t** dev_ptr, int* pitch) {
     if (!t || slot < 0 || slot > 1 || !dev_ptr || !pitch) return VIO_EINVAL;
     *dev_ptr = t->lvl[slot][0];

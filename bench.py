@@ -333,7 +333,7 @@ def tri_bench(vio, ctx, steps, want_cpu):
     return out
 
 
-def resize_bench(vio, ctx, steps):
+def resize_bench(vio, ctx, steps, want_cpu):
     """SURVEY §8 f3: cv::resize INTER_AREA of the frames (app/main.cpp:203), 3840x1920 -> 960x480,
     64 device-resident frames per launch (synthetic noise frames).  HBM-bound: value = source Mpx/s."""
     import torch
@@ -352,6 +352,19 @@ def resize_bench(vio, ctx, steps):
         kms.append(ctx.resize_kernel_ms())
     k_ms = float(np.mean(kms))
     alg = n * (W * H + dW * dH)
+    cpu = None
+    if want_cpu:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("resize_oracle", os.path.join(ROOT, "oracle", "resize_oracle.py"))
+        ro = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(ro)
+        frame = src[0].cpu().numpy()
+        reps, t_start = 0, time.perf_counter()
+        while reps < 3 or time.perf_counter() - t_start < 2.0:
+            ro.resize_area(frame, dW, dH)
+            reps += 1
+        cpu = {"value": reps * W * H / (time.perf_counter() - t_start) / 1e6, "unit": "Mpx/s", "cores": 1,
+               "kind": "port", "sample": f"{reps} frames through oracle/resize_oracle.py (numpy)"}
     return {
         "metric": "INTER_AREA frame resize Mpx/s (3840x1920 -> 960x480, 64 frames per launch)",
         "value": n * W * H / (k_ms * 1e-3) / 1e6,
@@ -360,6 +373,7 @@ def resize_bench(vio, ctx, steps):
         "roofline": {"bound": "hbm", "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
                      "frac": alg / (k_ms * 1e-3) / 8.0e12, "traffic": kernel_traffic("resize_area4_kernel"),
                      "note": "1 + 1/16 B per source pixel (read once, written at 1/16)"},
+        "cpu_baseline": cpu,
     }
 
 
@@ -447,7 +461,7 @@ def main():
         imu = None if args.no_imu else imu_bench(vio, ctx, 20, min(args.cpu_seconds, 3.0),
                                                  not args.no_cpu_baseline and world == 1)
         tri = None if args.no_tri else tri_bench(vio, ctx, 20, not args.no_cpu_baseline and world == 1)
-        rsz = None if args.no_resize else resize_bench(vio, ctx, 20)
+        rsz = None if args.no_resize else resize_bench(vio, ctx, 20, not args.no_cpu_baseline and world == 1)
         single_ips = args.lm_iters / single_wall
         out = {
             "metric": "sliding-window BA iters/sec (10KF x 500pts)",

@@ -237,6 +237,10 @@ int erp_tracker_create(vio_ctx* ctx, int W, int H, int max_points, int max_corne
    buffer of a slot (pitch *pitch bytes) for producers that write frames on the device */
 int erp_tracker_upload(erp_tracker* t, int slot, const uint8_t* img, int stride);
 int erp_tracker_device_frame(erp_tracker* t, int slot, uint8_t** dev_ptr, int* pitch);
+/* the demo's frame path (app/main.cpp:199-204): upload a W x H u8 camera frame and resize it on the
+   device with INTER_AREA (erp_resize_area) into slot's tracker resolution; integer factors only
+   (VIO_ENOSYS otherwise), a frame already at tracker resolution is uploaded as is */
+int erp_tracker_upload_resized(erp_tracker* t, int slot, const uint8_t* img, int W, int H, int stride);
 /* swap slots 0 and 1 (the current frame becomes the previous one, m_prev_image = current) */
 int erp_tracker_swap(erp_tracker* t);
 typedef struct {

@@ -177,3 +177,31 @@ def test_pipeline_full_size_config1(vio, gpu_ctx, synth):
     nxt, st, kept, corners = pipeline_oracle(vio, a, b, pts, prm, klt)
     assert np.array_equal(res["next"], nxt) and np.array_equal(res["kept"], kept)
     assert np.array_equal(res["corners"], corners)
+
+
+def test_pipeline_on_device_resized_frames(vio, gpu_ctx, synth):
+    """The demo frame path (app/main.cpp:199-204): 3840x1920 camera frames INTER_AREA-resized on the
+    device into the tracker's 960x480 slots give bitwise the pipeline on oracle-resized frames."""
+    from test_dataset import load_resize_oracle
+    ro = load_resize_oracle()
+    A, B, _ = synth.config1()  # 3840 x 1920
+    a, b = ro.resize_area(A, W, H), ro.resize_area(B, W, H)
+    pts = oracle_lib.gftt(a, region_mask(W, H), 300, float(np.float32(0.01)), 30.0)
+    prm = vio.default_tracker_params(max_corners=300, seed=78)
+    klt = vio.default_klt_params()
+    res = []
+    for resized_on_device in (True, False):
+        t = vio.Tracker(gpu_ctx, W, H, max_points=1024, max_corners=1024)
+        if resized_on_device:
+            t.upload_resized(0, A)
+            t.upload_resized(1, B)
+        else:
+            t.upload(0, a)
+            t.upload(1, b)
+        t.set_points(pts)
+        t.run(prm, klt)
+        res.append(t.download())
+        t.close()
+    for k in ("status", "next", "kept", "corners"):
+        assert np.array_equal(res[0][k], res[1][k]), k
+    assert res[0]["kept"].sum() > 200
