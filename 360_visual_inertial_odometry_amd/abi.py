@@ -55,11 +55,26 @@ class VioBaSummary(C.Structure):
     ]
 
 
+class VioBaIteration(C.Structure):
+    """Solver::Summary::iterations entry (ceres IterationSummary fields the solver sets)."""
+    _fields_ = [
+        ("iteration", C.c_int32), ("step_is_valid", C.c_int32), ("step_is_successful", C.c_int32),
+        ("_pad", C.c_int32), ("cost", C.c_double), ("cost_change", C.c_double),
+        ("gradient_max_norm", C.c_double), ("step_norm", C.c_double), ("relative_decrease", C.c_double),
+        ("trust_region_radius", C.c_double), ("model_cost_change", C.c_double),
+    ]
+
+
+TRACE_FIELDS = ("iteration", "step_is_valid", "step_is_successful", "cost", "cost_change", "gradient_max_norm",
+                "step_norm", "relative_decrease", "trust_region_radius", "model_cost_change")
+
+
 class VioBaOutput(C.Structure):
     _fields_ = [
         ("T_wb", C.POINTER(VioPose)), ("lm_xyz", _f64p), ("obs_chi2", _f64p), ("obs_outlier", _u8p),
         ("lm_bad", _u8p), ("vel", _f64p), ("bg", _f64p), ("ba", _f64p),
         ("summary", C.POINTER(VioBaSummary)),
+        ("trace", C.POINTER(VioBaIteration)), ("trace_cap", C.c_int32), ("_pad2", C.c_int32),
     ]
 
 
@@ -197,7 +212,7 @@ class BaProblem:
 
 
 class BaOutput:
-    def __init__(self, K, L, N):
+    def __init__(self, K, L, N, trace_cap=256):
         self.K, self.L, self.N = K, L, N
         self.T_wb = (VioPose * K)()
         self.lm_xyz = np.zeros(3 * max(L, 1))
@@ -218,6 +233,9 @@ class BaOutput:
         o.bg = _ptr(self.bg, C.c_double)
         o.ba = _ptr(self.ba, C.c_double)
         o.summary = C.pointer(self.summary)
+        self.trace = (VioBaIteration * max(trace_cap, 1))()
+        o.trace = C.cast(self.trace, C.POINTER(VioBaIteration))
+        o.trace_cap = trace_cap
         self.c = o
 
     def result(self):
@@ -236,7 +254,13 @@ class BaOutput:
             "num_unsuccessful_steps": s.num_unsuccessful_steps,
             "num_inliers": s.num_inliers, "num_outliers": s.num_outliers, "num_bad_lm": s.num_bad_lm,
             "initial_cost": s.initial_cost, "final_cost": s.final_cost, "fixed_cost": s.fixed_cost,
+            "trace": self.trace_dict(),
         }
+
+    def trace_dict(self):
+        """Summary::iterations as a dict of numpy arrays (one entry per recorded iteration)."""
+        n = min(max(self.summary.iterations, 0), self.c.trace_cap)
+        return {f: np.array([getattr(self.trace[i], f) for i in range(n)]) for f in TRACE_FIELDS}
 
 
 # ---------------------------------------------------------------------------------------------

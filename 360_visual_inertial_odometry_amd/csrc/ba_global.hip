@@ -132,7 +132,9 @@ __global__ void __launch_bounds__(GT) gba_lin_lm_kernel(GbaArgs A, int first, do
         }
         for (int i = 0; i < 6; ++i) A.V[(size_t)i * L + l] = v[i];
         for (int i = 0; i < 3; ++i) A.gl[(size_t)i * L + l] = g[i];
-        gm = fmax(fabs(g[0]), fmax(fabs(g[1]), fabs(g[2])));
+        // Ceres' |x - Plus(x, -g)| term (trust_region_minimizer.cc:288-299)
+        const double* xl = A.x_lm + 3 * (size_t)l;
+        gm = fmax(fabs(xl[0] - (xl[0] + (-g[0]))), fmax(fabs(xl[1] - (xl[1] + (-g[1]))), fabs(xl[2] - (xl[2] + (-g[2])))));
         if (first) {
             A.sl[l] = 1.0 / (1.0 + sqrt(v[0]));
             A.sl[(size_t)L + l] = 1.0 / (1.0 + sqrt(v[3]));
@@ -189,7 +191,10 @@ __global__ void __launch_bounds__(GT) gba_lin_pose_kernel(GbaArgs A, int first, 
             A.colsq_f[pf + lane] = cs;
             if (first) A.sf[pf + lane] = 1.0 / (1.0 + sqrt(cs));
         }
-        for (int i = 0; i < 6; ++i) gm = fmax(gm, fabs(acc[21 + i]));
+        for (int i = 0; i < 6; ++i) {
+            const double xv = A.x_pose[6 * (size_t)k + i];
+            gm = fmax(gm, fabs(xv - (xv + (-acc[21 + i]))));
+        }
     }
     __shared__ double red[GT / 64];
     if (lane == 0) red[wid] = gm;

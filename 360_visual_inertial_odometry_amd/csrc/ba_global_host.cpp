@@ -235,6 +235,15 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     const bool fixed = p.fixed_iterations != 0;
     int termination = VIO_TERM_NO_CONVERGENCE, iterations = 0, nsucc = 0, nunsucc = 0;
     double initial_cost, final_cost;
+    // Summary::iterations (pushed at FinalizeIterationAndCheckIfMinimizerCanContinue, :313-348)
+    vio_ba_iteration it;
+    std::memset(&it, 0, sizeof it);
+    auto push = [&](double radius) {
+        if (out->trace && iterations - 1 < out->trace_cap) {
+            out->trace[iterations - 1] = it;
+            out->trace[iterations - 1].trust_region_radius = radius;
+        }
+    };
     if (n_free == 0) {
         termination = VIO_TERM_CONVERGENCE;
         initial_cost = final_cost = fixed_cost;
@@ -251,6 +260,9 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
         int iteration = 0;
         bool step_ok = true;
         double model_change = 0, cand_cost = 0;
+        it.step_is_valid = it.step_is_successful = 1;  // IterationZero (:195-229)
+        it.cost = iter_cost;
+        it.gradient_max_norm = gmax;
         for (;;) {
             if (step_ok) {
                 nsucc++;
@@ -260,10 +272,13 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             }
             iterations++;
             final_cost = std::min(final_cost, iter_cost);
+            push(radius);
             if (iteration >= max_iter) { termination = VIO_TERM_NO_CONVERGENCE; break; }
             if (!fixed && step_ok && gmax <= 1e-10) { termination = VIO_TERM_CONVERGENCE; break; }
             if (!fixed && radius <= 1e-32) { termination = VIO_TERM_CONVERGENCE; break; }
             iteration++;
+            std::memset(&it, 0, sizeof it);
+            it.iteration = iteration;
             // ComputeTrustRegionStep + candidate cost, one batch of kernels, one readback
             GBA_CHECK(hipMemsetAsync(dfail, 0, sizeof(int), st));
             GBA_CHECK(gba_launch_step_prep(A, radius, partial, scal + 2, st));
@@ -277,6 +292,7 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             if ((rc = read(h, 0, 8))) return rc;
             bool valid = h[2] == 0.0 && hfail == 0 && h[3] == 0.0;
             model_change = h[4];
+            if (valid) it.model_cost_change = model_change;
             if (valid) valid = model_change > 0.0;
             if (!valid) {
                 if (++consecutive_invalid >= 5) { termination = VIO_TERM_FAILURE; break; }
@@ -284,14 +300,20 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
                 decrease *= 2.0;
                 step_ok = false;
                 iter_cost = x_cost + fixed_cost;
+                it.cost = iter_cost;
+                it.gradient_max_norm = gmax;
                 continue;
             }
             consecutive_invalid = 0;
             cand_cost = h[7];
             const double step_norm = std::sqrt(h[5]);
+            it.step_is_valid = 1;
+            it.step_norm = step_norm;
+            it.cost_change = x_cost - cand_cost;
             if (!fixed && step_norm <= 1e-8 * (x_norm + 1e-8)) { termination = VIO_TERM_CONVERGENCE; break; }
             if (!fixed && std::fabs(x_cost - cand_cost) <= 1e-6 * x_cost) { termination = VIO_TERM_CONVERGENCE; break; }
             const double rel = (step_eval_current - cand_cost) / model_change;
+            it.relative_decrease = rel;
             if (rel > 1e-3) {
                 GBA_CHECK(hipMemcpyAsync(A.x_pose, A.c_pose, sizeof(double) * 6 * K, hipMemcpyDeviceToDevice, st));
                 GBA_CHECK(hipMemcpyAsync(A.x_lm, A.c_lm, sizeof(double) * 3 * L, hipMemcpyDeviceToDevice, st));
@@ -312,6 +334,9 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
                 radius /= decrease;
                 decrease *= 2.0;
             }
+            it.step_is_successful = step_ok;
+            it.cost = iter_cost;
+            it.gradient_max_norm = gmax;
         }
         if (termination == VIO_TERM_FAILURE) {  // Ceres leaves the user's parameters untouched
             GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));

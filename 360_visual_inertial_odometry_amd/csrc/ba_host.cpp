@@ -36,6 +36,8 @@ int hip_fail(vio_ctx* ctx, hipError_t e, const char* what) {
     return e == hipErrorOutOfMemory ? VIO_ENOMEM : VIO_EDEVICE;
 }
 void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes) {
+    // the buffer must live on the context's device whatever device the calling thread has current
+    if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
     if ((int)ctx->bufs.size() <= slot) {
         ctx->bufs.resize(slot + 1, nullptr);
         ctx->caps.resize(slot + 1, 0);
@@ -61,7 +63,7 @@ struct Packed {
     std::vector<float> obs_uv;
     std::vector<vio_preint> preint;
     std::vector<std::vector<int32_t>> perm;  // per window: sorted position -> original obs index
-    int64_t ws_total = 0, out_total = 0, N_total = 0, L_total = 0;
+    int64_t ws_total = 0, out_total = 0, N_total = 0, L_total = 0, tr_total = 0;
 };
 
 int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
@@ -156,6 +158,9 @@ int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
     w.o_kfptr = (int64_t)pk.kf_ptr.size();
     w.o_ws = pk.ws_total;
     w.o_out = pk.out_total;
+    w.o_tr = pk.tr_total;
+    w.tr_cap = (w.max_iter + 1) * w.rounds;  // every Summary::iterations entry of every round
+    pk.tr_total += w.tr_cap;
     BaWsLayout WL = ba_ws_layout(K, L, N);
     pk.ws_total += WL.total + (int64_t)ba_ws_extra_doubles() + (int64_t)ba_phase_doubles(K, L, w.T);
     pk.ws_total = (pk.ws_total + 31) & ~(int64_t)31;
@@ -290,6 +295,8 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     d.P.out_i32 = (int32_t*)ptr;
     if ((rc = alloc(sizeof(double) * SD_COUNT * d.n, &ptr)) != VIO_OK) return rc;
     d.P.out_sum = (double*)ptr;
+    if ((rc = alloc(sizeof(vio_ba_iteration) * pk.tr_total, &ptr)) != VIO_OK) return rc;
+    d.P.out_trace = (vio_ba_iteration*)ptr;
     VIO_HIP(ctx, hipEventCreate(&d.ev0));
     VIO_HIP(ctx, hipEventCreate(&d.ev1));
     return VIO_OK;
@@ -313,6 +320,12 @@ static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
     std::vector<uint8_t> u8(pk.N_total), bad(pk.L_total);
     std::vector<int32_t> si(SI_COUNT * d.n);
     std::vector<double> sd(SD_COUNT * d.n);
+    bool want_trace = false;
+    for (int i = 0; i < d.n; ++i) want_trace |= outs[i].trace != nullptr && outs[i].trace_cap > 0;
+    std::vector<vio_ba_iteration> tr(want_trace ? pk.tr_total : 0);
+    if (want_trace)
+        VIO_HIP(ctx, hipMemcpyAsync(tr.data(), d.P.out_trace, sizeof(vio_ba_iteration) * tr.size(),
+                                    hipMemcpyDeviceToHost, ctx->stream));
     VIO_HIP(ctx, hipMemcpyAsync(out.data(), d.P.out, sizeof(double) * out.size(), hipMemcpyDeviceToHost, ctx->stream));
     VIO_HIP(ctx, hipMemcpyAsync(u8.data(), d.P.out_u8, u8.size(), hipMemcpyDeviceToHost, ctx->stream));
     VIO_HIP(ctx, hipMemcpyAsync(bad.data(), d.P.out_bad, bad.size(), hipMemcpyDeviceToHost, ctx->stream));
@@ -358,6 +371,10 @@ static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
             s.final_cost = b[SD_FINAL];
             s.fixed_cost = b[SD_FIXED];
         }
+        if (o.trace && o.trace_cap > 0) {
+            const int n_it = std::min(std::min(si[SI_COUNT * i + SI_ITERS], w.tr_cap), o.trace_cap);
+            for (int q = 0; q < n_it; ++q) o.trace[q] = tr[w.o_tr + q];
+        }
     }
     return VIO_OK;
 }
@@ -383,6 +400,7 @@ static bool force_monolithic(const BaDevice& d) {
 }
 
 static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
+    VIO_HIP(ctx, hipSetDevice(ctx->device));
     if (timed) VIO_HIP(ctx, hipEventRecord(d.ev0, ctx->stream));
     bool any_pnp = false, any_other = false;
     for (const BaWin& w : d.pk.win) (w.is_pnp ? any_pnp : any_other) = true;

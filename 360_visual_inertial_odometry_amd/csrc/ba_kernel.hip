@@ -36,6 +36,9 @@ struct LmState {
     double initial_cost, final_cost, fixed_cost, iter_cost, step_eval_current;
     double step_norm, cand_x_norm2, rel;
     double fused_cost;           // cost at the candidate, evaluated inside compute_step
+    // IterationSummary fields of the iteration in progress (pushed to the trace at finalisation)
+    double tr_cost_change, tr_step_norm, tr_rel, tr_model;
+    int tr_valid, tr_n;
     int iteration, nsucc, nunsucc, consecutive_invalid;
     int termination, done, step_ok, valid, fail, need_jac, pnp_round, cand_fail;
 };
@@ -333,7 +336,36 @@ struct WinCtx {
     double* Himu;     // [NI_MAX^2]
     double* gimu;     // [NI_MAX]
     uint8_t* outlier; // [N] doubles as the PnP round flags
+    vio_ba_iteration* trace;  // [w.tr_cap] Summary::iterations
 };
+
+// Summary::iterations: FinalizeIterationAndCheckIfMinimizerCanContinue pushes the iteration summary
+// (trust_region_minimizer.cc:313-348); one lane
+__device__ inline void trace_push(const WinCtx& c, LmState& s) {
+    if (s.tr_n < c.w->tr_cap) {
+        vio_ba_iteration& t = c.trace[s.tr_n];
+        t.iteration = s.iteration;
+        t.step_is_valid = s.tr_valid;
+        t.step_is_successful = s.step_ok;
+        t._pad = 0;
+        t.cost = s.iter_cost;
+        t.cost_change = s.tr_cost_change;
+        t.gradient_max_norm = s.gmax;
+        t.step_norm = s.tr_step_norm;
+        t.relative_decrease = s.tr_rel;
+        t.trust_region_radius = s.radius;
+        t.model_cost_change = s.tr_model;
+    }
+    s.tr_n++;
+}
+// a new iteration's summary: zero-length, invalid until the step says otherwise (IterationSummary())
+__device__ inline void trace_begin(LmState& s) {
+    s.tr_valid = 0;
+    s.tr_cost_change = s.tr_step_norm = s.tr_rel = s.tr_model = 0.0;
+}
+// Ceres' gradient max norm term |x - Plus(x, -g)| (trust_region_minimizer.cc:288-299; no local
+// parameterization: Plus is x + delta) — |g| up to the roundoff of x - g
+__device__ __forceinline__ double grad_term(double x, double g) { return fabs(x - (x + (-g))); }
 
 // pose cache for the parameter set at (xp): T_wb = SE3(T_init) * exp(delta), etc.
 __device__ __forceinline__ void pose_cache(BaShared& sh, const WinCtx& c, const double* xp) {
@@ -385,8 +417,8 @@ __device__ __forceinline__ Walk walk_geom(int K) {
 // Writes V / g_l (and the Jacobi scaling s_l on the first linearisation); returns the lane's
 // running max |g_l| (combined by a block max later, exact in any order).
 __device__ __forceinline__ double lm_sums9(const double* q, int l0, const Walk& g, int K, int L,
-                                           const uint8_t* lm_var, double* V, double* gl, double* sl, bool first,
-                                           double gm) {
+                                           const uint8_t* lm_var, const double* xl, double* V, double* gl, double* sl,
+                                           bool first, double gm) {
     for (int t = threadIdx.x; t < 9 * g.LC; t += BA_THREADS) {
         const int i = t / g.LC, j = t - i * g.LC, lj = l0 + j;
         if (lj >= L || !lm_var[lj]) continue;
@@ -399,7 +431,7 @@ __device__ __forceinline__ double lm_sums9(const double* q, int l0, const Walk& 
             V[(int64_t)i * L + lj] = v;
         } else {
             gl[(int64_t)(i - 6) * L + lj] = v;
-            gm = fmax(gm, fabs(v));
+            gm = fmax(gm, grad_term(xl[3 * lj + i - 6], v));
         }
         if (first && (i == 0 || i == 3 || i == 5)) sl[(int64_t)(i == 0 ? 0 : i == 3 ? 1 : 2) * L + lj] = 1.0 / (1.0 + sqrt(v));
     }
@@ -426,7 +458,18 @@ __device__ __forceinline__ double imu_factors(BaShared& sh, const WinCtx& c, con
     return cost;
 }
 
-__device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool first, double gm);
+__device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool first, double gm, const double* xp,
+                                         const double* xv, const double* xb);
+
+// value of reduced-system parameter f (pose delta, velocity or bias component) at (xp, xv, xb)
+__device__ inline double f_param_value(const BaWin& w, int f, const double* xp, const double* xv, const double* xb) {
+    for (int k = 0; k < w.K; ++k) {
+        if (w.pose_f[k] >= 0 && f >= w.pose_f[k] && f < w.pose_f[k] + 6) return xp[6 * k + f - w.pose_f[k]];
+        if (w.vel_f[k] >= 0 && f >= w.vel_f[k] && f < w.vel_f[k] + 3) return xv[3 * k + f - w.vel_f[k]];
+    }
+    if (w.bg_f >= 0 && f >= w.bg_f && f < w.bg_f + 3) return xb[f - w.bg_f];
+    return xb[3 + f - w.ba_f];
+}
 
 // Cost + residuals/Jacobians + normal-equation statistics at (xp, xl, xv, xb) in one walk:
 // BAFactor::Evaluate per observation lane (Factors.cpp:327-542) with Huber/Corrector scaling,
@@ -550,7 +593,7 @@ __device__ __forceinline__ double eval_lin(BaShared& sh, const WinCtx& c, const 
         for (int i = 0; i < 9; ++i) rb_[i * BA_THREADS + threadIdx.x] = v9[i];
         if (kProfWalk) prof_mark(sh, PF_EV_F);
         __syncthreads();
-        gm = lm_sums9(rb_, l0, g, K, L, c.lm_var, V, gl, sl, first, gm);
+        gm = lm_sums9(rb_, l0, g, K, L, c.lm_var, xl, V, gl, sl, first, gm);
         if (kProfWalk) prof_mark(sh, PF_EV_L);
         cur = nxt;
         o_nn = o_n2;
@@ -576,7 +619,7 @@ __device__ __forceinline__ double eval_lin(BaShared& sh, const WinCtx& c, const 
     const double anyfail = block_max((double)fail, sh.redm);
     if (threadIdx.x == 0 && anyfail > 0.0) sh.st.fail = 1;
     __syncthreads();
-    lin_tail(sh, c, first, gm);
+    lin_tail(sh, c, first, gm, xp, xv, xb);
     return total;
 }
 
@@ -592,7 +635,8 @@ __device__ __forceinline__ int imu_col(const BaWin& w, int k, int c) {
 
 // After eval_lin: IMU normal equations (imu-space H, g), f-space gradient, column norms (Jacobi
 // scaling at iteration 0) and the gradient max-norm (gm = landmark part from the walk).
-__device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool first, double gm) {
+__device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool first, double gm, const double* xp,
+                                         const double* xv, const double* xb) {
     const BaWin& w = *c.w;
     const int K = w.K;
     // IMU: per-factor residual/J already in LDS; assemble imu-space H (global) and g.  Factors are
@@ -655,7 +699,7 @@ __device__ __forceinline__ void lin_tail(BaShared& sh, const WinCtx& c, bool fir
         }
         sh.g_f[f] = g;
         sh.colsq_f[f] = cs;
-        gm = fmax(gm, fabs(g));
+        gm = fmax(gm, grad_term(f_param_value(w, f, xp, xv, xb), g));
         if (first) sh.s_f[f] = 1.0 / (1.0 + sqrt(cs));
     }
     double gmax = block_max(gm, sh.redm);
@@ -1498,6 +1542,8 @@ __device__ __forceinline__ void lm_solve(BaShared& sh, const WinCtx& c) {
         s.step_eval_current = cost;
         s.step_ok = 1;
         s.iter_cost = cost + s.fixed_cost;
+        trace_begin(s);  // IterationZero (:195-229): valid and successful
+        s.tr_valid = 1;
     }
     __syncthreads();
     for (;;) {
@@ -1511,10 +1557,14 @@ __device__ __forceinline__ void lm_solve(BaShared& sh, const WinCtx& c) {
                 s.nunsucc++;
             }
             s.final_cost = fmin(s.final_cost, s.iter_cost);
+            trace_push(c, s);
             if (s.iteration >= w.max_iter) { s.termination = VIO_TERM_NO_CONVERGENCE; s.done = 1; }
             else if (!fixed && s.step_ok && s.gmax <= 1e-10) { s.termination = VIO_TERM_CONVERGENCE; s.done = 1; }
             else if (!fixed && s.radius <= 1e-32) { s.termination = VIO_TERM_CONVERGENCE; s.done = 1; }
-            if (!s.done) s.iteration++;
+            if (!s.done) {
+                s.iteration++;
+                trace_begin(s);
+            }
         }
         __syncthreads();
         if (sh.st.done) break;
@@ -1522,7 +1572,10 @@ __device__ __forceinline__ void lm_solve(BaShared& sh, const WinCtx& c) {
         compute_step(sh, c);
         bool valid = sh.st.valid;
         if (valid) {
-            if (threadIdx.x == 0) sh.st.valid = sh.st.model_change > 0.0;
+            if (threadIdx.x == 0) {
+                sh.st.tr_model = sh.st.model_change;
+                sh.st.valid = sh.st.model_change > 0.0;
+            }
             __syncthreads();
             valid = sh.st.valid;
         }
@@ -1555,11 +1608,15 @@ __device__ __forceinline__ void lm_solve(BaShared& sh, const WinCtx& c) {
             LmState& s = sh.st;
             s.cand_cost = s.fail ? DBL_MAX : cc;
             s.fail = 0;
+            s.tr_valid = 1;
+            s.tr_step_norm = s.step_norm;
+            s.tr_cost_change = s.x_cost - s.cand_cost;
             if (!fixed && s.step_norm <= 1e-8 * (s.x_norm + 1e-8)) { s.termination = VIO_TERM_CONVERGENCE; s.done = 1; }
             else if (!fixed && fabs(s.x_cost - s.cand_cost) <= 1e-6 * s.x_cost) { s.termination = VIO_TERM_CONVERGENCE; s.done = 1; }
             else {
                 double rel = s.cand_cost >= DBL_MAX ? -DBL_MAX : (s.step_eval_current - s.cand_cost) / s.model_change;
                 s.rel = rel;
+                s.tr_rel = rel;
                 s.step_ok = rel > 1e-3;
                 if (!s.step_ok) {
                     s.iter_cost = s.cand_cost + s.fixed_cost;
@@ -1636,8 +1693,10 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
     c.Himu = c.sqi + 81 * BA_KMAX;
     c.gimu = c.Himu + NI_MAX * NI_MAX;
     c.outlier = P.out_u8 + w.o_obs;
+    c.trace = P.out_trace + w.o_tr;
     const int K = w.K, L = w.L, N = w.N;
     if (threadIdx.x == 0) {
+        sh.st.tr_n = 0;
         sh.prof_on = P.prof != nullptr;
         for (int i = 0; i < PF_NSLOT; ++i) sh.prof_acc[i] = 0;
         sh.prof_last = __builtin_amdgcn_s_memtime();
@@ -1816,13 +1875,22 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
 size_t ba_shared_bytes() { return sizeof(BaShared); }
 size_t ba_ws_extra_doubles() { return ba_ws_extra(); }
 
+// kernel attributes are per device: one flag per device ordinal (the caller has selected the
+// context's device)
+constexpr int kMaxDevices = 64;
+static int current_device() {
+    int d = 0;
+    return hipGetDevice(&d) == hipSuccess && d >= 0 && d < kMaxDevices ? d : 0;
+}
+
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream) {
-    static bool attr_set = false;
-    if (!attr_set) {
+    static bool attr_set[kMaxDevices] = {};
+    const int dev = current_device();
+    if (!attr_set[dev]) {
         hipError_t e = hipFuncSetAttribute((const void*)ba_window_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)sizeof(BaShared));
         if (e != hipSuccess) return e;
-        attr_set = true;
+        attr_set[dev] = true;
     }
     hipLaunchKernelGGL(ba_window_kernel, dim3(n), dim3(BA_THREADS), sizeof(BaShared), stream, P);
     return hipGetLastError();

@@ -21,7 +21,7 @@ struct BaWin {
     int32_t nf, np, npad, T;     // reduced size, pose rows (6*P), padded pose rows (16*T), tile
     int32_t ni;                  // imu-space size nf - np
     int32_t max_iter, fixed_iter, rounds;
-    int32_t is_vi, is_pnp, n_imu, _p0;
+    int32_t is_vi, is_pnp, n_imu, tr_cap; // tr_cap: Summary::iterations entries kept (out_trace)
     int32_t pose_f[BA_KMAX];     // f-offset of pose k or -1 (constant / unused)
     int32_t vel_f[BA_KMAX];      // f-offset of velocity k or -1
     int32_t bg_f, ba_f;
@@ -35,6 +35,7 @@ struct BaWin {
     int64_t o_kfptr;             // into kf_ptr (K+1 entries)
     int64_t o_ws;                // into the f64 workspace
     int64_t o_out;               // into the f64 output pool
+    int64_t o_tr;                // into the per-iteration trace pool (out_trace)
 };
 
 // pooled device arrays of a batch
@@ -60,6 +61,7 @@ struct BaPools {
     uint8_t* out_bad;            // [sum L] SetBad decisions
     int32_t* out_i32;            // per-window summary ints [n][8]
     double* out_sum;             // per-window summary doubles [n][4]
+    vio_ba_iteration* out_trace; // per-window Summary::iterations [sum tr_cap]
     unsigned long long* prof;    // optional [n][VIO_BA_PROF_SLOTS] per-phase shader clocks (diagnostics), may be null
     int route;                   // 0: ba_window_kernel solves every window; 1: it solves the PnP windows
                                  // only and the phase kernels (ba_phases.inc) the others

@@ -4,7 +4,8 @@
 // INTER_AREA when the image size differs (3840x1920 -> 960x480 in the demo configuration).
 // OpenCV 4.x takes its integer-factor "area fast" path there (modules/imgproc/src/resize.cpp,
 // resizeAreaFast_ for uchar): dst = saturate_cast<uchar>(Σ block · (1.f / (fx·fy))), i.e. the block
-// sum times the f32 reciprocal, rounded half-to-even.  Integer factors only (fx = W / dW,
+// sum times the f32 reciprocal, rounded half-to-even — except 2x2 blocks, which OpenCV's
+// ResizeAreaFastVec handles as (a + b + c + d + 2) >> 2 (round half up).  Integer factors only (fx = W / dW,
 // fy = H / dH exact); other sizes return VIO_ENOSYS.  OpenCV is not in /root/reference nor in
 // this image, so parity with it is unpinned; the oracle restates that formula
 // (oracle/resize_oracle.py) and the GPU matches it bitwise.
@@ -82,7 +83,9 @@ __global__ __launch_bounds__(256) void resize_area_kernel(ResizeArgs a) {
     int sum = 0;
     for (int k = 0; k < a.fy; ++k)
         for (int j = 0; j < a.fx; ++j) sum += s[(long long)k * a.stride + j];
-    a.dst[f * a.frame_bytes_dst + (long long)y * a.dstride + x] = area_round(sum, a.scale);
+    // 2x2: ResizeAreaFastVec's (sum + 2) >> 2; every other factor: sum * (1.f / (fx fy)), cvRound
+    a.dst[f * a.frame_bytes_dst + (long long)y * a.dstride + x] =
+        (a.fx == 2 && a.fy == 2) ? (uint8_t)((sum + 2) >> 2) : area_round(sum, a.scale);
 }
 
 }  // namespace vio360

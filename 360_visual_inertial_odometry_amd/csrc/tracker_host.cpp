@@ -326,6 +326,7 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
 
 int upload_frame(erp_tracker* t, int slot, const uint8_t* img, int stride) {
     if (!img || stride < t->W) { set_error(t->ctx, "bad frame"); return VIO_EINVAL; }
+    VIO_HIP(t->ctx, hipSetDevice(t->ctx->device));
     VIO_HIP(t->ctx, hipMemcpy2DAsync(t->lvl[slot][0], t->lp[0], img, stride, t->W, t->H, hipMemcpyHostToDevice,
                                      t->ctx->stream));
     return VIO_OK;
@@ -336,6 +337,10 @@ int read_corners(erp_tracker* t, float* out_xy, int* n_out) {
     int sc[10];
     VIO_HIP(t->ctx, hipMemcpyAsync(sc, t->d_scal, sizeof(sc), hipMemcpyDeviceToHost, t->ctx->stream));
     VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    if ((unsigned int)sc[3] > t->cand_cap) {  // NMS survivors beyond the candidate buffer: the corner set
+        set_error(t->ctx, "GFTT candidate buffer overflow");  // would differ from goodFeaturesToTrack
+        return VIO_ENOSYS;
+    }
     inc = sc[9];
     if (inc) {  // the top-K subset did not decide: exact pass over every candidate
         hipError_t e = launch_gftt_full(t->last_gf, (unsigned int)sc[3], t->d_sort_tmp, t->sort_tmp_bytes,
@@ -402,6 +407,7 @@ int erp_tracker_upload_resized(erp_tracker* t, int slot, const uint8_t* img, int
     if (!t || slot < 0 || slot > 1 || !img || W <= 0 || H <= 0 || stride < W) return VIO_EINVAL;
     if (W == t->W && H == t->H) return upload_frame(t, slot, img, stride);
     vio_ctx* ctx = t->ctx;
+    VIO_HIP(ctx, hipSetDevice(ctx->device));
     const int sp = (W + 15) & ~15;  // 16-byte rows: the resize fast path
     uint8_t* d_src = static_cast<uint8_t*>(ctx_buffer(ctx, kSlotResizeSrc, (size_t)sp * H));
     if (!d_src) {
@@ -444,6 +450,7 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         set_error(t->ctx, "bad erp_tracker_params");
         return VIO_EINVAL;
     }
+    VIO_HIP(t->ctx, hipSetDevice(t->ctx->device));
     if ((rc = ensure_iters(t, std::max(p->ransac_iters, 1)))) return rc;
     if ((rc = ensure_gftt(t, p->min_dist))) return rc;
     hipStream_t st = t->ctx->stream;
@@ -575,14 +582,7 @@ int erp_gftt(vio_ctx* ctx, const uint8_t* img, const uint8_t* mask, int W, int H
         }
         if (!rc) rc = enqueue_gftt(t, t->lvl[1][0], t->lp[0], dmask, t->lp[0], max_corners, quality, min_dist, false,
                                    0, 0.f);
-        if (!rc) rc = read_corners(t, out_xy, n_out);
-        if (!rc) {
-            unsigned int nc = 0;
-            if (hipMemcpy(&nc, t->d_scal + 3, sizeof(nc), hipMemcpyDeviceToHost) == hipSuccess && nc > t->cand_cap) {
-                set_error(ctx, "GFTT candidate buffer overflow");
-                rc = VIO_ENOSYS;
-            }
-        }
+        if (!rc) rc = read_corners(t, out_xy, n_out);  // reports a candidate-buffer overflow
     }
     erp_tracker_destroy(t);
     return rc;

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define VIO360_ABI_VERSION 1
+#define VIO360_ABI_VERSION 2
 
 /* ----------------------------------------------------------------------------------------- */
 /* error codes                                                                                */
@@ -145,6 +145,26 @@ typedef struct {
     double _pad1;
 } vio_ba_summary;
 
+/* One entry of Ceres Solver::Summary::iterations (ceres/iteration_callback.h IterationSummary), pushed
+   where TrustRegionMinimizer::FinalizeIterationAndCheckIfMinimizerCanContinue pushes it
+   (trust_region_minimizer.cc:313-348): iteration 0 (IterationZero :195-229), every valid, invalid
+   (HandleInvalidStep :453-486), accepted (HandleSuccessfulStep :806-826) or rejected (:118-129) step;
+   an iteration that ends the solve on the parameter / function tolerance is not pushed (:108-114).
+   The reference reads Summary::iterations.size() (src/optimization/Optimizer.cpp:481-483). */
+typedef struct {
+    int32_t iteration;
+    int32_t step_is_valid;
+    int32_t step_is_successful;
+    int32_t _pad;
+    double cost;                /* x or candidate cost + fixed cost */
+    double cost_change;         /* x_cost - candidate_cost (0 for an invalid step) */
+    double gradient_max_norm;   /* |x - Plus(x, -g)|_inf of the last linearisation */
+    double step_norm;           /* |x - candidate| */
+    double relative_decrease;   /* TrustRegionStepEvaluator::StepQuality */
+    double trust_region_radius; /* after the step's radius update */
+    double model_cost_change;   /* -(J h)^T (r + J h / 2); not an IterationSummary field (margin analysis) */
+} vio_ba_iteration;
+
 /* outputs, caller-owned; any pointer may be NULL if not wanted */
 typedef struct {
     vio_pose* T_wb;           /* K: SE3(T_wb_init) * exp(delta) (constant poses: SE3(T_wb_init)) */
@@ -156,6 +176,11 @@ typedef struct {
     double* bg;               /* 3 (VI) */
     double* ba;               /* 3 (VI) */
     vio_ba_summary* summary;  /* 1 */
+    /* per-iteration trace (Summary::iterations): up to trace_cap entries, summary->iterations of them
+       (PnP: the rounds' traces one after another); may be NULL */
+    vio_ba_iteration* trace;
+    int32_t trace_cap;
+    int32_t _pad2;
 } vio_ba_output;
 
 int vio_ba_solve(vio_ctx* ctx, const vio_ba_problem* prob, vio_ba_output* out);

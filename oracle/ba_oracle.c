@@ -644,10 +644,9 @@ typedef struct {
     int iterations; /* iterations.size() */
     int successful, unsuccessful;
     double initial_cost, final_cost;
-    /* trace for tests */
+    /* Solver::Summary::iterations (tests compare it with the HIP path's trace) */
     int trace_n;
-    double trace_cost[64], trace_radius[64];
-    int trace_ok[64];
+    vio_ba_iteration trace[256];
 } lm_summary;
 
 void oracle_lm_default_options(lm_options* o) {
@@ -678,13 +677,21 @@ void oracle_lm_step_rejected(lm_radius* s) {
     s->decrease_factor *= 2.0;
 }
 
-static void push_trace(lm_summary* sum, double cost, double radius, int ok) {
-    if (sum->trace_n < 64) {
-        sum->trace_cost[sum->trace_n] = cost;
-        sum->trace_radius[sum->trace_n] = radius;
-        sum->trace_ok[sum->trace_n] = ok;
+/* FinalizeIterationAndCheckIfMinimizerCanContinue pushes the iteration summary (trust_region_minimizer.cc:313-348) */
+static void push_trace(lm_summary* sum, const vio_ba_iteration* it, double radius) {
+    if (sum->trace_n < 256) {
+        sum->trace[sum->trace_n] = *it;
+        sum->trace[sum->trace_n].trust_region_radius = radius;
         sum->trace_n++;
     }
+}
+
+/* gradient_max_norm = |x - Plus(x, -g)|_inf (trust_region_minimizer.cc:288-299; Plus is x + delta:
+   no local parameterization is registered), which differs from |g|_inf by the roundoff of x - g */
+static double grad_max_norm(int n, const double* x, const double* g) {
+    double m = 0.0;
+    for (int i = 0; i < n; ++i) m = fmax(m, fabs(x[i] - (x[i] + (-g[i]))));
+    return m;
 }
 
 /* LM diagonal D = sqrt(clamp(diag(J~^T J~), min, max) / radius) (levenberg_marquardt_strategy.cc:76-88),
@@ -729,9 +736,13 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
         goto done;
     }
     for (int i = 0; i < n; ++i) s[i] = 1.0 / (1.0 + sqrt(colsq[i]));
-    double gmax = 0;
-    for (int i = 0; i < n; ++i) gmax = fmax(gmax, fabs(g[i]));
+    double gmax = grad_max_norm(n, x, g);
     sum->initial_cost = x_cost + opt->fixed_cost;
+    vio_ba_iteration it; /* IterationZero (:195-229) */
+    memset(&it, 0, sizeof it);
+    it.step_is_valid = it.step_is_successful = 1;
+    it.cost = x_cost + opt->fixed_cost;
+    it.gradient_max_norm = gmax;
     double step_evaluator_current = x_cost;
     int iteration = 0;
     int step_successful = 1;
@@ -752,12 +763,14 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
         }
         sum->iterations++;
         final_cost = fmin(final_cost, iter_cost);
-        push_trace(sum, iter_cost, rad.radius, step_successful);
+        push_trace(sum, &it, rad.radius);
         if (iteration >= opt->max_iterations) { sum->termination = VIO_TERM_NO_CONVERGENCE; break; }
         if (!fixed && step_successful && gmax <= opt->gradient_tolerance) { sum->termination = VIO_TERM_CONVERGENCE; break; }
         if (!fixed && rad.radius <= opt->min_radius) { sum->termination = VIO_TERM_CONVERGENCE; break; }
 
         iteration++;
+        memset(&it, 0, sizeof it);
+        it.iteration = iteration;
         /* ComputeTrustRegionStep */
         oracle_lm_diagonal(n, colsq, s, rad.radius, opt->min_diagonal, opt->max_diagonal, D);
         int valid = P->solve(P->user, s, D, y);
@@ -765,13 +778,15 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
             for (int i = 0; i < n; ++i)
                 if (!isfinite(y[i])) valid = 0;
         }
+        model_change = 0.0;
         if (valid) {
             for (int i = 0; i < n; ++i) y[i] = -y[i]; /* trust_region_step */
             model_change = P->model_change(P->user, s, y);
             valid = model_change > 0.0;
         }
+        it.model_cost_change = model_change;
         if (!valid) {
-            /* HandleInvalidStep */
+            /* HandleInvalidStep (:453-486): a zero-length, no-progress iteration */
             if (++consecutive_invalid >= opt->max_consecutive_invalid) {
                 sum->termination = VIO_TERM_FAILURE;
                 break;
@@ -779,8 +794,11 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
             oracle_lm_step_rejected(&rad);
             step_successful = 0;
             iter_cost = x_cost + opt->fixed_cost;
+            it.cost = iter_cost;
+            it.gradient_max_norm = gmax;
             continue;
         }
+        it.step_is_valid = 1;
         consecutive_invalid = 0;
         for (int i = 0; i < n; ++i) delta[i] = y[i] * s[i];
         for (int i = 0; i < n; ++i) cand[i] = x[i] + delta[i];
@@ -790,6 +808,8 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
         double step_norm = 0;
         for (int i = 0; i < n; ++i) { double d = x[i] - cand[i]; step_norm += d * d; }
         step_norm = sqrt(step_norm);
+        it.step_norm = step_norm;
+        it.cost_change = x_cost - cand_cost;
         if (!fixed && step_norm <= opt->parameter_tolerance * (x_norm + opt->parameter_tolerance)) {
             sum->termination = VIO_TERM_CONVERGENCE;
             break;
@@ -803,6 +823,7 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
         double rel;
         if (cand_cost >= DBL_MAX) rel = -DBL_MAX;
         else rel = (step_evaluator_current - cand_cost) / model_change;
+        it.relative_decrease = rel;
         if (rel > opt->min_relative_decrease) {
             /* HandleSuccessfulStep */
             memcpy(x, cand, sizeof(double) * n);
@@ -813,8 +834,7 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
                 sum->termination = VIO_TERM_FAILURE;
                 break;
             }
-            gmax = 0;
-            for (int i = 0; i < n; ++i) gmax = fmax(gmax, fabs(g[i]));
+            gmax = grad_max_norm(n, x, g);
             step_successful = 1;
             oracle_lm_step_accepted(&rad, rel);
             step_evaluator_current = cand_cost;
@@ -824,6 +844,9 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
             iter_cost = cand_cost + opt->fixed_cost;
             oracle_lm_step_rejected(&rad);
         }
+        it.step_is_successful = step_successful;
+        it.cost = iter_cost;
+        it.gradient_max_norm = gmax; /* kept from the last successful step when rejected (:118-129) */
     }
     sum->final_cost = final_cost;
 done:
@@ -1320,6 +1343,13 @@ static void write_pose(const pose_ctx* pc, const double* delta, vio_pose* out) {
     se3_mul(pc->R_init, pc->t_init, dR, dt, out->R, out->t);
 }
 
+static void trace_append(vio_ba_output* out, const lm_summary* sum, int* n) {
+    for (int i = 0; i < sum->trace_n && i < sum->iterations; ++i) {
+        if (out->trace && *n < out->trace_cap) out->trace[*n] = sum->trace[i];
+        (*n)++;
+    }
+}
+
 int oracle_ba_solve(const vio_ba_problem* p, vio_ba_output* out) {
     if (!p || !out || p->num_kf <= 0 || p->num_lm < 0 || p->num_obs < 0) return VIO_EINVAL;
     if (p->variant == VIO_BA_VI && (!p->preint || !p->preint_valid || !p->vel)) return VIO_EINVAL;
@@ -1337,11 +1367,13 @@ int oracle_ba_solve(const vio_ba_problem* p, vio_ba_output* out) {
     uint8_t* outl = (uint8_t*)calloc(N > 0 ? N : 1, 1);
     const uint8_t* marg = c.is_pnp ? p->lm_const : p->lm_marg;
 
+    int trace_n = 0;
     if (c.is_pnp) {
         int rounds = p->num_rounds > 0 ? p->num_rounds : 4;
         for (int round = 0; round < rounds; ++round) {
             memset(c.pose_val, 0, sizeof(double) * 6 * K);
             ba_ceres_solve(&c, &opt, &sum);
+            trace_append(out, &sum, &trace_n);
             if (round == 0) S.initial_cost = sum.initial_cost;
             S.iterations += sum.iterations;
             S.num_successful_steps += sum.successful;
@@ -1371,6 +1403,7 @@ int oracle_ba_solve(const vio_ba_problem* p, vio_ba_output* out) {
         S.fixed_cost = 0;
     } else {
         ba_ceres_solve(&c, &opt, &sum);
+        trace_append(out, &sum, &trace_n);
         S.initial_cost = sum.initial_cost;
         S.final_cost = sum.final_cost;
         S.iterations = sum.iterations;
@@ -1585,21 +1618,4 @@ void oracle_lm_radius_schedule(double initial_radius, double max_radius, const d
         else oracle_lm_step_rejected(&s);
         radii[i] = s.radius;
     }
-}
-
-/* summary trace for one solve (LM trace goldens): runs the problem and returns the trace */
-int oracle_ba_trace(const vio_ba_problem* p, double* costs, double* radii, int* ok, int cap, int* n_out) {
-    ba_ctx c;
-    ba_ctx_build(&c, p);
-    lm_options opt;
-    oracle_lm_default_options(&opt);
-    opt.max_iterations = p->max_iterations;
-    opt.fixed_iterations = p->fixed_iterations;
-    lm_summary sum;
-    ba_ceres_solve(&c, &opt, &sum);
-    int n = sum.trace_n < cap ? sum.trace_n : cap;
-    for (int i = 0; i < n; ++i) { costs[i] = sum.trace_cost[i]; radii[i] = sum.trace_radius[i]; ok[i] = sum.trace_ok[i]; }
-    *n_out = n;
-    ba_ctx_free(&c);
-    return 0;
 }

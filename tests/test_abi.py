@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol(vio):
 
 
 def test_abi_version(vio):
-    assert vio.lib().vio_abi_version() == 1
+    assert vio.lib().vio_abi_version() == 2
 
 
 STRUCTS = {
@@ -39,7 +39,10 @@ STRUCTS = {
                                         "kf_const", "lm_xyz", "obs_uv", "preint", "vel", "bg", "gravity",
                                         "max_iterations", "fixed_iterations", "num_rounds"]),
     "vio_ba_summary": ("VioBaSummary", ["success", "num_bad_lm", "initial_cost", "fixed_cost"]),
-    "vio_ba_output": ("VioBaOutput", ["T_wb", "lm_xyz", "obs_outlier", "summary"]),
+    "vio_ba_output": ("VioBaOutput", ["T_wb", "lm_xyz", "obs_outlier", "summary", "trace", "trace_cap"]),
+    "vio_ba_iteration": ("VioBaIteration", ["iteration", "step_is_valid", "step_is_successful", "cost",
+                                            "cost_change", "gradient_max_norm", "step_norm", "relative_decrease",
+                                            "trust_region_radius", "model_cost_change"]),
     "vio_imu_data": ("VioImuData", ["timestamp", "ax", "az", "gx", "gz"]),
     "vio_imu_noise": ("VioImuNoise", ["gyro_noise", "accel_bias_noise"]),
     "erp_klt_params": ("ErpKltParams", ["win", "max_level", "epsilon", "min_eig_threshold"]),

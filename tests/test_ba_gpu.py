@@ -60,29 +60,123 @@ def all_cases(vio, synth):
     return cases(vio, synth)
 
 
+# ---- LM trace parity (Solver::Summary::iterations, vio_ba_output.trace) ----------------------------
+PERTURB = (1e-15, -1e-15, 1e-14, -1e-14)  # relative changes of the landmark inputs: 5-50 ulp
+
+
+def oracle_cloud(vio, w, variant, **kw):
+    """The oracle on the window and on copies whose landmark inputs moved by a few ulp: how far
+    the reference algorithm itself moves under input roundoff (its numerical sensitivity)."""
+    return [oracle_lib.ba_solve(vio, vio.BaProblem(dict(w, lm_xyz=w["lm_xyz"] * (1 + e)), variant=variant, **kw))
+            for e in PERTURB]
+
+
+def roundoff_decided(tr, i, fixed):
+    """Is iteration i's accept / stop decision decided by roundoff?  Its margin in cost units —
+    |cost_change - 1e-3 model_change| for the rho > 1e-3 test (trust_region_step_evaluator.cc),
+    ||cost_change| - 1e-6 cost| for the function tolerance (trust_region_minimizer.cc:740-760) — is
+    within 1e-11 of the cost, i.e. within the roundoff of a cost summed over thousands of terms."""
+    if not tr["step_is_valid"][i] or i == 0:
+        return False
+    cost, dc, m = tr["cost"][i - 1], tr["cost_change"][i], tr["model_cost_change"][i]
+    tol = 1e-11 * abs(cost)
+    if abs(dc - 1e-3 * m) <= tol:
+        return True
+    return not fixed and abs(abs(dc) - 1e-6 * abs(cost)) <= tol
+
+
+def compare_traces(o, g, cloud, fixed, min_prefix):
+    """GPU vs oracle Summary::iterations up to the first roundoff-decided iteration (or the first
+    where the perturbed oracles disagree on a decision): identical decisions and iteration numbers,
+    and per-iteration costs within max(1e-12, 10 x the perturbed-oracle spread) relative.  Returns
+    the compared prefix length."""
+    to, tg = o["trace"], g["trace"]
+    n = min(len(to["cost"]), len(tg["cost"]))
+    stop = n
+    for i in range(n):
+        dis = any(i >= len(c["trace"]["cost"]) or c["trace"]["step_is_successful"][i] != to["step_is_successful"][i]
+                  for c in cloud)
+        if roundoff_decided(to, i, fixed) or dis:
+            stop = i
+            break
+    assert stop >= min_prefix, (stop, min_prefix)
+    for i in range(stop):
+        assert tg["iteration"][i] == to["iteration"][i] == i
+        assert tg["step_is_valid"][i] == to["step_is_valid"][i], i
+        assert tg["step_is_successful"][i] == to["step_is_successful"][i], i
+        env = max(abs(c["trace"]["cost"][i] - to["cost"][i]) for c in cloud) / to["cost"][i]
+        rel = abs(tg["cost"][i] - to["cost"][i]) / to["cost"][i]
+        assert rel <= max(1e-12, 10 * env), (i, rel, env)
+        assert abs(tg["trust_region_radius"][i] - to["trust_region_radius"][i]) <= \
+            max(1e-9, 10 * max(abs(c["trace"]["trust_region_radius"][i] - to["trust_region_radius"][i])
+                               for c in cloud) / to["trust_region_radius"][i]) * to["trust_region_radius"][i], i
+    return stop
+
+
+TRACE_CASES = [  # (case index in cases(), solver kwargs, min compared prefix)
+    (2, {}, 30),                                            # config 3, reference options (tolerance-terminated)
+    (2, dict(max_iterations=30, fixed_iterations=1), 31),   # config 3, the timed fixed-iteration mode
+    (5, dict(max_iterations=40, fixed_iterations=1), 20),   # VI K=6 far past convergence
+    (0, {}, 5),                                             # config 2 LocalBA
+    (3, {}, 5),                                             # LocalBA with marginalised MPs and outliers
+]
+
+
+@pytest.mark.parametrize("tc", range(len(TRACE_CASES)))
+def test_lm_trace_matches_oracle(vio, gpu_ctx, all_cases, tc):
+    """Per-iteration LM trace (cost, step validity / acceptance, radius) of both execution routes
+    against the oracle's, up to the first decision that roundoff decides (VI bar)."""
+    idx, kw, min_prefix = TRACE_CASES[tc]
+    name, w, var = all_cases[idx]
+    fixed = bool(kw.get("fixed_iterations", 0))
+    p = vio.BaProblem(w, variant=var, **kw)
+    o = oracle_lib.ba_solve(vio, p)
+    cloud = oracle_cloud(vio, w, var, **kw)
+    solo = gpu_ctx.ba_solve([p])[0]            # phase route
+    mono = gpu_ctx.ba_solve([p] * 33)[0]       # single-kernel route (batch above the phase-route size)
+    for g in (solo, mono):
+        assert len(g["trace"]["cost"]) == g["iterations"]
+        compare_traces(o, g, cloud, fixed, min(min_prefix, o["iterations"]))
+
+
+def test_pnp_trace_rounds(vio, gpu_ctx, all_cases):
+    """SolvePnP's four outlier rounds each restart Ceres: the trace holds the rounds one after
+    another, iteration numbers restarting at 0, equal to the oracle's (6 parameters: well conditioned)."""
+    name, w, var = all_cases[6]
+    p = vio.BaProblem(w, variant=var)
+    o, g = oracle_lib.ba_solve(vio, p), gpu_ctx.ba_solve([p])[0]
+    to, tg = o["trace"], g["trace"]
+    assert len(tg["cost"]) == g["iterations"] == o["iterations"] == len(to["cost"])
+    assert (to["iteration"] == 0).sum() == 4 and np.array_equal(tg["iteration"], to["iteration"])
+    assert np.array_equal(tg["step_is_successful"], to["step_is_successful"])
+    assert np.allclose(tg["cost"], to["cost"], rtol=1e-9, atol=0)
+
+
 def assert_parity_vi_converged(vio, w, o, g, **kw):
     """VI windows with the reference's IMU information (the rotation block of the preintegrated
     covariance is never propagated, IMUPreintegrator.cpp:240-274, so its sqrt-information is 1e4)
-    are ill-conditioned near the optimum: a 1e-13 relative perturbation of the input moves the
-    ORACLE's own converged answer by ~1e-4 m (poses) / ~1e-3 m (landmarks) and changes its
-    iteration count (43 vs 47 on config 3), because late accept / stop decisions flip.  So for
-    tolerance-terminated VI solves the bar is the oracle's own roundoff sensitivity, measured here:
-    GPU-vs-oracle differences must stay within 3x the oracle-vs-perturbed-oracle differences (and
-    within 1e-3 m / 1e-2 m / 1e-4 rel cost absolutely).  The fixed-iteration trajectory itself is
-    compared at the tight bar (test_ba_parity_fixed_iterations)."""
-    w2 = dict(w, lm_xyz=w["lm_xyz"] * (1 + 1e-13))
-    o2 = oracle_lib.ba_solve(vio, vio.BaProblem(w2, variant=vio.VIO_BA_VI, **kw))
-    dt_self = np.abs(o["T_wb"][:, :3, 3] - o2["T_wb"][:, :3, 3]).max()
-    dl_self = np.abs(o["lm_xyz"] - o2["lm_xyz"]).max()
-    dc_self = abs(o["final_cost"] - o2["final_cost"])
+    are ill-conditioned near the optimum: the oracle's own answer moves by ~2e-4 m (poses) / ~2e-3 m
+    (landmarks) and its iteration count by up to 8 when its landmark inputs move by 1e-15..1e-14
+    relative (a few ulp) — the per-iteration traces (test_lm_trace_matches_oracle) show that
+    difference growing smoothly from 1e-16 at iteration 0, not a flipped decision.  So for
+    tolerance-terminated VI solves the bar is that perturbed-oracle cloud: GPU-vs-oracle
+    differences within 2x its largest member's (and within 1e-4 m / 1e-3 m when the cloud is tighter),
+    iterations inside the cloud's range +-1, final cost within 2x the cloud's spread or 1e-6."""
+    cloud = oracle_cloud(vio, w, vio.VIO_BA_VI, **kw)
+    dt_c = max(np.abs(o["T_wb"][:, :3, 3] - c["T_wb"][:, :3, 3]).max() for c in cloud)
+    dl_c = max(np.abs(o["lm_xyz"] - c["lm_xyz"]).max() for c in cloud)
+    dc_c = max(abs(o["final_cost"] - c["final_cost"]) for c in cloud)
+    dr_c = max(rot_angle(o["T_wb"][k, :3, :3], c["T_wb"][k, :3, :3]) for c in cloud for k in range(len(o["T_wb"])))
     dt = np.abs(o["T_wb"][:, :3, 3] - g["T_wb"][:, :3, 3]).max()
     dl = np.abs(o["lm_xyz"] - g["lm_xyz"]).max()
     dc = abs(o["final_cost"] - g["final_cost"])
-    assert dt <= min(1e-3, max(1e-4, 3 * dt_self)), (dt, dt_self)
-    assert dl <= min(1e-2, max(1e-3, 3 * dl_self)), (dl, dl_self)
-    assert dc <= min(1e-4 * o["final_cost"], max(1e-6 * o["final_cost"], 3 * dc_self)), (dc, dc_self)
+    assert dt <= max(1e-4, 2 * dt_c), (dt, dt_c)
+    assert dl <= max(1e-3, 2 * dl_c), (dl, dl_c)
+    assert dc <= max(1e-6 * o["final_cost"], 2 * dc_c), (dc, dc_c)
     for k in range(len(o["T_wb"])):
-        assert rot_angle(o["T_wb"][k, :3, :3], g["T_wb"][k, :3, :3]) <= 1e-4, k
+        assert rot_angle(o["T_wb"][k, :3, :3], g["T_wb"][k, :3, :3]) <= max(1e-5, 2 * dr_c), k
+    its = [o["iterations"]] + [c["iterations"] for c in cloud]
+    assert min(its) - 1 <= g["iterations"] <= max(its) + 1, (g["iterations"], its)
     assert abs(o["initial_cost"] - g["initial_cost"]) <= 1e-9 * o["initial_cost"]
     assert g["success"] == o["success"] == 1
 
@@ -118,8 +212,9 @@ def test_ba_parity_fixed_iterations(vio, gpu_ctx, all_cases, idx, iters):
 
 def test_ba_vi_long_fixed_trajectory(vio, gpu_ctx, all_cases):
     """40 fixed LM iterations on a VI window run past convergence, where accept / reject decisions
-    are made on roundoff-sized cost changes (the oracle's own 1e-13-perturbed run flips them too):
-    judged at the oracle self-sensitivity bar, with the iteration count exact."""
+    are made on roundoff-sized cost changes (from iteration 26 on the decision margins are within
+    1e-11 of the cost; the oracle's own perturbed runs flip them too): judged at the perturbed-oracle
+    cloud bar, with the iteration count exact."""
     name, w, var = all_cases[5]
     assert var == vio.VIO_BA_VI
     kw = dict(max_iterations=40, fixed_iterations=1)
@@ -199,17 +294,36 @@ def test_edge_cases(vio, synth, gpu_ctx):
 
 
 def test_config4_full_size_properties(vio, synth, gpu_ctx):
-    """256 VIO windows (config 4 shape) in one launch: every window converges (cost drops by orders
-    of magnitude, success) and sampled windows match the oracle (converged answers at the VI bar,
-    fixed-iteration trajectories at the tight bar).  Closeness to the synthetic ground truth is not
-    a property of the reference solver here: from the perturbed start the oracle (Ceres LM) stops in a
-    different (higher-cost) minimum than from the truth, so it is not asserted."""
+    """256 VIO windows (config 4 shape) in one launch against the oracle's converged results for
+    all 256 (tests/golden/config4_oracle.json, tests/golden/gen_config4_summary.py): initial costs
+    to 1e-9, final costs within 2e-4 (the perturbed-oracle cloud reaches 3.4e-5 on window 0),
+    iteration counts per window within 10 and in total within 2 %, the improvement of the pose
+    error over the perturbed start (final / initial distance to the synthetic truth) per window
+    within 0.05 of the oracle's and on average within 0.01; sampled windows at the VI bar and
+    fixed-iteration trajectories at the tight bar."""
+    import json
+    import os
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "config4_oracle.json")))["windows"]
     ws = synth.config4(256)
     probs = [vio.BaProblem(w, variant=vio.VIO_BA_VI) for w in ws]
     res = gpu_ctx.ba_solve(probs)
-    for g in res:
-        assert g["success"] == 1 and g["final_cost"] < 1e-2 * g["initial_cost"]
-    # converged answers of sampled windows at the VI parity bar (oracle self-sensitivity)
+    ratio_g, ratio_o, it_g, it_o = [], [], [], []
+    for w, g, r in zip(ws, res, ref):
+        assert g["success"] == r["success"] == 1 and g["final_cost"] < 1e-2 * g["initial_cost"]
+        assert abs(g["initial_cost"] - r["initial_cost"]) <= 1e-9 * r["initial_cost"], r["window"]
+        assert abs(g["final_cost"] - r["final_cost"]) <= 2e-4 * r["final_cost"], r["window"]
+        assert abs(g["iterations"] - r["iterations"]) <= 10, (r["window"], g["iterations"], r["iterations"])
+        e0 = np.abs(w["T_wb_init"][:, :3, 3] - w["T_wb_true"][:, :3, 3]).mean()
+        e1 = np.abs(g["T_wb"][:, :3, 3] - w["T_wb_true"][:, :3, 3]).mean()
+        ratio_g.append(e1 / e0)
+        ratio_o.append(r["pose_err_final"] / r["pose_err_init"])
+        it_g.append(g["iterations"])
+        it_o.append(r["iterations"])
+    ratio_g, ratio_o = np.array(ratio_g), np.array(ratio_o)
+    assert np.abs(ratio_g - ratio_o).max() <= 0.05
+    assert abs(ratio_g.mean() - ratio_o.mean()) <= 0.01 and ratio_g.mean() < 0.2
+    assert abs(sum(it_g) - sum(it_o)) <= 0.02 * sum(it_o), (sum(it_g), sum(it_o))
+    # converged answers of sampled windows at the VI parity bar (oracle perturbation cloud)
     for i in (0, 255):
         assert_parity_vi_converged(vio, ws[i], oracle_lib.ba_solve(vio, probs[i]), res[i])
     fixed = [vio.BaProblem(ws[i], variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1) for i in (0, 97, 255)]

@@ -73,3 +73,6 @@ def test_resize_oracle_closed_forms():
             b[:] = 1
             b[:k - 16] = 2
         assert ro.resize_area(b.reshape(4, 4), 1, 1)[0, 0] == want, k
+    # factor 2x2 takes OpenCV's ResizeAreaFastVec: (a + b + c + d + 2) >> 2 = round half UP
+    for blk, want in [((1, 1, 0, 0), 1), ((1, 0, 0, 0), 0), ((1, 1, 1, 0), 1), ((3, 3, 0, 0), 2), ((255,) * 4, 255)]:
+        assert ro.resize_area(np.array(blk, np.uint8).reshape(2, 2), 1, 1)[0, 0] == want, blk

@@ -186,3 +186,45 @@ def test_factor_jacobian_finite_difference(vio):
             assert np.allclose(fd, Jl.reshape(2, 3)[:, j], rtol=1e-4, atol=1e-3), (i, j)
         checked += 1
     assert checked >= 20
+
+
+@pytest.mark.parametrize("kw", [{}, dict(max_iterations=12, fixed_iterations=1)])
+def test_oracle_trace_is_ceres_summary(vio, synth, kw):
+    """Summary::iterations of the oracle obey Ceres' bookkeeping (trust_region_minimizer.cc): one
+    entry per iteration incl. 0, iteration 0 valid + successful at initial_cost, final_cost = the
+    smallest entry cost, the radius follows LevenbergMarquardtStrategy (accept: /max(1/3, 1-(2rho-1)^3),
+    reject / invalid: /2, /4, ...), and an unsuccessful entry keeps the previous gradient norm."""
+    import oracle_lib
+    p = vio.BaProblem(synth.config3(), variant=vio.VIO_BA_VI, **kw)
+    o = oracle_lib.ba_solve(vio, p)
+    t = o["trace"]
+    n = o["iterations"]
+    assert len(t["cost"]) == n > 3
+    assert list(t["iteration"]) == list(range(n))
+    assert t["step_is_valid"][0] == t["step_is_successful"][0] == 1 and t["cost"][0] == o["initial_cost"]
+    assert o["final_cost"] == t["cost"].min()
+    assert t["trust_region_radius"][0] == 1e4
+    dec = 2.0
+    for i in range(1, n):
+        r0, r1 = t["trust_region_radius"][i - 1], t["trust_region_radius"][i]
+        if t["step_is_successful"][i]:
+            q = t["relative_decrease"][i]
+            assert q > 1e-3 and r1 == min(1e16, r0 / max(1 / 3, 1 - (2 * q - 1) ** 3))
+            dec = 2.0
+        else:
+            assert r1 == r0 / dec and t["gradient_max_norm"][i] == t["gradient_max_norm"][i - 1]
+            dec *= 2.0
+        if t["step_is_valid"][i]:
+            assert t["model_cost_change"][i] > 0
+
+
+def test_config4_fixture_reproduces(vio, synth):
+    """tests/golden/config4_oracle.json (the GPU config-4 test's reference) is this oracle's output."""
+    import json
+    import oracle_lib
+    ref = json.load(open(os.path.join(GOLDEN, "config4_oracle.json")))["windows"]
+    assert len(ref) == 256
+    for i in (1, 3):
+        o = oracle_lib.ba_solve(vio, vio.BaProblem(synth.config3(synth.SEED + i), variant=vio.VIO_BA_VI))
+        assert o["iterations"] == ref[i]["iterations"] and o["final_cost"] == ref[i]["final_cost"]
+        assert o["initial_cost"] == ref[i]["initial_cost"]

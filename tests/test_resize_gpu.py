@@ -34,6 +34,16 @@ def test_erp_frame_and_strided_source(ctx, synth):
     np.testing.assert_array_equal(ctx.resize_area(view, 240, 120), ro.resize_area(view, 240, 120))
 
 
+def test_factor2_rounds_half_up(ctx):
+    """2x2 blocks follow OpenCV's ResizeAreaFastVec, (a + b + c + d + 2) >> 2: {1,1,0,0} -> 1 (round
+    half up), not the half-to-even 0 of the generic area-fast formula."""
+    blocks = np.array([[1, 1, 0, 0], [1, 0, 0, 0], [3, 3, 0, 0], [1, 1, 1, 0]], np.uint8)
+    img = np.zeros((2, 8), np.uint8)
+    for i, b in enumerate(blocks):
+        img[:, 2 * i:2 * i + 2] = b.reshape(2, 2)
+    np.testing.assert_array_equal(ctx.resize_area(img, 4, 1)[0], [1, 0, 2, 1])
+
+
 def test_non_integer_factor_rejected(vio, ctx):
     with pytest.raises(vio.VioError):
         ctx.resize_area(np.zeros((480, 960), np.uint8), 640, 320)
