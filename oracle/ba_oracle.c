@@ -615,6 +615,283 @@ void oracle_imu_factor(const vio_preint* p, const double* g, const vio_pose* Ti,
 }
 
 /* ========================================================================================= */
+/* Block-sparse Schur complement (Ceres SchurEliminator::Eliminate / BackSubstitute,           */
+/* internal/ceres/schur_eliminator_impl.h:179-377; DENSE/SPARSE_SCHUR's reduced system,        */
+/* schur_complement_solver.cc:118-176).  Generic over block sizes: the BA step (ba_solve) and   */
+/* the restated Ceres fixtures (LinearLeastSquaresProblem2/4 with schur_eliminator_test.cc)     */
+/* run the same code.                                                                         */
+/* ========================================================================================= */
+typedef struct {
+    int n_cols;             /* column blocks */
+    const int* col_size;    /* scalar size of each column block */
+    const int* col_pos;     /* position of the block in the full solution vector x */
+    const int* col_red;     /* f-blocks: position in the reduced system; e-blocks: -1 */
+    int n_red;              /* reduced system size */
+    int n_rows;             /* row blocks (residual blocks) */
+    const int* row_size;
+    const int* row_pos;     /* position of the row block in b */
+    const int* row_cell;    /* CSR: cells of row r are row_cell[r] .. row_cell[r+1]-1 */
+    const int* cell_col;    /* column block of the cell (at most one e-block per row) */
+    const int* cell_off;    /* row-major row_size x col_size values of the cell in `values` */
+    const double* values;
+} oracle_bsm;
+
+static int bsm_is_e(const oracle_bsm* A, int cb) { return A->col_red[cb] < 0; }
+
+/* small dense kernels of the eliminator: C (m x n, leading dim ldc) += A^T B with A rs x m, B rs x n
+   (row-major); out (m) += A^T b.  The common BA shapes are dispatched with constant sizes so the
+   compiler unrolls them (a generic loop nest is ~3x slower, and this oracle is also the CPU baseline). */
+static inline __attribute__((always_inline)) void k_tn(int rs, int m, int n, const double* A, const double* B,
+                                                       double* C, size_t ldc, double sign) {
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = 0.0;
+            for (int t = 0; t < rs; ++t) acc += A[t * m + i] * B[t * n + j];
+            C[i * ldc + j] += sign * acc;
+        }
+}
+static void acc_tn(int rs, int m, int n, const double* A, const double* B, double* C, size_t ldc) {
+    if (rs == 2 && m == 6 && n == 6) k_tn(2, 6, 6, A, B, C, ldc, 1.0);
+    else if (rs == 2 && m == 6 && n == 3) k_tn(2, 6, 3, A, B, C, ldc, 1.0);
+    else if (rs == 2 && m == 3 && n == 3) k_tn(2, 3, 3, A, B, C, ldc, 1.0);
+    else if (rs == 9 && m == 3 && n == 3) k_tn(9, 3, 3, A, B, C, ldc, 1.0);
+    else k_tn(rs, m, n, A, B, C, ldc, 1.0);
+}
+static inline __attribute__((always_inline)) void k_tv(int rs, int m, const double* A, const double* b, double* out) {
+    for (int i = 0; i < m; ++i) {
+        double acc = 0.0;
+        for (int t = 0; t < rs; ++t) acc += A[t * m + i] * b[t];
+        out[i] += acc;
+    }
+}
+static void acc_tv(int rs, int m, const double* A, const double* b, double* out) {
+    if (rs == 2 && m == 6) k_tv(2, 6, A, b, out);
+    else if (rs == 2 && m == 3) k_tv(2, 3, A, b, out);
+    else if (rs == 9 && m == 3) k_tv(9, 3, A, b, out);
+    else k_tv(rs, m, A, b, out);
+}
+/* C (m x n, ldc) -= Y Z^T with Y m x es, Z n x es (Z rows with leading dim es) */
+static inline __attribute__((always_inline)) void k_ytz(int m, int n, int es, const double* Y, const double* Z,
+                                                        double* C, size_t ldc) {
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = 0.0;
+            for (int t = 0; t < es; ++t) acc += Y[i * es + t] * Z[j * es + t];
+            C[i * ldc + j] -= acc;
+        }
+}
+static void sub_ytz(int m, int n, int es, const double* Y, const double* Z, double* C, size_t ldc) {
+    if (m == 6 && n == 6 && es == 3) k_ytz(6, 6, 3, Y, Z, C, ldc);
+    else if (m == 3 && n == 3 && es == 3) k_ytz(3, 3, 3, Y, Z, C, ldc);
+    else if (m == 6 && n == 3 && es == 3) k_ytz(6, 3, 3, Y, Z, C, ldc);
+    else if (m == 3 && n == 6 && es == 3) k_ytz(3, 6, 3, Y, Z, C, ldc);
+    else k_ytz(m, n, es, Y, Z, C, ldc);
+}
+
+/* E^T E + diag(D_e)^2 of e-block e over its rows, inverted by LLT (schur_eliminator_impl.h:226-240,
+   BlockRandomAccessDiagonalMatrix::Invert); Einv is es x es. rows: the e-block's row list. */
+static int bsm_e_inverse(const oracle_bsm* A, int e, const int* rows, int nr, const double* D, double* Einv) {
+    const int es = A->col_size[e];
+    double M[9 * 9];
+    memset(M, 0, sizeof(double) * es * es);
+    for (int q = 0; q < nr; ++q) {
+        const int r = rows[q], rs = A->row_size[r];
+        for (int c = A->row_cell[r]; c < A->row_cell[r + 1]; ++c) {
+            if (A->cell_col[c] != e) continue;
+            const double* E = A->values + A->cell_off[c];
+            acc_tn(rs, es, es, E, E, M, es);
+        }
+    }
+    if (D)
+        for (int i = 0; i < es; ++i) M[i * es + i] += D[A->col_pos[e] + i] * D[A->col_pos[e] + i];
+    if (dense_llt(es, M) != 0) return 0;
+    for (int c = 0; c < es; ++c) {
+        double v[9] = {0};
+        v[c] = 1.0;
+        dense_llt_solve(es, M, v);
+        for (int r = 0; r < es; ++r) Einv[r * es + c] = v[r];
+    }
+    return 1;
+}
+
+/* row lists per e-block (rows without an e-cell go to the list n_e == "f-only") */
+static int* bsm_row_groups(const oracle_bsm* A, int** ptr_out) {
+    int* ecell = (int*)malloc(sizeof(int) * (A->n_rows > 0 ? A->n_rows : 1));
+    int* ptr = (int*)calloc(A->n_cols + 2, sizeof(int));
+    for (int r = 0; r < A->n_rows; ++r) {
+        int e = A->n_cols; /* sentinel: no e-block */
+        for (int c = A->row_cell[r]; c < A->row_cell[r + 1]; ++c)
+            if (bsm_is_e(A, A->cell_col[c])) e = A->cell_col[c];
+        ecell[r] = e;
+        ptr[e + 1]++;
+    }
+    for (int e = 0; e <= A->n_cols; ++e) ptr[e + 1] += ptr[e];
+    int* list = (int*)malloc(sizeof(int) * (A->n_rows > 0 ? A->n_rows : 1));
+    int* fill = (int*)calloc(A->n_cols + 1, sizeof(int));
+    for (int r = 0; r < A->n_rows; ++r) list[ptr[ecell[r]] + fill[ecell[r]]++] = r;
+    free(fill); free(ecell);
+    *ptr_out = ptr;
+    return list;
+}
+
+/* lhs (n_red x n_red, full symmetric, row-major) = F^T F + D_f^2 - F^T E (E^T E + D_e^2)^-1 E^T F,
+   rhs = F^T b - F^T E (E^T E + D_e^2)^-1 E^T b.  D may be NULL (no regularisation).  Returns 0 if an
+   e-block is not positive definite. */
+int oracle_schur_eliminate(const oracle_bsm* A, const double* b, const double* D, double* lhs, double* rhs) {
+    const int S = A->n_red;
+    memset(lhs, 0, sizeof(double) * (size_t)S * S);
+    memset(rhs, 0, sizeof(double) * S);
+    if (D)
+        for (int cb = 0; cb < A->n_cols; ++cb) {
+            if (bsm_is_e(A, cb)) continue;
+            for (int i = 0; i < A->col_size[cb]; ++i)
+                lhs[(size_t)(A->col_red[cb] + i) * S + A->col_red[cb] + i] += D[A->col_pos[cb] + i] * D[A->col_pos[cb] + i];
+        }
+    int* ptr;
+    int* list = bsm_row_groups(A, &ptr);
+    /* F^T F and F^T b of every row (schur_eliminator_impl.h:384-420 ChunkOuterProduct / NoEBlockRowsUpdate) */
+    for (int r = 0; r < A->n_rows; ++r) {
+        const int rs = A->row_size[r];
+        const double* br = b + A->row_pos[r];
+        for (int c1 = A->row_cell[r]; c1 < A->row_cell[r + 1]; ++c1) {
+            const int f1 = A->cell_col[c1];
+            if (bsm_is_e(A, f1)) continue;
+            const int s1 = A->col_size[f1], o1 = A->col_red[f1];
+            const double* F1 = A->values + A->cell_off[c1];
+            acc_tv(rs, s1, F1, br, rhs + o1);
+            for (int c2 = A->row_cell[r]; c2 < A->row_cell[r + 1]; ++c2) {
+                const int f2 = A->cell_col[c2];
+                if (bsm_is_e(A, f2)) continue;
+                const int s2 = A->col_size[f2], o2 = A->col_red[f2];
+                const double* F2 = A->values + A->cell_off[c2];
+                acc_tn(rs, s1, s2, F1, F2, lhs + (size_t)o1 * S + o2, S);
+            }
+        }
+    }
+    /* per e-block chunk: Y_f = (F^T E)_f Einv, lhs -= Y_f1 (F^T E)_f2^T, rhs -= Y_f E^T b */
+    int ok = 1;
+    double* FtE = (double*)malloc(sizeof(double) * (size_t)(S > 0 ? S : 1) * 9);
+    uint8_t* touched = (uint8_t*)calloc(A->n_cols > 0 ? A->n_cols : 1, 1);
+    int* tlist = (int*)malloc(sizeof(int) * (A->n_cols > 0 ? A->n_cols : 1));
+    for (int e = 0; e < A->n_cols && ok; ++e) {
+        if (!bsm_is_e(A, e)) continue;
+        const int* rows = list + ptr[e];
+        const int nr = ptr[e + 1] - ptr[e];
+        const int es = A->col_size[e];
+        double Einv[81], Etb[9] = {0};
+        if (!bsm_e_inverse(A, e, rows, nr, D, Einv)) { ok = 0; break; }
+        /* the f-blocks sharing a row with e (first-seen order), their F^T E rows zeroed */
+        int nt = 0;
+        for (int q = 0; q < nr; ++q)
+            for (int c = A->row_cell[rows[q]]; c < A->row_cell[rows[q] + 1]; ++c) {
+                const int f = A->cell_col[c];
+                if (bsm_is_e(A, f) || touched[f]) continue;
+                touched[f] = 1;
+                tlist[nt++] = f;
+                memset(FtE + (size_t)A->col_red[f] * es, 0, sizeof(double) * A->col_size[f] * es);
+            }
+        for (int q = 0; q < nr; ++q) {
+            const int r = rows[q], rs = A->row_size[r];
+            const double* E = NULL;
+            for (int c = A->row_cell[r]; c < A->row_cell[r + 1]; ++c)
+                if (A->cell_col[c] == e) E = A->values + A->cell_off[c];
+            const double* br = b + A->row_pos[r];
+            acc_tv(rs, es, E, br, Etb);
+            for (int c = A->row_cell[r]; c < A->row_cell[r + 1]; ++c) {
+                const int f = A->cell_col[c];
+                if (bsm_is_e(A, f)) continue;
+                const int fs = A->col_size[f], of = A->col_red[f];
+                acc_tn(rs, fs, es, A->values + A->cell_off[c], E, FtE + (size_t)of * es, es);
+            }
+        }
+        for (int a = 0; a < nt; ++a) {
+            const int f1 = tlist[a];
+            const int s1 = A->col_size[f1], o1 = A->col_red[f1];
+            double Y[9 * 9];  /* Y = (F^T E)_f1 Einv, s1 x es */
+            for (int i = 0; i < s1; ++i) {
+                for (int j = 0; j < es; ++j) {
+                    double acc = 0.0;
+                    for (int t = 0; t < es; ++t) acc += FtE[(size_t)(o1 + i) * es + t] * Einv[t * es + j];
+                    Y[i * es + j] = acc;
+                }
+                double acc = 0.0;
+                for (int j = 0; j < es; ++j) acc += Y[i * es + j] * Etb[j];
+                rhs[o1 + i] -= acc;
+            }
+            for (int bq = 0; bq < nt; ++bq) {
+                const int f2 = tlist[bq];
+                sub_ytz(s1, A->col_size[f2], es, Y, FtE + (size_t)A->col_red[f2] * es, lhs + (size_t)o1 * S + A->col_red[f2], S);
+            }
+        }
+        for (int a = 0; a < nt; ++a) touched[tlist[a]] = 0;
+    }
+    free(FtE); free(touched); free(tlist); free(list); free(ptr);
+    return ok;
+}
+
+/* x (full vector): f-blocks copied from z (reduced solution), e-blocks
+   x_e = (E^T E + D_e^2)^-1 E^T (b - sum_f F z_f) (schur_eliminator_impl.h:311-377) */
+int oracle_schur_back_substitute(const oracle_bsm* A, const double* b, const double* D, const double* z, double* x) {
+    for (int cb = 0; cb < A->n_cols; ++cb)
+        if (!bsm_is_e(A, cb))
+            for (int i = 0; i < A->col_size[cb]; ++i) x[A->col_pos[cb] + i] = z[A->col_red[cb] + i];
+    int* ptr;
+    int* list = bsm_row_groups(A, &ptr);
+    int ok = 1;
+    for (int e = 0; e < A->n_cols && ok; ++e) {
+        if (!bsm_is_e(A, e)) continue;
+        const int* rows = list + ptr[e];
+        const int nr = ptr[e + 1] - ptr[e];
+        const int es = A->col_size[e];
+        double Einv[81], rhs[9] = {0};
+        if (!bsm_e_inverse(A, e, rows, nr, D, Einv)) { ok = 0; break; }
+        for (int q = 0; q < nr; ++q) {
+            const int r = rows[q], rs = A->row_size[r];
+            double sres[9];
+            const double* E = NULL;
+            for (int t = 0; t < rs; ++t) sres[t] = b[A->row_pos[r] + t];
+            for (int c = A->row_cell[r]; c < A->row_cell[r + 1]; ++c) {
+                const int f = A->cell_col[c];
+                if (f == e) { E = A->values + A->cell_off[c]; continue; }
+                const int fs = A->col_size[f];
+                const double* F = A->values + A->cell_off[c];
+                for (int t = 0; t < rs; ++t) {
+                    double acc = 0.0;
+                    for (int i = 0; i < fs; ++i) acc += F[t * fs + i] * z[A->col_red[f] + i];
+                    sres[t] -= acc;
+                }
+            }
+            for (int i = 0; i < es; ++i)
+                for (int t = 0; t < rs; ++t) rhs[i] += E[t * es + i] * sres[t];
+        }
+        for (int i = 0; i < es; ++i) {
+            double acc = 0.0;
+            for (int j = 0; j < es; ++j) acc += Einv[i * es + j] * rhs[j];
+            x[A->col_pos[e] + i] = acc;
+        }
+    }
+    free(list); free(ptr);
+    return ok;
+}
+
+/* SchurComplementSolver::SolveImpl (schur_complement_solver.cc:118-176): eliminate, dense LLT of the
+   reduced system (an empty one when every column block is eliminated), back-substitute.  x: full
+   solution of min |A x - b|^2 + |D x|^2 (D may be NULL).  Returns 0 on a non-positive-definite block. */
+int oracle_schur_solve(const oracle_bsm* A, const double* b, const double* D, double* x) {
+    const int S = A->n_red;
+    double* lhs = (double*)malloc(sizeof(double) * (size_t)(S > 0 ? S : 1) * (S > 0 ? S : 1));
+    double* rhs = (double*)malloc(sizeof(double) * (S > 0 ? S : 1));
+    int ok = oracle_schur_eliminate(A, b, D, lhs, rhs);
+    if (ok && S > 0) {
+        if (dense_llt(S, lhs) != 0) ok = 0;
+        else dense_llt_solve(S, lhs, rhs);
+    }
+    if (ok) ok = oracle_schur_back_substitute(A, b, D, rhs, x);
+    free(lhs); free(rhs);
+    return ok;
+}
+
+/* ========================================================================================= */
 /* Generic Ceres-2.0 LM minimiser (TrustRegionMinimizer + LevenbergMarquardtStrategy)         */
 /* ========================================================================================= */
 typedef struct {
@@ -893,6 +1170,13 @@ typedef struct {
     int* lm_ptr;
     int* lm_obs;
     int eval_failed;
+    /* the scaled Jacobian as a block-sparse matrix for the Schur eliminator (built once) */
+    oracle_bsm A;
+    int *col_size, *col_pos, *col_red, *row_size, *row_pos, *row_cell, *cell_col, *cell_off;
+    int* cell_src;       /* per cell: observation o (pose cell: 2*o, point cell: 2*o+1) or IMU block -(1 + 4k + b) */
+    double* values;
+    double* bvec;        /* residuals in row order */
+    int* row_src;        /* per row: observation o, or -(1 + k) for the IMU factor k-1 -> k */
 } ba_ctx;
 
 static void ba_unpack(ba_ctx* c, const double* x) {
@@ -1004,151 +1288,39 @@ static int ba_eval(void* user, const double* x, double* cost, int want_jac, doub
     return 1;
 }
 
-/* Schur complement solve: points are the e-blocks, everything else the reduced system */
+/* Schur complement solve: points are the e-blocks, everything else the reduced system.  The scaled
+   Jacobian J~ = J diag(s) goes through the generic eliminator (oracle_schur_eliminate, pinned by the
+   Ceres SchurEliminatorTest fixtures), the reduced system through a dense LLT (SPARSE_SCHUR's LDLT is
+   the same factorisation up to roundoff), the points through oracle_schur_back_substitute. */
 static int ba_solve(void* user, const double* s, const double* D, double* y) {
     ba_ctx* c = (ba_ctx*)user;
-    const vio_ba_problem* p = c->p;
-    int nf = c->nf;
-    double* S = (double*)calloc((size_t)(nf > 0 ? nf : 1) * (nf > 0 ? nf : 1), sizeof(double));
-    double* bf = (double*)calloc(nf > 0 ? nf : 1, sizeof(double));
-    /* f-block normal equations: scaled J^T J and J^T r */
-    for (int o = 0; o < c->N; ++o) {
-        if (!c->obs_active[o]) continue;
-        int po = c->pose_off[p->obs_kf[o]];
-        if (po < 0) continue;
-        int fi = c->f_index[po];
-        const double* J = c->Jp + 12 * o;
-        const double* r = c->r + 2 * o;
-        for (int a = 0; a < 6; ++a) {
-            bf[fi + a] += s[po + a] * (J[a] * r[0] + J[6 + a] * r[1]);
-            for (int b = 0; b < 6; ++b)
-                S[(fi + a) * nf + fi + b] += s[po + a] * s[po + b] * (J[a] * J[b] + J[6 + a] * J[6 + b]);
+    const oracle_bsm* A = &c->A;
+    /* values of J~ and the residual vector, row by row */
+    for (int r = 0; r < A->n_rows; ++r) {
+        const int src = c->row_src[r];
+        if (src >= 0) {
+            c->bvec[A->row_pos[r]] = c->r[2 * src];
+            c->bvec[A->row_pos[r] + 1] = c->r[2 * src + 1];
+        } else {
+            memcpy(c->bvec + A->row_pos[r], c->ri + 9 * (-src - 1), 9 * sizeof(double));
         }
-    }
-    if (c->is_vi) {
-        for (int k = 1; k < c->K; ++k) {
-            if (!c->imu_active[k]) continue;
-            const double* J = c->Ji + 108 * k;
-            const double* r = c->ri + 9 * k;
-            int offs[4] = {c->vel_off[k - 1], c->bg_off, c->ba_off, c->vel_off[k]};
-            for (int a = 0; a < 4; ++a) {
-                if (offs[a] < 0) continue;
-                int fa = c->f_index[offs[a]];
-                for (int i = 0; i < 3; ++i) {
-                    double gsum = 0;
-                    for (int q = 0; q < 9; ++q) gsum += J[27 * a + 3 * q + i] * r[q];
-                    bf[fa + i] += s[offs[a] + i] * gsum;
-                }
-                for (int b = 0; b < 4; ++b) {
-                    if (offs[b] < 0) continue;
-                    int fb = c->f_index[offs[b]];
-                    for (int i = 0; i < 3; ++i)
-                        for (int j = 0; j < 3; ++j) {
-                            double h = 0;
-                            for (int q = 0; q < 9; ++q) h += J[27 * a + 3 * q + i] * J[27 * b + 3 * q + j];
-                            S[(fa + i) * nf + fb + j] += s[offs[a] + i] * s[offs[b] + j] * h;
-                        }
-                }
+        for (int q = A->row_cell[r]; q < A->row_cell[r + 1]; ++q) {
+            const int cs = c->cell_src[q], cb = A->cell_col[q], w = A->col_size[cb], pos = A->col_pos[cb];
+            double* v = c->values + A->cell_off[q];
+            if (cs >= 0) {
+                const int o = cs >> 1;
+                const double* J = (cs & 1) ? c->Jl + 6 * o : c->Jp + 12 * o;
+                for (int t = 0; t < 2; ++t)
+                    for (int j = 0; j < w; ++j) v[t * w + j] = J[t * w + j] * s[pos + j];
+            } else {
+                const int k = (-cs - 1) >> 2, b = (-cs - 1) & 3;
+                const double* J = c->Ji + 108 * k + 27 * b;
+                for (int t = 0; t < 9; ++t)
+                    for (int j = 0; j < 3; ++j) v[3 * t + j] = J[3 * t + j] * s[pos + j];
             }
         }
     }
-    for (int i = 0; i < c->n; ++i)
-        if (c->f_index[i] >= 0) S[c->f_index[i] * nf + c->f_index[i]] += D[i] * D[i];
-    /* eliminate points (SchurEliminator::Eliminate) */
-    double* Vinv = (double*)malloc(sizeof(double) * 9 * (c->L > 0 ? c->L : 1));
-    double* gl = (double*)malloc(sizeof(double) * 3 * (c->L > 0 ? c->L : 1));
-    for (int l = 0; l < c->L; ++l) {
-        int lo = c->lm_off[l];
-        if (lo < 0) continue;
-        double V[9] = {0}, g[3] = {0};
-        for (int q = c->lm_ptr[l]; q < c->lm_ptr[l + 1]; ++q) {
-            int o = c->lm_obs[q];
-            if (!c->obs_active[o]) continue;
-            const double* J = c->Jl + 6 * o;
-            const double* r = c->r + 2 * o;
-            for (int a = 0; a < 3; ++a) {
-                g[a] += s[lo + a] * (J[a] * r[0] + J[3 + a] * r[1]);
-                for (int b = 0; b < 3; ++b) V[3 * a + b] += s[lo + a] * s[lo + b] * (J[a] * J[b] + J[3 + a] * J[3 + b]);
-            }
-        }
-        for (int a = 0; a < 3; ++a) V[4 * a] += D[lo + a] * D[lo + a];
-        /* inverse via LLT */
-        double Lc[9];
-        memcpy(Lc, V, sizeof Lc);
-        if (dense_llt(3, Lc) != 0) { free(S); free(bf); free(Vinv); free(gl); return 0; }
-        double* Vi = Vinv + 9 * l;
-        for (int cc = 0; cc < 3; ++cc) {
-            double e[3] = {0, 0, 0};
-            e[cc] = 1.0;
-            dense_llt_solve(3, Lc, e);
-            for (int rr = 0; rr < 3; ++rr) Vi[3 * rr + cc] = e[rr];
-        }
-        memcpy(gl + 3 * l, g, sizeof g);
-        /* Y_a = W~_a V^-1 (6x3) for each obs; S -= Y_a W~_b^T ; b -= Y_a g */
-        for (int qa = c->lm_ptr[l]; qa < c->lm_ptr[l + 1]; ++qa) {
-            int oa = c->lm_obs[qa];
-            if (!c->obs_active[oa]) continue;
-            int pa = c->pose_off[p->obs_kf[oa]];
-            if (pa < 0) continue;
-            int fa = c->f_index[pa];
-            double W[18], Y[18];
-            const double* Jp = c->Jp + 12 * oa;
-            const double* Jl = c->Jl + 6 * oa;
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 3; ++j)
-                    W[3 * i + j] = s[pa + i] * s[lo + j] * (Jp[i] * Jl[j] + Jp[6 + i] * Jl[3 + j]);
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j < 3; ++j)
-                    Y[3 * i + j] = W[3 * i] * Vi[j] + W[3 * i + 1] * Vi[3 + j] + W[3 * i + 2] * Vi[6 + j];
-            for (int i = 0; i < 6; ++i) bf[fa + i] -= Y[3 * i] * g[0] + Y[3 * i + 1] * g[1] + Y[3 * i + 2] * g[2];
-            for (int qb = c->lm_ptr[l]; qb < c->lm_ptr[l + 1]; ++qb) {
-                int ob = c->lm_obs[qb];
-                if (!c->obs_active[ob]) continue;
-                int pb = c->pose_off[p->obs_kf[ob]];
-                if (pb < 0) continue;
-                int fb = c->f_index[pb];
-                const double* Jpb = c->Jp + 12 * ob;
-                const double* Jlb = c->Jl + 6 * ob;
-                double Wb[18];
-                for (int i = 0; i < 6; ++i)
-                    for (int j = 0; j < 3; ++j)
-                        Wb[3 * i + j] = s[pb + i] * s[lo + j] * (Jpb[i] * Jlb[j] + Jpb[6 + i] * Jlb[3 + j]);
-                for (int i = 0; i < 6; ++i)
-                    for (int j = 0; j < 6; ++j)
-                        S[(fa + i) * nf + fb + j] -= Y[3 * i] * Wb[3 * j] + Y[3 * i + 1] * Wb[3 * j + 1] + Y[3 * i + 2] * Wb[3 * j + 2];
-            }
-        }
-    }
-    /* reduced solve (dense LLT; SPARSE_SCHUR's LDLT is the same factorisation up to roundoff) */
-    if (nf > 0) {
-        if (dense_llt(nf, S) != 0) { free(S); free(bf); free(Vinv); free(gl); return 0; }
-        dense_llt_solve(nf, S, bf);
-    }
-    for (int i = 0; i < c->n; ++i)
-        if (c->f_index[i] >= 0) y[i] = bf[c->f_index[i]];
-    /* back-substitution (SchurEliminator::BackSubstitute) */
-    for (int l = 0; l < c->L; ++l) {
-        int lo = c->lm_off[l];
-        if (lo < 0) continue;
-        double rhs[3] = {gl[3 * l], gl[3 * l + 1], gl[3 * l + 2]};
-        for (int q = c->lm_ptr[l]; q < c->lm_ptr[l + 1]; ++q) {
-            int o = c->lm_obs[q];
-            if (!c->obs_active[o]) continue;
-            int po = c->pose_off[p->obs_kf[o]];
-            if (po < 0) continue;
-            const double* Jp = c->Jp + 12 * o;
-            const double* Jl = c->Jl + 6 * o;
-            for (int j = 0; j < 3; ++j) {
-                double w = 0;
-                for (int i = 0; i < 6; ++i) w += s[po + i] * s[lo + j] * (Jp[i] * Jl[j] + Jp[6 + i] * Jl[3 + j]) * y[po + i];
-                rhs[j] -= w;
-            }
-        }
-        const double* Vi = Vinv + 9 * l;
-        for (int j = 0; j < 3; ++j) y[lo + j] = Vi[3 * j] * rhs[0] + Vi[3 * j + 1] * rhs[1] + Vi[3 * j + 2] * rhs[2];
-    }
-    free(S); free(bf); free(Vinv); free(gl);
-    return 1;
+    return oracle_schur_solve(A, c->bvec, D, y);
 }
 
 static double ba_model_change(void* user, const double* s, const double* h) {
@@ -1197,6 +1369,65 @@ static void pose_ctx_init(pose_ctx* pc, const vio_pose* Twb, const vio_pose* Tcb
     oracle_nearest_rotation(Tcb->R, pc->R_cb);
     memcpy(pc->t_cb, Tcb->t, sizeof pc->t_cb);
     memcpy(pc->R_cb_raw, Tcb->R, sizeof pc->R_cb_raw);
+}
+
+/* column blocks: poses, velocities, biases (f-blocks at their x offsets, the reduced system's
+   order), points (e-blocks); row blocks: active observations (2 rows: point and pose cells), then
+   the IMU factors (9 rows: v_i, bg, ba, v_j cells) */
+static void ba_build_bsm(ba_ctx* c) {
+    const vio_ba_problem* p = c->p;
+    const int K = c->K, L = c->L, N = c->N;
+    int nc = 0;
+    const int cap_c = 2 * K + 2 + L + 1;
+    c->col_size = (int*)malloc(sizeof(int) * cap_c);
+    c->col_pos = (int*)malloc(sizeof(int) * cap_c);
+    c->col_red = (int*)malloc(sizeof(int) * cap_c);
+    int* pose_cb = (int*)malloc(sizeof(int) * K);
+    int* vel_cb = (int*)malloc(sizeof(int) * K);
+    int* lm_cb = (int*)malloc(sizeof(int) * (L > 0 ? L : 1));
+#define ADD_COL(sz, pos, red) (c->col_size[nc] = (sz), c->col_pos[nc] = (pos), c->col_red[nc] = (red), nc++)
+    for (int k = 0; k < K; ++k) pose_cb[k] = c->pose_off[k] >= 0 ? ADD_COL(6, c->pose_off[k], c->pose_off[k]) : -1;
+    for (int k = 0; k < K; ++k) vel_cb[k] = c->vel_off[k] >= 0 ? ADD_COL(3, c->vel_off[k], c->vel_off[k]) : -1;
+    const int bg_cb = c->bg_off >= 0 ? ADD_COL(3, c->bg_off, c->bg_off) : -1;
+    const int ba_cb = c->ba_off >= 0 ? ADD_COL(3, c->ba_off, c->ba_off) : -1;
+    for (int l = 0; l < L; ++l) lm_cb[l] = c->lm_off[l] >= 0 ? ADD_COL(3, c->lm_off[l], -1) : -1;
+#undef ADD_COL
+    int nr = 0, ncell = 0, nval = 0, bpos = 0;
+    const int cap_r = N + K + 1;
+    c->row_size = (int*)malloc(sizeof(int) * cap_r);
+    c->row_pos = (int*)malloc(sizeof(int) * cap_r);
+    c->row_cell = (int*)malloc(sizeof(int) * (cap_r + 1));
+    c->row_src = (int*)malloc(sizeof(int) * cap_r);
+    c->cell_col = (int*)malloc(sizeof(int) * (2 * N + 4 * K + 1));
+    c->cell_off = (int*)malloc(sizeof(int) * (2 * N + 4 * K + 1));
+    c->cell_src = (int*)malloc(sizeof(int) * (2 * N + 4 * K + 1));
+    c->row_cell[0] = 0;
+    for (int o = 0; o < N; ++o) {
+        if (!c->obs_active[o]) continue;
+        const int pc_ = pose_cb[p->obs_kf[o]], lc = lm_cb[p->obs_lm[o]];
+        c->row_size[nr] = 2; c->row_pos[nr] = bpos; c->row_src[nr] = o; bpos += 2;
+        if (lc >= 0) { c->cell_col[ncell] = lc; c->cell_off[ncell] = nval; c->cell_src[ncell] = 2 * o + 1; ncell++; nval += 6; }
+        if (pc_ >= 0) { c->cell_col[ncell] = pc_; c->cell_off[ncell] = nval; c->cell_src[ncell] = 2 * o; ncell++; nval += 12; }
+        c->row_cell[++nr] = ncell;
+    }
+    if (c->is_vi)
+        for (int k = 1; k < K; ++k) {
+            if (!c->imu_active[k]) continue;
+            c->row_size[nr] = 9; c->row_pos[nr] = bpos; c->row_src[nr] = -(1 + k); bpos += 9;
+            const int cbs[4] = {vel_cb[k - 1], bg_cb, ba_cb, vel_cb[k]};
+            for (int b = 0; b < 4; ++b) {
+                if (cbs[b] < 0) continue;
+                c->cell_col[ncell] = cbs[b]; c->cell_off[ncell] = nval; c->cell_src[ncell] = -(1 + 4 * k + b);
+                ncell++; nval += 27;
+            }
+            c->row_cell[++nr] = ncell;
+        }
+    c->values = (double*)malloc(sizeof(double) * (nval > 0 ? nval : 1));
+    c->bvec = (double*)malloc(sizeof(double) * (bpos > 0 ? bpos : 1));
+    oracle_bsm A = {nc, c->col_size, c->col_pos, c->col_red, c->nf, nr, c->row_size, c->row_pos, c->row_cell,
+                    c->cell_col, c->cell_off, c->values};
+    c->A = A;
+    free(pose_cb); free(vel_cb); free(lm_cb);
 }
 
 static int ba_ctx_build(ba_ctx* c, const vio_ba_problem* p) {
@@ -1288,6 +1519,7 @@ static int ba_ctx_build(ba_ctx* c, const vio_ba_problem* p) {
     }
     free(fill);
     free(pose_used); free(lm_used); free(vel_used);
+    ba_build_bsm(c);
     return 0;
 }
 
@@ -1295,6 +1527,8 @@ static void ba_ctx_free(ba_ctx* c) {
     free(c->pc); free(c->pose_val); free(c->lm_val); free(c->vel_val); free(c->obs_active); free(c->obs_outlier);
     free(c->r); free(c->Jp); free(c->Jl); free(c->imu); free(c->imu_active); free(c->ri); free(c->Ji);
     free(c->pose_off); free(c->vel_off); free(c->lm_off); free(c->f_index); free(c->lm_ptr); free(c->lm_obs);
+    free(c->col_size); free(c->col_pos); free(c->col_red); free(c->row_size); free(c->row_pos); free(c->row_cell);
+    free(c->row_src); free(c->cell_col); free(c->cell_off); free(c->cell_src); free(c->values); free(c->bvec);
 }
 
 /* cost of the residual blocks whose parameters are all constant (program.cc:305-390) */
@@ -1607,6 +1841,121 @@ int oracle_powell(const int* mask, double* x, int* iterations, double* final_cos
     *iterations = s.iterations;
     *final_cost = s.final_cost;
     *termination = s.termination;
+    return 0;
+}
+
+/* DENSE_QR (dense_qr_solver.cc): Householder QR of the augmented [J~; diag(D)] (m + n rows),
+   y = argmin |J~ y - r|^2 + |D y|^2.  Returns 0 on a zero column. */
+static int dense_qr_lm_solve(int m, int n, const double* Js /* m x n */, const double* r, const double* D, double* y) {
+    const int rows = m + n;
+    double* A = (double*)calloc((size_t)rows * n, sizeof(double));
+    double* b = (double*)calloc(rows, sizeof(double));
+    double* v = (double*)malloc(sizeof(double) * rows);
+    memcpy(A, Js, sizeof(double) * m * n);
+    memcpy(b, r, sizeof(double) * m);
+    for (int j = 0; j < n; ++j) A[(m + j) * n + j] = D ? D[j] : 0.0;
+    int ok = 1;
+    for (int j = 0; j < n && ok; ++j) {
+        double nrm = 0;
+        for (int i = j; i < rows; ++i) nrm += A[i * n + j] * A[i * n + j];
+        nrm = sqrt(nrm);
+        if (nrm == 0.0) { ok = 0; break; }
+        const double alpha = A[j * n + j] > 0 ? -nrm : nrm;
+        for (int i = 0; i < rows; ++i) v[i] = i >= j ? A[i * n + j] : 0.0;
+        v[j] -= alpha;
+        double vn = 0;
+        for (int i = j; i < rows; ++i) vn += v[i] * v[i];
+        if (vn == 0.0) continue;
+        for (int c = j; c < n; ++c) {
+            double d = 0;
+            for (int i = j; i < rows; ++i) d += v[i] * A[i * n + c];
+            d = 2.0 * d / vn;
+            for (int i = j; i < rows; ++i) A[i * n + c] -= d * v[i];
+        }
+        double d = 0;
+        for (int i = j; i < rows; ++i) d += v[i] * b[i];
+        d = 2.0 * d / vn;
+        for (int i = j; i < rows; ++i) b[i] -= d * v[i];
+    }
+    if (ok)
+        for (int j = n - 1; j >= 0; --j) {
+            double t = b[j];
+            for (int c = j + 1; c < n; ++c) t -= A[j * n + c] * y[c];
+            y[j] = t / A[j * n + j];
+        }
+    free(A); free(b); free(v);
+    return ok;
+}
+
+/* JacobiScalingTest (trust_region_minimizer_test.cc:325-410): CurveCostFunction, one residual
+   target - sum_i |y_i - y_{i-1}| over a closed polygon of nv 2-D vertices (y_{-1} = y_{nv-1}),
+   solved by LM + DENSE_QR with the default Solver::Options (Jacobi scaling on). */
+typedef struct { int nv; double target; double J[64]; double r; } curve_ctx;
+static void curve_eval_rj(const curve_ctx* c, const double* y, double* r, double* J) {
+    const int nv = c->nv;
+    double res = c->target;
+    for (int i = 0; i < nv; ++i) {
+        const int prev = (nv + i - 1) % nv;
+        double len = 0.0;
+        for (int d = 0; d < 2; ++d) { const double diff = y[2 * prev + d] - y[2 * i + d]; len += diff * diff; }
+        res -= sqrt(len);
+    }
+    *r = res;
+    if (!J) return;
+    for (int i = 0; i < nv; ++i) {
+        const int prev = (nv + i - 1) % nv, next = (i + 1) % nv;
+        double u[2], v[2], nu = 0, nvv = 0;
+        for (int d = 0; d < 2; ++d) {
+            u[d] = y[2 * i + d] - y[2 * prev + d]; nu += u[d] * u[d];
+            v[d] = y[2 * next + d] - y[2 * i + d]; nvv += v[d] * v[d];
+        }
+        nu = sqrt(nu); nvv = sqrt(nvv);
+        for (int d = 0; d < 2; ++d) {
+            double j = 0.0;
+            if (nu > DBL_MIN) j -= u[d] / nu;
+            if (nvv > DBL_MIN) j += v[d] / nvv;
+            J[2 * i + d] = j;
+        }
+    }
+}
+static int curve_eval(void* u, const double* x, double* cost, int want, double* g, double* colsq) {
+    curve_ctx* c = (curve_ctx*)u;
+    double r, J[64];
+    curve_eval_rj(c, x, &r, want ? J : NULL);
+    *cost = 0.5 * r * r;
+    if (want) {
+        c->r = r;
+        memcpy(c->J, J, sizeof(double) * 2 * c->nv);
+        for (int j = 0; j < 2 * c->nv; ++j) { g[j] = J[j] * r; colsq[j] = J[j] * J[j]; }
+    }
+    return 1;
+}
+static int curve_solve(void* u, const double* s, const double* D, double* y) {
+    curve_ctx* c = (curve_ctx*)u;
+    double Js[64];
+    for (int j = 0; j < 2 * c->nv; ++j) Js[j] = c->J[j] * s[j];
+    return dense_qr_lm_solve(1, 2 * c->nv, Js, &c->r, D, y);
+}
+static double curve_model(void* u, const double* s, const double* h) {
+    curve_ctx* c = (curve_ctx*)u;
+    double m = 0;
+    for (int j = 0; j < 2 * c->nv; ++j) m += c->J[j] * s[j] * h[j];
+    return -(m * (c->r + m / 2.0));
+}
+/* y: 2 nv values in/out */
+int oracle_curve_kat(int nv, double target, double* y, double* final_cost, int* iterations, int* termination) {
+    if (nv < 3 || nv > 32) return VIO_EINVAL;
+    curve_ctx c;
+    c.nv = nv;
+    c.target = target;
+    lm_problem P = {2 * nv, &c, curve_eval, curve_solve, curve_model};
+    lm_options o;
+    oracle_lm_default_options(&o);
+    lm_summary sum;
+    oracle_lm_minimize(&P, &o, y, &sum);
+    *final_cost = sum.final_cost;
+    *iterations = sum.iterations;
+    *termination = sum.termination;
     return 0;
 }
 

@@ -228,3 +228,123 @@ def test_config4_fixture_reproduces(vio, synth):
         o = oracle_lib.ba_solve(vio, vio.BaProblem(synth.config3(synth.SEED + i), variant=vio.VIO_BA_VI))
         assert o["iterations"] == ref[i]["iterations"] and o["final_cost"] == ref[i]["final_cost"]
         assert o["initial_cost"] == ref[i]["initial_cost"]
+
+
+# ---- Schur complement: the reference's own Ceres fixtures -----------------------------------------
+class OracleBsm(C.Structure):
+    """oracle_bsm (oracle/ba_oracle.c): block-sparse matrix of the generic Schur eliminator."""
+    _fields_ = [("n_cols", C.c_int), ("col_size", C.c_void_p), ("col_pos", C.c_void_p), ("col_red", C.c_void_p),
+                ("n_red", C.c_int), ("n_rows", C.c_int), ("row_size", C.c_void_p), ("row_pos", C.c_void_p),
+                ("row_cell", C.c_void_p), ("cell_col", C.c_void_p), ("cell_off", C.c_void_p), ("values", C.c_void_p)]
+
+
+def bsm_from_fixture(pr):
+    """The Ceres block structure (e-blocks first, CompressedRowBlockStructure) as an oracle_bsm plus
+    its dense matrix."""
+    cs = pr["col_sizes"]
+    ne = pr["num_eliminate_blocks"]
+    col_pos = np.cumsum([0] + cs[:-1]).astype(np.int32)
+    ne_cols = int(sum(cs[:ne]))
+    col_red = np.array([-1 if b < ne else int(col_pos[b]) - ne_cols for b in range(len(cs))], np.int32)
+    row_size, row_pos, row_cell, cell_col, cell_off, vals = [], [], [0], [], [], []
+    r0 = 0
+    for rs, cells in pr["rows"]:
+        row_size.append(rs)
+        row_pos.append(r0)
+        for cb, v in cells:
+            assert len(v) == rs * cs[cb]
+            cell_col.append(cb)
+            cell_off.append(len(vals))
+            vals.extend(v)
+        row_cell.append(len(cell_col))
+        r0 += rs
+    dense = np.zeros((r0, int(sum(cs))))
+    for r, (rs, cells) in enumerate(pr["rows"]):
+        for cb, v in cells:
+            dense[row_pos[r]:row_pos[r] + rs, col_pos[cb]:col_pos[cb] + cs[cb]] = np.array(v, float).reshape(rs, cs[cb])
+    arrs = dict(col_size=np.array(cs, np.int32), col_pos=col_pos, col_red=col_red, row_size=np.array(row_size, np.int32),
+                row_pos=np.array(row_pos, np.int32), row_cell=np.array(row_cell, np.int32),
+                cell_col=np.array(cell_col, np.int32), cell_off=np.array(cell_off, np.int32),
+                values=np.array(vals, np.float64))
+    m = OracleBsm(len(cs), *[arrs[k].ctypes.data for k in ("col_size", "col_pos", "col_red")], int(sum(cs)) - ne_cols,
+                  len(row_size), *[arrs[k].ctypes.data for k in ("row_size", "row_pos", "row_cell", "cell_col",
+                                                                 "cell_off", "values")])
+    return m, arrs, dense, ne_cols
+
+
+def ceres_fixture(name):
+    import json
+    return json.load(open(os.path.join(GOLDEN, "ceres_lls_problems.json")))[name]
+
+
+@pytest.mark.parametrize("name,reg", [("problem2", False), ("problem2", True), ("problem4", True)])
+def test_schur_eliminator_ceres_kat(name, reg):
+    """SchurEliminatorTest (schur_eliminator_test.cc:196-225: ScalarProblemNoRegularization,
+    ScalarProblemWithRegularization, VaryingFBlockSize): the reduced system lhs / rhs and the
+    back-substituted solution against the dense computation of ComputeReferenceSolution (:81-115),
+    relative tolerance 1e-14, on LinearLeastSquaresProblem2 / 4 (tests/golden/ceres_lls_problems.json)."""
+    L = oracle_lib.load()
+    pr = ceres_fixture(name)
+    A, keep, J, ne = bsm_from_fixture(pr)
+    b = np.array(pr["b"], np.float64)
+    D = np.array(pr["D"], np.float64) if reg else np.zeros(J.shape[1])
+    # ComputeReferenceSolution: H = D^2 + J^T J, P = blockwise inverse of the e-e part
+    H = np.diag(D * D) + J.T @ J
+    g = J.T @ b
+    P = H[:ne, :ne].copy()
+    pos = 0
+    for cb in range(pr["num_eliminate_blocks"]):
+        sz = pr["col_sizes"][cb]
+        P[pos:pos + sz, pos:pos + sz] = np.linalg.inv(P[pos:pos + sz, pos:pos + sz])
+        pos += sz
+    Q, R = H[:ne, ne:], H[ne:, ne:]
+    lhs_e = R - Q.T @ P @ Q
+    rhs_e = g[ne:] - Q.T @ P @ g[:ne]
+    sol_e = np.linalg.solve(H, g)
+    S = J.shape[1] - ne
+    lhs, rhs, x = np.zeros((S, S)), np.zeros(S), np.zeros(J.shape[1])
+    L.oracle_schur_eliminate.argtypes = [C.POINTER(OracleBsm), dp, dp, dp, dp]
+    L.oracle_schur_solve.argtypes = [C.POINTER(OracleBsm), dp, dp, dp]
+    assert L.oracle_schur_eliminate(C.byref(A), _d(b)[1], _d(D)[1], lhs.ctypes.data_as(dp), rhs.ctypes.data_as(dp)) == 1
+    assert L.oracle_schur_solve(C.byref(A), _d(b)[1], _d(D)[1], x.ctypes.data_as(dp)) == 1
+    assert np.linalg.norm(np.triu(lhs - lhs_e)) / np.linalg.norm(lhs_e) <= 1e-14
+    assert np.linalg.norm(rhs - rhs_e) / np.linalg.norm(rhs_e) <= 1e-14
+    assert np.linalg.norm(x - sol_e) / np.linalg.norm(sol_e) <= 1e-14
+
+
+@pytest.mark.parametrize("name,reg", [("problem2", False), ("problem2", True), ("problem3", False),
+                                      ("problem3", True), ("problem4", True)])
+def test_schur_complement_solver_ceres_kat(name, reg):
+    """SchurComplementSolverTest (schur_complement_solver_test.cc:50-220, DENSE_SCHUR / SPARSE_SCHUR on
+    problems 2, 3 — every column eliminated — and 4): |x - x_QR| / num_cols <= 1e-10 against the dense
+    least-squares solution of [A; diag(D)] x = [b; 0]."""
+    L = oracle_lib.load()
+    pr = ceres_fixture(name)
+    A, keep, J, ne = bsm_from_fixture(pr)
+    b = np.array(pr["b"], np.float64)
+    n = J.shape[1]
+    D = np.array(pr["D"], np.float64) if reg else None
+    Aa = np.vstack([J, np.diag(D)]) if reg else J
+    ba = np.concatenate([b, np.zeros(n)]) if reg else b
+    x_qr = np.linalg.lstsq(Aa, ba, rcond=None)[0]
+    x = np.zeros(n)
+    L.oracle_schur_solve.argtypes = [C.POINTER(OracleBsm), dp, dp, dp]
+    assert L.oracle_schur_solve(C.byref(A), _d(b)[1], _d(D)[1] if reg else None, x.ctypes.data_as(dp)) == 1
+    assert np.linalg.norm(x - x_qr) / n <= 1e-10
+
+
+def test_jacobi_scaling_ceres_kat():
+    """JacobiScalingTest (trust_region_minimizer_test.cc:389-410): a closed 6-vertex polygon on the unit
+    circle stretched to perimeter 10 through one residual, LM + DENSE_QR with Jacobi scaling (the
+    default options): final_cost <= 1e-10."""
+    L = oracle_lib.load()
+    N = 6
+    th = np.arange(N) * 2.0 * 3.1415926535897932384626433 / N
+    y = np.stack([np.cos(th), np.sin(th)], 1).reshape(-1).copy()
+    fc, it, term = C.c_double(), C.c_int(), C.c_int()
+    L.oracle_curve_kat.argtypes = [C.c_int, C.c_double, dp, C.POINTER(C.c_double), C.POINTER(C.c_int),
+                                   C.POINTER(C.c_int)]
+    assert L.oracle_curve_kat(N, 10.0, y.ctypes.data_as(dp), C.byref(fc), C.byref(it), C.byref(term)) == 0
+    assert fc.value <= 1e-10
+    per = sum(np.linalg.norm(y.reshape(N, 2)[i] - y.reshape(N, 2)[i - 1]) for i in range(N))
+    assert abs(per - 10.0) <= 1e-4
