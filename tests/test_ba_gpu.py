@@ -294,12 +294,14 @@ def test_edge_cases(vio, synth, gpu_ctx):
 
 
 def test_config4_full_size_properties(vio, synth, gpu_ctx):
-    """256 VIO windows (config 4 shape) in one launch against the oracle's converged results for
-    all 256 (tests/golden/config4_oracle.json, tests/golden/gen_config4_summary.py): initial costs
-    to 1e-9, final costs within 2e-4 (the perturbed-oracle cloud reaches 3.4e-5 on window 0),
-    iteration counts per window within 10 and in total within 2 %, the improvement of the pose
-    error over the perturbed start (final / initial distance to the synthetic truth) per window
-    within 0.05 of the oracle's and on average within 0.01; sampled windows at the VI bar and
+    """256 VIO windows (config 4 shape) in one launch against the oracle's converged results for all
+    256 and their perturbation clouds (landmark inputs x (1 + e), e = +-1e-15 .. +-1e-14;
+    tests/golden/config4_oracle.json, tests/golden/gen_config4_summary.py): initial costs to 1e-9;
+    final costs within 2e-4 of the oracle's or of a cloud member's (the VI windows bifurcate under
+    roundoff: window 179 stops after 51 or after 27 iterations, at cost 2814.2 or 2861.55, depending
+    on a 1e-15 input change); iteration counts inside the cloud's range +-1; at most 2 windows (<1 %;
+    a held-out e = -5e-14 oracle run has 1) outside those bands; the pose error against the synthetic
+    truth (final / initial) on average within 0.01 of the oracle's.  Sampled windows at the VI bar,
     fixed-iteration trajectories at the tight bar."""
     import json
     import os
@@ -307,22 +309,23 @@ def test_config4_full_size_properties(vio, synth, gpu_ctx):
     ws = synth.config4(256)
     probs = [vio.BaProblem(w, variant=vio.VIO_BA_VI) for w in ws]
     res = gpu_ctx.ba_solve(probs)
-    ratio_g, ratio_o, it_g, it_o = [], [], [], []
+    ratio_g, ratio_o, off_cost, off_it = [], [], [], []
     for w, g, r in zip(ws, res, ref):
         assert g["success"] == r["success"] == 1 and g["final_cost"] < 1e-2 * g["initial_cost"]
         assert abs(g["initial_cost"] - r["initial_cost"]) <= 1e-9 * r["initial_cost"], r["window"]
-        assert abs(g["final_cost"] - r["final_cost"]) <= 2e-4 * r["final_cost"], r["window"]
-        assert abs(g["iterations"] - r["iterations"]) <= 10, (r["window"], g["iterations"], r["iterations"])
+        costs = [r["final_cost"]] + r["cloud_final_cost"]
+        its = [r["iterations"]] + r["cloud_iterations"]
+        if min(abs(g["final_cost"] - c) / c for c in costs) > 2e-4:
+            off_cost.append((r["window"], g["final_cost"], costs))
+        if not min(its) - 1 <= g["iterations"] <= max(its) + 1:
+            off_it.append((r["window"], g["iterations"], its))
         e0 = np.abs(w["T_wb_init"][:, :3, 3] - w["T_wb_true"][:, :3, 3]).mean()
         e1 = np.abs(g["T_wb"][:, :3, 3] - w["T_wb_true"][:, :3, 3]).mean()
         ratio_g.append(e1 / e0)
         ratio_o.append(r["pose_err_final"] / r["pose_err_init"])
-        it_g.append(g["iterations"])
-        it_o.append(r["iterations"])
+    assert len(off_cost) <= 2 and len(off_it) <= 2, (off_cost, off_it)
     ratio_g, ratio_o = np.array(ratio_g), np.array(ratio_o)
-    assert np.abs(ratio_g - ratio_o).max() <= 0.05
     assert abs(ratio_g.mean() - ratio_o.mean()) <= 0.01 and ratio_g.mean() < 0.2
-    assert abs(sum(it_g) - sum(it_o)) <= 0.02 * sum(it_o), (sum(it_g), sum(it_o))
     # converged answers of sampled windows at the VI parity bar (oracle perturbation cloud)
     for i in (0, 255):
         assert_parity_vi_converged(vio, ws[i], oracle_lib.ba_solve(vio, probs[i]), res[i])
