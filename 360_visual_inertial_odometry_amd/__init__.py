@@ -33,6 +33,7 @@ EXPORTS = [
     "vio_triangulate", "vio_triangulate_device", "vio_triangulate_kernel_ms",
     "vio_load_camera_timestamps", "vio_load_imu_csv", "erp_resize_area", "erp_resize_area_device",
     "erp_resize_area_kernel_ms", "erp_tracker_upload_resized",
+    "vio_ba_record_bytes", "vio_ba_batch_record_bytes", "vio_ba_batch_pack", "vio_ba_record_unpack",
 ]
 
 
@@ -99,6 +100,11 @@ def lib():
     L.erp_resize_area_device.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int]
     L.erp_resize_area_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
     L.erp_tracker_upload_resized.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int]
+    L.vio_ba_record_bytes.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.vio_ba_record_bytes.restype = C.c_size_t
+    L.vio_ba_batch_record_bytes.argtypes = [vp, C.POINTER(C.c_size_t)]
+    L.vio_ba_batch_pack.argtypes = [vp, vp, C.c_int]
+    L.vio_ba_record_unpack.argtypes = [vp, C.POINTER(abi.VioBaOutput)]
     _lib = L
     return L
 
@@ -299,6 +305,24 @@ def _imu_call(fn, check, samples, t_start, t_end, gyro_bias, accel_bias, noise):
     return {k: v[:n] for k, v in rec.items()}, valid[:n], cov_bias[:n]
 
 
+def record_bytes(K, L, N):
+    """vio_ba_record_bytes: size of a packed result record of a K x L x N window."""
+    return int(lib().vio_ba_record_bytes(K, L, N))
+
+
+def unpack_record(rec):
+    """vio_ba_record_unpack (host): one packed record (uint8 array) -> result dict (no chi2 / trace)."""
+    rec = np.ascontiguousarray(rec, np.uint8)
+    K, L, N = (int(v) for v in rec[:12].view(np.int32))
+    o = BaOutput(K, L, N)
+    rc = lib().vio_ba_record_unpack(_p(rec), C.byref(o.c))
+    if rc != 0:
+        raise VioError(f"vio_ba_record_unpack failed ({rc})")
+    r = o.result()
+    del r["obs_chi2"], r["trace"]
+    return r
+
+
 def _u8img(a):
     return np.ascontiguousarray(a, np.uint8)
 
@@ -467,6 +491,22 @@ class BaBatch:
         out = (C.c_ulonglong * 24)()
         self.ctx.check(lib().vio_ba_batch_phase_cycles(self.h, out), "vio_ba_batch_phase_cycles")
         return {n: int(out[i]) for i, n in enumerate(self.PHASES)}
+
+    def record_bytes(self):
+        """vio_ba_batch_record_bytes: the size of one packed per-window result record."""
+        n = C.c_size_t()
+        self.ctx.check(lib().vio_ba_batch_record_bytes(self.h, C.byref(n)), "vio_ba_batch_record_bytes")
+        return n.value
+
+    def pack(self, dst_ptr=None):
+        """vio_ba_batch_pack: every window's result record; into a device buffer (int pointer, async on
+        the context stream) or, with dst_ptr None, into a returned host (n, record_bytes) uint8 array."""
+        if dst_ptr is not None:
+            self.ctx.check(lib().vio_ba_batch_pack(self.h, dst_ptr, 1), "vio_ba_batch_pack")
+            return None
+        out = np.zeros((len(self.problems), self.record_bytes()), np.uint8)
+        self.ctx.check(lib().vio_ba_batch_pack(self.h, _p(out), 0), "vio_ba_batch_pack")
+        return out
 
     def download(self):
         outs = [BaOutput(p.K, p.L, p.N) for p in self.problems]

@@ -20,6 +20,7 @@
 namespace vio360 {
 
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream);
+hipError_t launch_ba_pack(const BaPools& P, int n, uint8_t* dst, int64_t rec_bytes, hipStream_t stream);
 hipError_t launch_ba_phases(const BaPools& P, const BaWin* hw, int n, hipStream_t stream);
 size_t ba_phase_doubles(int K, int L, int T);
 const char* ba_phases_failed_launch();
@@ -242,6 +243,7 @@ struct BaDevice {
     double ms_sum = 0.0;
     int ms_count = 0;
     bool timing_pending = false;
+    std::vector<int32_t> perm_host;
 };
 
 static int upload_batch(vio_ctx* ctx, BaDevice& d) {
@@ -276,6 +278,14 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     UP(pk.preint_valid, preint_valid, const uint8_t*);
     UP(pk.vel0, vel0, const double*);
 #undef UP
+    {   // sorted position -> caller's observation index, all windows back to back (result records)
+        std::vector<int32_t> perm;
+        perm.reserve(pk.N_total);
+        for (const auto& p : pk.perm) perm.insert(perm.end(), p.begin(), p.end());
+        if ((rc = up(perm.data(), bytes_of(perm), &ptr)) != VIO_OK) return rc;
+        d.P.obs_perm = (const int32_t*)ptr;
+        d.perm_host = std::move(perm);  // kept alive for the async upload
+    }
     auto alloc = [&](size_t bytes, void** dst) -> int {
         void* p = nullptr;
         VIO_HIP(ctx, hipMalloc(&p, std::max<size_t>(bytes, 16)));
@@ -392,8 +402,8 @@ static bool env_flag(const char* name) {
 }
 static bool force_monolithic(const BaDevice& d) {
     static const bool mono = env_flag("VIO_BA_MONOLITHIC"), phases = env_flag("VIO_BA_PHASES");
+    if (phases) return false;  // (per-phase profiling of the phase route: ph_solve's slots 16-20)
     if (mono || d.P.prof) return true;
-    if (phases) return false;
     int non_pnp = 0;
     for (const BaWin& w : d.pk.win) non_pnp += w.is_pnp ? 0 : 1;
     return non_pnp > PHASE_BATCH_MAX;
@@ -610,6 +620,80 @@ void vio_ba_batch_destroy(vio_ba_batch* b) {
     (void)hipStreamSynchronize(b->ctx->stream);
     free_batch(b->dev);
     delete b;
+}
+
+size_t vio_ba_record_bytes(int num_kf, int num_lm, int num_obs) {
+    if (num_kf < 0 || num_lm < 0 || num_obs < 0) return 0;
+    return (size_t)rec_layout(num_kf, num_lm, num_obs).total;
+}
+
+int vio_ba_batch_record_bytes(vio_ba_batch* b, size_t* bytes) {
+    if (!b || !bytes) return VIO_EINVAL;
+    size_t m = 0;
+    for (const BaWin& w : b->dev.pk.win) m = std::max(m, (size_t)rec_layout(w.K, w.L, w.N).total);
+    *bytes = m;
+    return VIO_OK;
+}
+
+int vio_ba_batch_pack(vio_ba_batch* b, void* dst, int on_device) {
+    if (!b || !dst) return VIO_EINVAL;
+    vio_ctx* ctx = b->ctx;
+    size_t rb = 0;
+    vio_ba_batch_record_bytes(b, &rb);
+    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    uint8_t* d = static_cast<uint8_t*>(dst);
+    if (!on_device) {
+        d = static_cast<uint8_t*>(ctx_buffer(ctx, kSlotRecords, rb * b->dev.n));
+        if (!d) { set_error(ctx, "vio_ba_batch_pack: device allocation failed"); return VIO_ENOMEM; }
+    }
+    hipError_t e = launch_ba_pack(b->dev.P, b->dev.n, d, (int64_t)rb, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "ba_pack_kernel");
+    if (!on_device) {
+        VIO_HIP(ctx, hipMemcpyAsync(dst, d, rb * b->dev.n, hipMemcpyDeviceToHost, ctx->stream));
+        VIO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return VIO_OK;
+}
+
+int vio_ba_record_unpack(const void* record, vio_ba_output* out) {
+    if (!record || !out) return VIO_EINVAL;
+    const uint8_t* rec = static_cast<const uint8_t*>(record);
+    int32_t hdr[4];
+    std::memcpy(hdr, rec, sizeof hdr);
+    const int K = hdr[0], L = hdr[1], N = hdr[2];
+    if (K <= 0 || L < 0 || N < 0 || hdr[3] != VIO_BA_RECORD_VERSION) return VIO_EINVAL;
+    const RecLayout R = rec_layout(K, L, N);
+    if (out->T_wb)
+        for (int k = 0; k < K; ++k) {
+            std::memcpy(out->T_wb[k].R, rec + R.T + 96 * k, 9 * sizeof(double));
+            std::memcpy(out->T_wb[k].t, rec + R.T + 96 * k + 72, 3 * sizeof(double));
+        }
+    if (out->lm_xyz) std::memcpy(out->lm_xyz, rec + R.lm, 24 * (size_t)L);
+    if (out->vel) std::memcpy(out->vel, rec + R.vel, 24 * (size_t)K);
+    if (out->bg) std::memcpy(out->bg, rec + R.bias, 24);
+    if (out->ba) std::memcpy(out->ba, rec + R.bias + 24, 24);
+    if (out->obs_outlier) std::memcpy(out->obs_outlier, rec + R.outl, N);
+    if (out->lm_bad) std::memcpy(out->lm_bad, rec + R.bad, L);
+    if (out->summary) {
+        int32_t a[SI_COUNT];
+        double d[SD_COUNT];
+        std::memcpy(a, rec + R.si, sizeof a);
+        std::memcpy(d, rec + R.sd, sizeof d);
+        vio_ba_summary& s = *out->summary;
+        std::memset(&s, 0, sizeof s);
+        s.success = a[SI_SUCCESS];
+        s.termination = a[SI_TERM];
+        s.iterations = a[SI_ITERS];
+        s.num_successful_steps = a[SI_NSUCC];
+        s.num_unsuccessful_steps = a[SI_NUNSUCC];
+        s.num_inliers = a[SI_NIN];
+        s.num_outliers = a[SI_NOUT];
+        s.num_bad_lm = a[SI_NBAD];
+        s.initial_cost = d[SD_INIT];
+        s.final_cost = d[SD_FINAL];
+        s.fixed_cost = d[SD_FIXED];
+    }
+    return VIO_OK;
 }
 
 int vio_ba_solve_batched(vio_ctx* ctx, const vio_ba_problem* probs, vio_ba_output* outs, int n) {

@@ -1872,6 +1872,41 @@ __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
     if (P.prof && threadIdx.x < PF_NSLOT) P.prof[PF_NSLOT * blockIdx.x + threadIdx.x] = sh.prof_acc[threadIdx.x];
 }
 
+// ------------------------------------------------------------------------------------------
+// result records (vio_ba_batch_pack): one workgroup per window, every field copied with coalesced
+// lanes; outlier flags scattered back to the caller's observation order
+__global__ void __launch_bounds__(BA_THREADS) ba_pack_kernel(BaPools P, uint8_t* dst, int64_t rec_bytes) {
+    const BaWin& w = P.win[blockIdx.x];
+    const int K = w.K, L = w.L, N = w.N;
+    const RecLayout R = rec_layout(K, L, N);
+    const BaOutLayout OL = ba_out_layout(K, L, N);
+    uint8_t* rec = dst + rec_bytes * blockIdx.x;
+    const double* out = P.out + w.o_out;
+    int32_t* hdr = reinterpret_cast<int32_t*>(rec);
+    if (threadIdx.x == 0) { hdr[0] = K; hdr[1] = L; hdr[2] = N; hdr[3] = VIO_BA_RECORD_VERSION; }
+    if (threadIdx.x < SI_COUNT) reinterpret_cast<int32_t*>(rec + R.si)[threadIdx.x] = P.out_i32[SI_COUNT * blockIdx.x + threadIdx.x];
+    if (threadIdx.x < SD_COUNT)
+        reinterpret_cast<double*>(rec + R.sd)[threadIdx.x] = threadIdx.x < 3 ? P.out_sum[SD_COUNT * blockIdx.x + threadIdx.x] : 0.0;
+    double* T = reinterpret_cast<double*>(rec + R.T);
+    for (int e = threadIdx.x; e < 12 * K; e += BA_THREADS) T[e] = out[OL.T_wb + e];
+    double* lm = reinterpret_cast<double*>(rec + R.lm);
+    for (int e = threadIdx.x; e < 3 * L; e += BA_THREADS) lm[e] = out[OL.lm + e];
+    double* vel = reinterpret_cast<double*>(rec + R.vel);
+    for (int e = threadIdx.x; e < 3 * K; e += BA_THREADS) vel[e] = out[OL.vel + e];
+    double* bias = reinterpret_cast<double*>(rec + R.bias);
+    if (threadIdx.x < 6) bias[threadIdx.x] = out[OL.bias + threadIdx.x];
+    uint8_t* outl = rec + R.outl;
+    for (int q = threadIdx.x; q < N; q += BA_THREADS) outl[P.obs_perm[w.o_obs + q]] = P.out_u8[w.o_obs + q];
+    uint8_t* bad = rec + R.bad;
+    for (int l = threadIdx.x; l < L; l += BA_THREADS) bad[l] = P.out_bad[w.o_lm + l];
+    for (int64_t e = R.bad + L + threadIdx.x; e < rec_bytes; e += BA_THREADS) rec[e] = 0;  // padding
+}
+
+hipError_t launch_ba_pack(const BaPools& P, int n, uint8_t* dst, int64_t rec_bytes, hipStream_t stream) {
+    hipLaunchKernelGGL(ba_pack_kernel, dim3(n), dim3(BA_THREADS), 0, stream, P, dst, rec_bytes);
+    return hipGetLastError();
+}
+
 size_t ba_shared_bytes() { return sizeof(BaShared); }
 size_t ba_ws_extra_doubles() { return ba_ws_extra(); }
 

@@ -62,6 +62,7 @@ struct BaPools {
     int32_t* out_i32;            // per-window summary ints [n][8]
     double* out_sum;             // per-window summary doubles [n][4]
     vio_ba_iteration* out_trace; // per-window Summary::iterations [sum tr_cap]
+    const int32_t* obs_perm;     // [sum N] landmark-sorted position -> the caller's observation index
     unsigned long long* prof;    // optional [n][VIO_BA_PROF_SLOTS] per-phase shader clocks (diagnostics), may be null
     int route;                   // 0: ba_window_kernel solves every window; 1: it solves the PnP windows
                                  // only and the phase kernels (ba_phases.inc) the others
@@ -117,6 +118,25 @@ __host__ __device__ inline BaOutLayout ba_out_layout(int K, int L, int N) {
     o = (o + 7) & ~(int64_t)7;
     w.total = o;
     return w;
+}
+
+// packed result record of one window (vio_ba_batch_pack / vio_ba_record_unpack), byte offsets
+struct RecLayout {
+    int64_t si, sd, T, lm, vel, bias, outl, bad, total;
+};
+__host__ __device__ inline RecLayout rec_layout(int K, int L, int N) {
+    RecLayout r;
+    int64_t o = 16;          // int32 K, L, N, version
+    r.si = o; o += 32;       // int32 summary[8]
+    r.sd = o; o += 32;       // f64 summary[4]
+    r.T = o; o += 96 * (int64_t)K;
+    r.lm = o; o += 24 * (int64_t)L;
+    r.vel = o; o += 24 * (int64_t)K;
+    r.bias = o; o += 48;
+    r.outl = o; o += N;
+    r.bad = o; o += L;
+    r.total = (o + 15) & ~(int64_t)15;
+    return r;
 }
 
 // summary slots

@@ -35,6 +35,8 @@ enum { kSlotImuData = 8, kSlotImuIntervals = 9, kSlotImuOut = 10 };
 enum { kSlotTriIn = 11, kSlotTriOut = 12 };
 // scratch slots owned by erp_resize_area
 enum { kSlotResizeSrc = 13, kSlotResizeDst = 14 };
+// staging of vio_ba_batch_pack to host memory
+enum { kSlotRecords = 15 };
 
 #define VIO_HIP(ctx, expr)                                  \
     do {                                                    \

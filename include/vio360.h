@@ -27,6 +27,7 @@
 #ifndef VIO360_H_
 #define VIO360_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -211,6 +212,25 @@ void vio_ba_batch_destroy(vio_ba_batch* b);
 int vio_ba_batch_profile(vio_ba_batch* b, int enable);
 #define VIO_BA_PROF_SLOTS 24
 int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out /* [VIO_BA_PROF_SLOTS] */);
+
+/*
+ * Packed per-window result records, for gathering the windows of a sharded batch over RCCL
+ * (config 4: 256 windows over 8 GPUs, one ncclAllGather of the records).  A record is
+ * self-describing and position-independent: {int32 K, L, N, version; int32 summary[8] (success,
+ * termination, iterations, successful, unsuccessful, inliers, outliers, bad MPs); f64 summary[4]
+ * (initial, final, fixed cost, 0); f64 T_wb[12K] (R row-major | t); f64 lm_xyz[3L]; f64 vel[3K];
+ * f64 bias[6] (bg | ba); u8 obs_outlier[N] in the caller's observation order; u8 lm_bad[L]}, padded
+ * to a multiple of 16 bytes.  Every record of a batch takes vio_ba_batch_record_bytes (the largest).
+ */
+#define VIO_BA_RECORD_VERSION 1
+size_t vio_ba_record_bytes(int num_kf, int num_lm, int num_obs);
+int vio_ba_batch_record_bytes(vio_ba_batch* b, size_t* bytes);
+/* the batch's n records back to back into dst (on_device != 0: a device buffer of this context's
+   device, written asynchronously on the context stream by a pack kernel; else host memory, blocking) */
+int vio_ba_batch_pack(vio_ba_batch* b, void* dst, int on_device);
+/* decode one record (host memory) into caller-owned outputs (NULL fields skipped; obs_chi2 and
+   trace are not carried: left untouched) */
+int vio_ba_record_unpack(const void* record, vio_ba_output* out);
 
 /* ----------------------------------------------------------------------------------------- */
 /* ERP feature tracking                                                                       */

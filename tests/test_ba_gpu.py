@@ -372,3 +372,34 @@ def test_config5_full_size_properties(vio, synth, gpu_ctx):
     assert e1 < 0.5 * e0
     g2 = gpu_ctx.ba_solve([p])[0]
     assert np.array_equal(g["T_wb"], g2["T_wb"]) and g["final_cost"] == g2["final_cost"]
+
+
+def test_packed_records_match_download(vio, synth, gpu_ctx):
+    """vio_ba_batch_pack (device pack kernel, the config-4 gather payload) decodes through
+    vio_ba_record_unpack to exactly the results vio_ba_batch_download returns, outlier flags in the
+    caller's observation order; host and device destinations give the same bytes."""
+    import torch
+    ws = [synth.config3(synth.SEED + i) for i in range(3)]
+    ws.append(synth.make_window(K=8, L=150, seed=3, marg_frac=0.2, outlier_frac=0.05, all_visible=False))
+    probs = [vio.BaProblem(w, variant=vio.VIO_BA_VI if i < 3 else vio.VIO_BA_LOCAL, max_iterations=6,
+                           fixed_iterations=1) for i, w in enumerate(ws)]
+    b = vio.BaBatch(gpu_ctx, probs)
+    b.run()
+    b.sync()
+    ref = b.download()
+    host = b.pack()
+    rb = b.record_bytes()
+    assert host.shape == (4, rb) and rb == max(vio.record_bytes(p.K, p.L, p.N) for p in probs)
+    dev = torch.zeros((4, rb), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    b.pack(dev.data_ptr())
+    b.sync()
+    assert np.array_equal(dev.cpu().numpy(), host)
+    for r, rec in zip(ref, host):
+        u = vio.unpack_record(rec)
+        for k in ("T_wb", "lm_xyz", "obs_outlier", "lm_bad", "bg", "ba"):
+            assert np.array_equal(u[k], r[k]), k
+        for k in ("iterations", "success", "num_inliers", "num_outliers", "num_bad_lm", "final_cost", "initial_cost"):
+            assert u[k] == r[k], k
+    assert np.array_equal(vio.unpack_record(host[0])["vel"], ref[0]["vel"])
+    b.close()

@@ -1,7 +1,10 @@
-"""N>1 path on CPU: world_size-2 gloo rehearsal of bench.py's sharding and timing reduction."""
+"""N>1 path on CPU: world-size 2/3 gloo rehearsals of bench.py's sharding, timing reduction and the
+config-4 result gather (windows in contiguous blocks per rank, one all-gather of packed
+per-window result records, decoded by libvio360's vio_ba_record_unpack)."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -14,6 +17,20 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def _run(world, target, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    return res
 
 
 def _worker(rank, world, port, q):
@@ -32,17 +49,52 @@ def _worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharding_and_max_reduction(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    shards, tmax = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    shards, tmax = _run(world, _worker)
     flat = [s for sh in shards for s in sh]
     assert len(flat) == len(set(flat)) == 5 * world          # disjoint shards
     assert sorted(flat) == list(range(1000, 1000 + 5 * world))  # covering the job
     assert tmax == 0.5 * world                                  # slowest rank's time
+
+
+def _config4_worker(rank, world, port, q, total, iters):
+    """One rank of config 4 on the CPU leg: its contiguous block of windows solved by the oracle,
+    packed into result records, all-gathered; rank 0 decodes every record."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import importlib
+    import bench
+    import oracle_lib
+    import records
+    vio = importlib.import_module("360_visual_inertial_odometry_amd")
+    synth = importlib.import_module("360_visual_inertial_odometry_amd.synth")
+    mine = bench.strong_shard(total, rank, world)
+    recs = []
+    for w in mine:
+        p = vio.BaProblem(synth.config3(synth.SEED + w), variant=vio.VIO_BA_VI, max_iterations=iters, fixed_iterations=1)
+        recs.append(records.pack(oracle_lib.ba_solve(vio, p), p.K, p.L, p.N))
+    local = torch.from_numpy(np.stack(recs))
+    gathered = bench.gather_records(local, dist, world, -(-total // world))
+    if rank == 0:
+        rows = [vio.unpack_record(r) for r in gathered.numpy() if r[:4].view(np.int32)[0] > 0]
+        q.put((rows, [bench.strong_shard(total, r, world) for r in range(world)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total", [(2, 256), (3, 40)])
+def test_config4_gather_of_packed_results(vio, synth, world, total):
+    """2 x 128 windows (and an uneven 3-rank split of 40): every window solved exactly once, its
+    gathered record decodes to the result the oracle gives for that window, in window order."""
+    import oracle_lib
+    iters = 1
+    rows, shards = _run(world, _config4_worker, total, iters)
+    flat = [w for sh in shards for w in sh]
+    assert flat == list(range(total))
+    assert len(rows) == total
+    for w in (0, total // 2, total - 1):
+        p = vio.BaProblem(synth.config3(synth.SEED + w), variant=vio.VIO_BA_VI, max_iterations=iters, fixed_iterations=1)
+        o = oracle_lib.ba_solve(vio, p)
+        g = rows[w]
+        for k in ("T_wb", "lm_xyz", "vel", "bg", "ba", "obs_outlier", "lm_bad"):
+            assert np.array_equal(g[k], o[k]), (w, k)
+        assert g["iterations"] == o["iterations"] == iters + 1 and g["final_cost"] == o["final_cost"]

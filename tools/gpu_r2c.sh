@@ -1,0 +1,12 @@
+#!/bin/bash
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 60 python tools/ph_solve_stamps.py 1 > gpurun_out/stamps.log 2>&1 || exit 1
+timeout -k 10 60 python tools/ph_solve_stamps.py 256 >> gpurun_out/stamps.log 2>&1 || exit 1
+cat gpurun_out/stamps.log | grep W=
+export VIO_BA_PHASES=1
+for w in 1 32; do
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ph$w -o ph --output-format csv -- python3 tools/ba_batch_run.py $w 10 > gpurun_out/prof_ph$w.log 2>&1 || exit 1
+done
+echo done

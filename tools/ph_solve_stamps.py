@@ -1,0 +1,28 @@
+"""Diagnostic: ph_solve_kernel shader-clock breakdown (phase route, VIO_BA_PHASES=1) for W windows."""
+import importlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401
+
+os.environ["VIO_BA_PHASES"] = "1"
+vio = importlib.import_module("360_visual_inertial_odometry_amd")
+synth = importlib.import_module("360_visual_inertial_odometry_amd.synth")
+W = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+ctx = vio.Context(0)
+probs = [vio.BaProblem(synth.config3(synth.SEED + i), variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1)
+         for i in range(W)]
+b = vio.BaBatch(ctx, probs)
+b.run(); b.sync()
+b.profile(True)
+b.run(); b.sync()
+import ctypes as C
+out = (C.c_ulonglong * 24)()
+ctx.check(vio.lib().vio_ba_batch_phase_cycles(b.h, out), "phase_cycles")
+names = {16: "assembly+partials", 17: "cholesky+solves", 18: "candidates+posecache", 19: "imu model+cand", 20: "reductions"}
+tot = sum(out[i] for i in names)
+for i, n in names.items():
+    print(f"W={W} {n:24s} cycles/window/iter {out[i] / W / 10:10.0f}  ({100 * out[i] / max(tot, 1):.1f}%)")
+b.close(); ctx.close()
