@@ -597,6 +597,10 @@ int vio_ba_batch_profile(vio_ba_batch* b, int enable) {
         VIO_HIP(b->ctx, hipMemsetAsync(b->dev.prof_buf, 0, sizeof(unsigned long long) * VIO_BA_PROF_SLOTS * b->dev.n, b->ctx->stream));
     }
     b->dev.P.prof = enable ? (unsigned long long*)b->dev.prof_buf : nullptr;
+    if (b->dev.phase_graph) {  // the captured phase sequence holds the old kernel arguments
+        (void)hipGraphExecDestroy(b->dev.phase_graph);
+        b->dev.phase_graph = nullptr;
+    }
     return VIO_OK;
 }
 

@@ -15,14 +15,16 @@ ctx = vio.Context(0)
 probs = [vio.BaProblem(synth.config3(synth.SEED + i), variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1)
          for i in range(W)]
 b = vio.BaBatch(ctx, probs)
-b.run(); b.sync()
 b.profile(True)
 b.run(); b.sync()
 import ctypes as C
 out = (C.c_ulonglong * 24)()
 ctx.check(vio.lib().vio_ba_batch_phase_cycles(b.h, out), "phase_cycles")
-names = {16: "assembly+partials", 17: "cholesky+solves", 18: "candidates+posecache", 19: "imu model+cand", 20: "reductions"}
+names = {0: "prep U partials", 1: "prep imu", 2: "prep cost partials", 3: "prep imu normal eq", 4: "prep gradient",
+         5: "prep finalize+diag",
+         16: "solve assembly+partials", 17: "solve cholesky+solves", 18: "solve candidates+posecache",
+         19: "solve imu model+cand", 20: "solve reductions", 21: "ctrl lane", 22: "ctrl copies"}
 tot = sum(out[i] for i in names)
 for i, n in names.items():
-    print(f"W={W} {n:24s} cycles/window/iter {out[i] / W / 10:10.0f}  ({100 * out[i] / max(tot, 1):.1f}%)")
+    print(f"W={W} {n:28s} cycles/window/iter {out[i] / W / 11:10.0f}  ({100 * out[i] / max(tot, 1):.1f}%)")
 b.close(); ctx.close()
