@@ -64,6 +64,7 @@ struct __align__(16) BaShared {
     int posef[BA_KMAX];          // copy of BaWin::pose_f (per-lane indexed in the Schur fill)
     int pvalid[BA_KMAX];         // preint_valid
     int8_t icol[BA_KMAX][12];    // imu_col(w, k, c): imu-space index of column c of IMU factor k, or -1
+    int8_t tile_i[24], tile_j[24];  // lower 16x16 tile t -> (tile row, tile column) (ph_solve assembly)
     double Rlin[BA_KMAX][9];     // R_bw at the linearisation point (Jacobians are stored compressed)
 };
 static_assert(sizeof(BaShared) <= 160 * 1024, "BaShared exceeds the 160 KB LDS of a gfx950 CU");
@@ -982,7 +983,13 @@ __device__ __forceinline__ void schur_gemm(BaShared& sh, const WinCtx& c) {
 // one wave (lanes = 16 rows x 4 column groups; the tile's right-hand side is broadcast through LDS).
 // Fixed operation order: bitwise reproducible.  (tools/probe/chol_probe.hip times the variants.)
 // Returns false (uniformly) when a pivot is not positive (S not positive definite).
-__device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
+struct NoStamp {
+    __device__ void operator()(int) const {}
+};
+// stamp(slot): optional diagnostic marks (diagonal tiles 8, panels 9, trailing updates 10, forward 11,
+// backward 12)
+template <typename Stamp = NoStamp>
+__device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf, Stamp stamp = Stamp()) {
     double* S = sh.S;
     double* LB = sh.stage;  // [nb][16 m][16 c] = Linv_J[c][m]
     double* LT = sh.stage + 256 * ((BA_NF_MAX + 15) >> 4);  // [16 m][16 q] = L_JJ[q][m]; then 16 rhs
@@ -999,6 +1006,7 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
             if (lane == 0) sh.chol_bad = bad;
         }
         __syncthreads();
+        stamp(8);
         if (sh.chol_bad) return false;
         // (B) panel: L_IJ = S_IJ Linv_J^T
         const double* lb = LB + 256 * J;
@@ -1015,6 +1023,7 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
             for (int r = 0; r < 4; ++r) A[(kk + 4 * r) * ls + r16] = acc[r];
         }
         __syncthreads();
+        stamp(9);
         // (C) trailing update of the lower tiles (I, K), J < K <= I < nb
         const int m = nb - J - 1, nt = m * (m + 1) / 2;
         for (int t = wid; t < nt; t += NW) {
@@ -1036,6 +1045,7 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
             for (int r = 0; r < 4; ++r) C[(kk + 4 * r) * ls + r16] -= acc[r];
         }
         __syncthreads();
+        stamp(10);
     }
     // triangular solves by wave 0: lane (row r16 of the tile column, column group kk)
     if (wid == 0) {
@@ -1061,6 +1071,7 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
             if (kk == 0) y[16 * J + r16] = v;
             wave_lds_sync();
         }
+        stamp(11);
         for (int J = nb - 1; J >= 0; --J) {  // backward: x_J = Linv_J^T (y_J - sum_{K>J} L_KJ^T x_K)
             double p0 = 0.0, p1 = 0.0;
             int cix = 16 * (J + 1) + kk;
@@ -1085,6 +1096,7 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf) {
             if (kk == 0) y[16 * J + r16] = v;
             wave_lds_sync();
         }
+        stamp(12);
     }
     __syncthreads();
     return true;
