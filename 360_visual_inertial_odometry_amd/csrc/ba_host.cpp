@@ -22,7 +22,7 @@ namespace vio360 {
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream);
 hipError_t launch_ba_pack(const BaPools& P, int n, uint8_t* dst, int64_t rec_bytes, hipStream_t stream);
 hipError_t launch_ba_phases(const BaPools& P, const BaWin* hw, int n, hipStream_t stream);
-size_t ba_phase_doubles(int K, int L, int T);
+size_t ba_phase_doubles(int K, int L, int N, int T);
 const char* ba_phases_failed_launch();
 hipError_t ba_phases_prepare(const BaWin* hw, int n);
 bool global_ba_applicable(const vio_ba_problem& p);
@@ -163,7 +163,7 @@ int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
     w.tr_cap = (w.max_iter + 1) * w.rounds;  // every Summary::iterations entry of every round
     pk.tr_total += w.tr_cap;
     BaWsLayout WL = ba_ws_layout(K, L, N);
-    pk.ws_total += WL.total + (int64_t)ba_ws_extra_doubles() + (int64_t)ba_phase_doubles(K, L, w.T);
+    pk.ws_total += WL.total + (int64_t)ba_ws_extra_doubles() + (int64_t)ba_phase_doubles(K, L, N, w.T);
     pk.ws_total = (pk.ws_total + 31) & ~(int64_t)31;
     pk.out_total += ba_out_layout(K, L, N).total;
     // poses

@@ -56,6 +56,7 @@ struct __align__(16) BaShared {
     double imu_J[VI_KMAX][108];  // per factor 9x12: [vi | bg | ba | vj]
     double red[BA_THREADS / 64 + 4];
     double redm[BA_THREADS / 64 + 4];
+    double redv[(BA_THREADS / 64) * 8];  // block_reduce exchange (up to 8 values)
     LmState st;
     unsigned long long prof_acc[VIO_BA_PROF_SLOTS];
     unsigned long long prof_last;
@@ -124,6 +125,28 @@ __device__ __forceinline__ double block_max(double v, double* red) {
 #pragma unroll
     for (int w = 0; w < BA_THREADS / 64; ++w) r = fmax(r, red[w]);
     return r;
+}
+
+// NS sums then NM maxima of per-thread values over the workgroup in one exchange (two barriers for
+// all of them); each value reduced in the fixed order of block_sum / block_max.  red: NW*(NS+NM) doubles
+template <int NS, int NM>
+__device__ __forceinline__ void block_reduce(double (&v)[NS + NM], double* red) {
+    constexpr int NV = NS + NM, NW = BA_THREADS / 64;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = i < NS ? wave_sum(v[i]) : wave_max(v[i]);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) red[(threadIdx.x >> 6) * NV + i] = v[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        double r = 0.0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) r = i < NS ? r + red[w * NV + i] : fmax(r, red[w * NV + i]);
+        v[i] = r;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
