@@ -179,24 +179,79 @@ def config4_strong(vio, synth, ctx, dist, rank, world, steps, warmup, lm_iters, 
                     "the records; rank 0 decodes every record"}
 
 
+def cpu_threads_available():
+    """Host threads this process may use: the affinity mask, capped by OMP_NUM_THREADS (the GPU box
+    exports its per-GPU CPU share there; os.cpu_count() is the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_host_info():
+    return {"nproc": os.cpu_count(), "threads_available": cpu_threads_available(), "cpu_model": cpu_model()}
+
+
 def cpu_baseline(vio, synth, lm_iters, seconds):
-    """Oracle (C restatement of the reference path, 1 thread) on config-3 windows, fixed iterations."""
+    """Oracle (C restatement of the reference path) on config-3 windows, fixed iterations, at 1 / 4 /
+    all available host threads (Ceres runs num_threads = 4, Optimizer.cpp:79):
+      - single window: the threads work inside one solve (oracle_set_threads: OpenMP over the
+        observations, the Schur elimination chunks and the back-substitution), as Ceres does;
+      - config 4: independent windows over a pool of threads (one window per thread at a time; the
+        ctypes call releases the GIL), the CPU counterpart of the GPU's throughput metric.
+    value = config-4 throughput at all available threads (the strongest CPU number)."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     L = oracle_lib.load()
-    solves, busy = 0, 0.0
-    while busy < seconds or solves < 3:
-        p = vio.BaProblem(synth.config3(synth.SEED + solves), variant=vio.VIO_BA_VI, max_iterations=lm_iters,
-                          fixed_iterations=1)
+    nthr = cpu_threads_available()
+    pool = [vio.BaProblem(synth.config3(synth.SEED + i), variant=vio.VIO_BA_VI, max_iterations=lm_iters,
+                          fixed_iterations=1) for i in range(max(8, min(nthr, 64)))]
+
+    def solve(p):
         O = vio.BaOutput(p.K, p.L, p.N)
-        ts = time.perf_counter()
         rc = L.oracle_ba_solve(C.byref(p.c), C.byref(O.c))
-        busy += time.perf_counter() - ts
         assert rc == 0
-        solves += 1
-    return {"value": solves * lm_iters / busy, "unit": "window-LM-iterations/s", "cores": 1, "kind": "port",
-            "sample": f"{solves} config-3 VIO windows x {lm_iters} LM iterations (oracle/ba_oracle.c, -O3, 1 thread), "
-                      f"{busy:.1f} s of solve time"}
+
+    single = {}
+    for T in (1, 4):
+        L.oracle_set_threads(T)
+        n, t0 = 0, time.perf_counter()
+        while n < 2 or time.perf_counter() - t0 < seconds / 4:
+            solve(pool[n % len(pool)])
+            n += 1
+        single[T] = n * lm_iters / (time.perf_counter() - t0)
+    L.oracle_set_threads(1)
+    multi = {}
+    for T in sorted({1, 4, nthr}):
+        n, t0 = 0, time.perf_counter()
+        with ThreadPoolExecutor(T) as ex:
+            while n < 2 * T or time.perf_counter() - t0 < seconds / 6:
+                list(ex.map(solve, [pool[(n + i) % len(pool)] for i in range(T)]))
+                n += T
+        multi[T] = n * lm_iters / (time.perf_counter() - t0)
+    return {"value": multi[nthr], "unit": "window-LM-iterations/s", "cores": nthr, "kind": "port",
+            **cpu_host_info(),
+            "config4_windows_parallel": {str(t): v for t, v in multi.items()},
+            "single_window_threads": {str(t): v for t, v in single.items()},
+            "sample": f"config-3 VIO windows x {lm_iters} LM iterations through oracle/ba_oracle.c (-O3, OpenMP): "
+                      f"single window at 1/4 threads inside the solve (~{seconds / 4:.0f} s each), independent "
+                      f"windows over 1/4/{nthr} threads (~{seconds / 6:.0f} s each)"}
 
 
 def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
@@ -255,21 +310,29 @@ def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
         kp = vio.default_klt_params()
-        n, busy = 0, 0.0
-        while busy < cpu_seconds or n < 1:
-            ts = time.perf_counter()
-            nxt, st, _ = oracle_lib.klt_track(a, b, pts, kp)
-            vr = nxt[:, 1] / np.float32(H)
-            good = np.nonzero((st == 1) & (vr >= 0.15) & (vr <= 0.85) & (nxt[:, 0] >= 20) & (nxt[:, 0] <= W - 20))[0]
-            s = vio.ransac_samples(1, len(good), 1000)
-            km, _ = oracle_lib.rot_ransac(pts[good], nxt[good], W, H, s, vio.ransac_threshold())
-            m2 = mask.copy()
-            oracle_lib.gftt(b, m2, 300, float(np.float32(0.01)), 30.0)
-            busy += time.perf_counter() - ts
-            n += 1
-        out["cpu_baseline"] = {"value": n * mpx / busy, "unit": "Mpx/s", "cores": 1, "kind": "port",
-                               "sample": f"{n} config-1 frame pairs through oracle/tracker_oracle.c (pyramids+LK+RANSAC+GFTT), "
-                                         f"{busy:.1f} s"}
+        L = oracle_lib.load()
+        nthr = cpu_threads_available()
+        by_t = {}
+        for T in sorted({1, 4, nthr}):
+            L.oracle_set_threads(T)
+            n, busy = 0, 0.0
+            while busy < cpu_seconds / 3 or n < 1:
+                ts = time.perf_counter()
+                nxt, st, _ = oracle_lib.klt_track(a, b, pts, kp)
+                vr = nxt[:, 1] / np.float32(H)
+                good = np.nonzero((st == 1) & (vr >= 0.15) & (vr <= 0.85) & (nxt[:, 0] >= 20) & (nxt[:, 0] <= W - 20))[0]
+                s = vio.ransac_samples(1, len(good), 1000)
+                km, _ = oracle_lib.rot_ransac(pts[good], nxt[good], W, H, s, vio.ransac_threshold())
+                m2 = mask.copy()
+                oracle_lib.gftt(b, m2, 300, float(np.float32(0.01)), 30.0)
+                busy += time.perf_counter() - ts
+                n += 1
+            by_t[str(T)] = n * mpx / busy
+        L.oracle_set_threads(1)
+        out["cpu_baseline"] = {"value": by_t[str(nthr)], "unit": "Mpx/s", "cores": nthr, "kind": "port",
+                               **cpu_host_info(), "by_threads": by_t,
+                               "sample": f"config-1 frame pairs through oracle/tracker_oracle.c (pyramids+LK+RANSAC+GFTT; "
+                                         f"OpenMP over rows / points at 1/4/{nthr} threads, ~{cpu_seconds / 3:.0f} s each)"}
     return out
 
 
@@ -343,7 +406,7 @@ def imu_bench(vio, ctx, steps, cpu_seconds, want_cpu):
             oracle_lib.imu_preintegrate(vio, imu, t0, t1)
             reps += 1
         cpu_s = (time.perf_counter() - t_start) / reps
-        out["cpu_baseline"] = {"value": n_int / cpu_s, "unit": "intervals/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": n_int / cpu_s, "unit": "intervals/s", "cores": 1, "kind": "port", **cpu_host_info(),
                                "sample": f"{reps} x 2304 intervals through oracle/imu_oracle.c (1 thread)"}
     return out
 
@@ -396,7 +459,7 @@ def tri_bench(vio, ctx, steps, want_cpu):
         t_start = time.perf_counter()
         tri.triangulate(T, pairs[:m], B[:m], 3840)
         cpu_s = time.perf_counter() - t_start
-        out["cpu_baseline"] = {"value": m / cpu_s, "unit": "candidates/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": m / cpu_s, "unit": "candidates/s", "cores": 1, "kind": "port", **cpu_host_info(),
                                "sample": f"{m} candidates through oracle/tri_oracle.py (numpy / LAPACK batched SVD)"}
     return out
 
@@ -525,6 +588,13 @@ def main():
         single_wall = (time.perf_counter() - t1) / n1
         single_kms, _ = one.kernel_ms()
         one.close()
+        # the same window through vio_ba_solve: host problem in, host result out (upload + solve +
+        # download per call, SURVEY §8d's single-window definition)
+        ctx.ba_solve(probs[:1])
+        t1 = time.perf_counter()
+        for _ in range(n1):
+            ctx.ba_solve(probs[:1])
+        single_xfer_wall = (time.perf_counter() - t1) / n1
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(vio, synth, args.lm_iters, args.cpu_seconds)
         gba = None if args.no_global else global_ba_bench(vio, synth, ctx, args.lm_iters)
         klt = None if args.no_klt else klt_bench(vio, synth, ctx, args.klt_steps, 3, args.cpu_seconds,
@@ -570,8 +640,15 @@ def main():
             "single_window": {
                 "config": "config 3 (one window per launch)",
                 "iters_per_s_wall": single_ips,
+                "iters_per_s_with_transfer": args.lm_iters / single_xfer_wall,
                 "kernel_ms": single_kms,
-                "vs_cpu": (single_ips / cpu["value"]) if cpu else None,
+                "vs_cpu_1t": (single_ips / cpu["single_window_threads"]["1"]) if cpu else None,
+                "vs_cpu_4t": (single_ips / cpu["single_window_threads"]["4"]) if cpu else None,
+                "vs_cpu_4t_with_transfer": (args.lm_iters / single_xfer_wall / cpu["single_window_threads"]["4"])
+                if cpu else None,
+                "note": "resident = BaBatch re-run on device-resident inputs; with_transfer = vio_ba_solve "
+                        "(pack + upload + solve + download) per call; CPU = the oracle on one window at 1 / 4 "
+                        "threads inside the solve",
             },
             "cpu_baseline": cpu,
             "config4_strong": c4,

@@ -28,6 +28,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #include "../include/vio360.h"
 
@@ -36,6 +39,14 @@
 #endif
 
 #define EPS_D 1e-10 /* kEpsilonD, src/util/LieUtils.h:24 */
+
+/* Threads of one window solve (the CPU-baseline leg only; Ceres runs num_threads = 4,
+   src/optimization/Optimizer.cpp:79).  1 (the default, and what every parity test uses) runs the
+   single-threaded code paths unchanged; > 1 switches the observation loops, the Schur elimination
+   and the back-substitution to OpenMP variants whose reduction order differs from the serial one. */
+static int oracle_threads = 1;
+void oracle_set_threads(int n) { oracle_threads = n > 1 ? n : 1; }
+int oracle_get_threads(void) { return oracle_threads; }
 
 /* ========================================================================================= */
 /* 3x3 helpers (row-major)                                                                   */
@@ -737,8 +748,11 @@ static int* bsm_row_groups(const oracle_bsm* A, int** ptr_out) {
 /* lhs (n_red x n_red, full symmetric, row-major) = F^T F + D_f^2 - F^T E (E^T E + D_e^2)^-1 E^T F,
    rhs = F^T b - F^T E (E^T E + D_e^2)^-1 E^T b.  D may be NULL (no regularisation).  Returns 0 if an
    e-block is not positive definite. */
+static int schur_eliminate_mt(const oracle_bsm* A, const double* b, const double* D, double* lhs, double* rhs);
+
 int oracle_schur_eliminate(const oracle_bsm* A, const double* b, const double* D, double* lhs, double* rhs) {
     const int S = A->n_red;
+    if (oracle_threads > 1 && S <= 1024) return schur_eliminate_mt(A, b, D, lhs, rhs);
     memset(lhs, 0, sizeof(double) * (size_t)S * S);
     memset(rhs, 0, sizeof(double) * S);
     if (D)
@@ -829,6 +843,112 @@ int oracle_schur_eliminate(const oracle_bsm* A, const double* b, const double* D
     return ok;
 }
 
+/* The same elimination with the e-block chunks spread over oracle_threads threads (Ceres'
+   ParallelFor over chunks, schur_eliminator_impl.h:179-260): each thread accumulates its chunks'
+   updates into a private reduced system, the partials are added in thread order. */
+static int schur_eliminate_mt(const oracle_bsm* A, const double* b, const double* D, double* lhs, double* rhs) {
+    const int S = A->n_red, T = oracle_threads;
+    memset(lhs, 0, sizeof(double) * (size_t)S * S);
+    memset(rhs, 0, sizeof(double) * S);
+    if (D)
+        for (int cb = 0; cb < A->n_cols; ++cb) {
+            if (bsm_is_e(A, cb)) continue;
+            for (int i = 0; i < A->col_size[cb]; ++i)
+                lhs[(size_t)(A->col_red[cb] + i) * S + A->col_red[cb] + i] += D[A->col_pos[cb] + i] * D[A->col_pos[cb] + i];
+        }
+    int* ptr;
+    int* list = bsm_row_groups(A, &ptr);
+    for (int r = 0; r < A->n_rows; ++r) {
+        const int rs = A->row_size[r];
+        const double* br = b + A->row_pos[r];
+        for (int c1 = A->row_cell[r]; c1 < A->row_cell[r + 1]; ++c1) {
+            const int f1 = A->cell_col[c1];
+            if (bsm_is_e(A, f1)) continue;
+            const int s1 = A->col_size[f1], o1 = A->col_red[f1];
+            const double* F1 = A->values + A->cell_off[c1];
+            acc_tv(rs, s1, F1, br, rhs + o1);
+            for (int c2 = A->row_cell[r]; c2 < A->row_cell[r + 1]; ++c2) {
+                const int f2 = A->cell_col[c2];
+                if (bsm_is_e(A, f2)) continue;
+                acc_tn(rs, s1, A->col_size[f2], F1, A->values + A->cell_off[c2], lhs + (size_t)o1 * S + A->col_red[f2], S);
+            }
+        }
+    }
+    const size_t SS = (size_t)(S > 0 ? S : 1);
+    double* part = (double*)calloc((size_t)T * (SS * SS + SS), sizeof(double));
+    int ok = 1;
+#pragma omp parallel num_threads(T) reduction(&& : ok)
+    {
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        double* pl = part + (size_t)tid * (SS * SS + SS);
+        double* pr = pl + SS * SS;
+        double* FtE = (double*)malloc(sizeof(double) * SS * 9);
+        uint8_t* touched = (uint8_t*)calloc(A->n_cols > 0 ? A->n_cols : 1, 1);
+        int* tlist = (int*)malloc(sizeof(int) * (A->n_cols > 0 ? A->n_cols : 1));
+#pragma omp for schedule(static)
+        for (int e = 0; e < A->n_cols; ++e) {
+            if (!bsm_is_e(A, e) || !ok) continue;
+            const int* rows = list + ptr[e];
+            const int nr = ptr[e + 1] - ptr[e];
+            const int es = A->col_size[e];
+            double Einv[81], Etb[9] = {0};
+            if (!bsm_e_inverse(A, e, rows, nr, D, Einv)) { ok = 0; continue; }
+            int nt = 0;
+            for (int q = 0; q < nr; ++q)
+                for (int c = A->row_cell[rows[q]]; c < A->row_cell[rows[q] + 1]; ++c) {
+                    const int f = A->cell_col[c];
+                    if (bsm_is_e(A, f) || touched[f]) continue;
+                    touched[f] = 1;
+                    tlist[nt++] = f;
+                    memset(FtE + (size_t)A->col_red[f] * es, 0, sizeof(double) * A->col_size[f] * es);
+                }
+            for (int q = 0; q < nr; ++q) {
+                const int r = rows[q], rs = A->row_size[r];
+                const double* E = NULL;
+                for (int c = A->row_cell[r]; c < A->row_cell[r + 1]; ++c)
+                    if (A->cell_col[c] == e) E = A->values + A->cell_off[c];
+                acc_tv(rs, es, E, b + A->row_pos[r], Etb);
+                for (int c = A->row_cell[r]; c < A->row_cell[r + 1]; ++c) {
+                    const int f = A->cell_col[c];
+                    if (bsm_is_e(A, f)) continue;
+                    acc_tn(rs, A->col_size[f], es, A->values + A->cell_off[c], E, FtE + (size_t)A->col_red[f] * es, es);
+                }
+            }
+            for (int a = 0; a < nt; ++a) {
+                const int f1 = tlist[a];
+                const int s1 = A->col_size[f1], o1 = A->col_red[f1];
+                double Y[9 * 9];
+                for (int i = 0; i < s1; ++i) {
+                    for (int j = 0; j < es; ++j) {
+                        double acc = 0.0;
+                        for (int t = 0; t < es; ++t) acc += FtE[(size_t)(o1 + i) * es + t] * Einv[t * es + j];
+                        Y[i * es + j] = acc;
+                    }
+                    double acc = 0.0;
+                    for (int j = 0; j < es; ++j) acc += Y[i * es + j] * Etb[j];
+                    pr[o1 + i] -= acc;
+                }
+                for (int bq = 0; bq < nt; ++bq) {
+                    const int f2 = tlist[bq];
+                    sub_ytz(s1, A->col_size[f2], es, Y, FtE + (size_t)A->col_red[f2] * es, pl + (size_t)o1 * S + A->col_red[f2], S);
+                }
+            }
+            for (int a = 0; a < nt; ++a) touched[tlist[a]] = 0;
+        }
+        free(FtE); free(touched); free(tlist);
+    }
+    for (int t = 0; t < T; ++t) {
+        const double* pl = part + (size_t)t * (SS * SS + SS);
+        for (size_t i = 0; i < (size_t)S * S; ++i) lhs[i] += pl[i];
+        for (int i = 0; i < S; ++i) rhs[i] += pl[SS * SS + i];
+    }
+    free(part); free(list); free(ptr);
+    return ok;
+}
+
 /* x (full vector): f-blocks copied from z (reduced solution), e-blocks
    x_e = (E^T E + D_e^2)^-1 E^T (b - sum_f F z_f) (schur_eliminator_impl.h:311-377) */
 int oracle_schur_back_substitute(const oracle_bsm* A, const double* b, const double* D, const double* z, double* x) {
@@ -838,13 +958,15 @@ int oracle_schur_back_substitute(const oracle_bsm* A, const double* b, const dou
     int* ptr;
     int* list = bsm_row_groups(A, &ptr);
     int ok = 1;
-    for (int e = 0; e < A->n_cols && ok; ++e) {
-        if (!bsm_is_e(A, e)) continue;
+    /* the e-blocks are independent: threads only change which core computes each one */
+#pragma omp parallel for num_threads(oracle_threads) schedule(static) reduction(&& : ok) if (oracle_threads > 1)
+    for (int e = 0; e < A->n_cols; ++e) {
+        if (!bsm_is_e(A, e) || !ok) continue;
         const int* rows = list + ptr[e];
         const int nr = ptr[e + 1] - ptr[e];
         const int es = A->col_size[e];
         double Einv[81], rhs[9] = {0};
-        if (!bsm_e_inverse(A, e, rows, nr, D, Einv)) { ok = 0; break; }
+        if (!bsm_e_inverse(A, e, rows, nr, D, Einv)) { ok = 0; continue; }
         for (int q = 0; q < nr; ++q) {
             const int r = rows[q], rs = A->row_size[r];
             double sres[9];
@@ -1177,6 +1299,9 @@ typedef struct {
     double* values;
     double* bvec;        /* residuals in row order */
     int* row_src;        /* per row: observation o, or -(1 + k) for the IMU factor k-1 -> k */
+    /* per-observation scratch of the multi-threaded evaluation (oracle_threads > 1) */
+    double* obs_tmp;     /* N */
+    uint8_t* obs_ok;     /* N */
 } ba_ctx;
 
 static void ba_unpack(ba_ctx* c, const double* x) {
@@ -1234,13 +1359,34 @@ static int ba_eval(void* user, const double* x, double* cost, int want_jac, doub
         memset(g, 0, sizeof(double) * c->n);
         memset(colsq, 0, sizeof(double) * c->n);
     }
+    /* multi-threaded: the factors are evaluated in parallel first, the sums below keep their order */
+    const int mt = oracle_threads > 1;
+    if (mt) {
+#pragma omp parallel for num_threads(oracle_threads) schedule(static)
+        for (int o = 0; o < c->N; ++o) {
+            if (!c->obs_active[o]) continue;
+            double r[2];
+            c->obs_ok[o] = (uint8_t)ba_eval_obs(c, o, &c->obs_tmp[o], r, want_jac ? c->Jp + 12 * o : NULL,
+                                                want_jac ? c->Jl + 6 * o : NULL);
+            if (want_jac) {
+                c->r[2 * o] = r[0];
+                c->r[2 * o + 1] = r[1];
+            }
+        }
+    }
     for (int o = 0; o < c->N; ++o) {
         if (!c->obs_active[o]) continue;
         int k = c->p->obs_kf[o], l = c->p->obs_lm[o];
         double cst, r[2];
         double* Jp = want_jac ? c->Jp + 12 * o : NULL;
         double* Jl = want_jac ? c->Jl + 6 * o : NULL;
-        if (!ba_eval_obs(c, o, &cst, r, Jp, Jl)) return 0;
+        if (mt) {
+            if (!c->obs_ok[o]) return 0;
+            cst = c->obs_tmp[o];
+            if (want_jac) { r[0] = c->r[2 * o]; r[1] = c->r[2 * o + 1]; }
+        } else if (!ba_eval_obs(c, o, &cst, r, Jp, Jl)) {
+            return 0;
+        }
         total += cst;
         if (want_jac) {
             c->r[2 * o] = r[0];
@@ -1296,6 +1442,7 @@ static int ba_solve(void* user, const double* s, const double* D, double* y) {
     ba_ctx* c = (ba_ctx*)user;
     const oracle_bsm* A = &c->A;
     /* values of J~ and the residual vector, row by row */
+#pragma omp parallel for num_threads(oracle_threads) schedule(static) if (oracle_threads > 1)
     for (int r = 0; r < A->n_rows; ++r) {
         const int src = c->row_src[r];
         if (src >= 0) {
@@ -1327,6 +1474,8 @@ static double ba_model_change(void* user, const double* s, const double* h) {
     ba_ctx* c = (ba_ctx*)user;
     const vio_ba_problem* p = c->p;
     double mc = 0.0;
+    /* per-observation terms (in parallel when oracle_threads > 1), summed in observation order */
+#pragma omp parallel for num_threads(oracle_threads) schedule(static) if (oracle_threads > 1)
     for (int o = 0; o < c->N; ++o) {
         if (!c->obs_active[o]) continue;
         int po = c->pose_off[p->obs_kf[o]], lo = c->lm_off[p->obs_lm[o]];
@@ -1343,8 +1492,10 @@ static double ba_model_change(void* user, const double* s, const double* h) {
                 m[0] += c->Jl[6 * o + j] * hj;
                 m[1] += c->Jl[6 * o + 3 + j] * hj;
             }
-        mc -= m[0] * (c->r[2 * o] + m[0] / 2.0) + m[1] * (c->r[2 * o + 1] + m[1] / 2.0);
+        c->obs_tmp[o] = m[0] * (c->r[2 * o] + m[0] / 2.0) + m[1] * (c->r[2 * o + 1] + m[1] / 2.0);
     }
+    for (int o = 0; o < c->N; ++o)
+        if (c->obs_active[o]) mc -= c->obs_tmp[o];
     if (c->is_vi) {
         for (int k = 1; k < c->K; ++k) {
             if (!c->imu_active[k]) continue;
@@ -1463,6 +1614,8 @@ static int ba_ctx_build(ba_ctx* c, const vio_ba_problem* p) {
     c->r = (double*)calloc(2 * (size_t)(N > 0 ? N : 1), sizeof(double));
     c->Jp = (double*)calloc(12 * (size_t)(N > 0 ? N : 1), sizeof(double));
     c->Jl = (double*)calloc(6 * (size_t)(N > 0 ? N : 1), sizeof(double));
+    c->obs_tmp = (double*)calloc(N > 0 ? N : 1, sizeof(double));
+    c->obs_ok = (uint8_t*)calloc(N > 0 ? N : 1, 1);
     c->imu = (imu_ctx*)calloc(K, sizeof(imu_ctx));
     c->imu_active = (uint8_t*)calloc(K, 1);
     c->ri = (double*)calloc(9 * K, sizeof(double));
@@ -1529,6 +1682,7 @@ static void ba_ctx_free(ba_ctx* c) {
     free(c->pose_off); free(c->vel_off); free(c->lm_off); free(c->f_index); free(c->lm_ptr); free(c->lm_obs);
     free(c->col_size); free(c->col_pos); free(c->col_red); free(c->row_size); free(c->row_pos); free(c->row_cell);
     free(c->row_src); free(c->cell_col); free(c->cell_off); free(c->cell_src); free(c->values); free(c->bvec);
+    free(c->obs_tmp); free(c->obs_ok);
 }
 
 /* cost of the residual blocks whose parameters are all constant (program.cc:305-390) */

@@ -42,6 +42,8 @@
 #define M_PI 3.14159265358979323846
 #endif
 
+int oracle_get_threads(void); /* ba_oracle.c: host threads of the CPU-baseline leg (1 for every parity test) */
+
 static inline int reflect101(int p, int n) {
     if (n == 1) return 0;
     while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
@@ -53,6 +55,7 @@ static inline int reflect101(int p, int n) {
 void oracle_pyr_down(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dstride) {
     static const int wk[5] = {1, 4, 6, 4, 1};
     int dw = (sw + 1) / 2, dh = (sh + 1) / 2;
+#pragma omp parallel for num_threads(oracle_get_threads()) schedule(static) if (oracle_get_threads() > 1)
     for (int y = 0; y < dh; ++y)
         for (int x = 0; x < dw; ++x) {
             int tot = 0;
@@ -76,6 +79,7 @@ typedef struct {
 /* calcSharrDeriv: [3 10 3]^T x [-1 0 1] and transpose, BORDER_REFLECT_101 inside the image */
 static void scharr(const level_t* L, int16_t* dx, int16_t* dy) {
     int w = L->w, h = L->h;
+#pragma omp parallel for num_threads(oracle_get_threads()) schedule(static) if (oracle_get_threads() > 1)
     for (int y = 0; y < h; ++y) {
         const uint8_t* r0 = L->img + (size_t)reflect101(y - 1, h) * w;
         const uint8_t* r1 = L->img + (size_t)y * w;
@@ -253,14 +257,20 @@ int oracle_klt_track(const uint8_t* prev, const uint8_t* curr, int W, int H, int
     level_t I[16], J[16];
     int lv = build_pyramid(prev, W, H, stride, win, max_level, 1, I);
     build_pyramid(curr, W, H, stride, win, max_level, 0, J);
-    int16_t* Iw = (int16_t*)malloc(sizeof(int16_t) * win * win);
-    int16_t* dIw = (int16_t*)malloc(sizeof(int16_t) * 2 * win * win);
     for (int i = 0; i < n; ++i) { status[i] = 1; err[i] = 0.f; }
-    for (int level = lv; level >= 0; --level)
-        for (int i = 0; i < n; ++i)
-            lk_point(&I[level], &J[level], level, lv, pts + 2 * i, next + 2 * i, status + i, err + i, win, max_iters,
-                     eps2, p->min_eig_threshold, Iw, dIw);
-    free(Iw); free(dIw);
+    /* points are independent (LKTrackerInvoker is a parallel_for over them); per-thread window scratch */
+    for (int level = lv; level >= 0; --level) {
+#pragma omp parallel num_threads(oracle_get_threads()) if (oracle_get_threads() > 1)
+        {
+            int16_t* Iw = (int16_t*)malloc(sizeof(int16_t) * win * win);
+            int16_t* dIw = (int16_t*)malloc(sizeof(int16_t) * 2 * win * win);
+#pragma omp for schedule(dynamic, 4)
+            for (int i = 0; i < n; ++i)
+                lk_point(&I[level], &J[level], level, lv, pts + 2 * i, next + 2 * i, status + i, err + i, win,
+                         max_iters, eps2, p->min_eig_threshold, Iw, dIw);
+            free(Iw); free(dIw);
+        }
+    }
     free_pyramid(I, lv);
     free_pyramid(J, lv);
     return VIO_OK;
@@ -273,6 +283,7 @@ int oracle_klt_track(const uint8_t* prev, const uint8_t* curr, int W, int H, int
 void oracle_min_eig_map(const uint8_t* img, int W, int H, int stride, float* eig) {
     const float scale = (float)(1.0 / 3060.0); /* 1 / (2^(3-1) * 3 * 255) */
     float* cov = (float*)malloc(sizeof(float) * 3 * (size_t)W * H);
+#pragma omp parallel for num_threads(oracle_get_threads()) schedule(static) if (oracle_get_threads() > 1)
     for (int y = 0; y < H; ++y) {
         const uint8_t* r0 = img + (size_t)reflect101(y - 1, H) * stride;
         const uint8_t* r1 = img + (size_t)y * stride;
@@ -286,6 +297,7 @@ void oracle_min_eig_map(const uint8_t* img, int W, int H, int stride, float* eig
             c[0] = dx * dx; c[1] = dx * dy; c[2] = dy * dy;
         }
     }
+#pragma omp parallel for num_threads(oracle_get_threads()) schedule(static) if (oracle_get_threads() > 1)
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             double s0 = 0, s1 = 0, s2 = 0;
@@ -317,6 +329,7 @@ int oracle_gftt(const uint8_t* img, const uint8_t* mask, int W, int H, int strid
     float* eig = (float*)malloc(sizeof(float) * (size_t)W * H);
     oracle_min_eig_map(img, W, H, stride, eig);
     double maxv = 0.0;
+#pragma omp parallel for num_threads(oracle_get_threads()) schedule(static) reduction(max : maxv) if (oracle_get_threads() > 1)
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x)
             if (!mask || mask[(size_t)y * stride + x]) { double v = eig[(size_t)y * W + x]; if (v > maxv) maxv = v; }

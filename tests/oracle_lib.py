@@ -24,6 +24,7 @@ def load():
     L.oracle_ba_solve.argtypes = [C.c_void_p, C.c_void_p]
     vp = C.c_void_p
     L.oracle_imu_preintegrate.argtypes = [vp, C.c_int, vp, vp, C.c_int, vp, vp, vp, vp, vp, vp]
+    L.oracle_set_threads.argtypes = [C.c_int]
     _lib = L
     return L
 

@@ -348,3 +348,33 @@ def test_jacobi_scaling_ceres_kat():
     assert fc.value <= 1e-10
     per = sum(np.linalg.norm(y.reshape(N, 2)[i] - y.reshape(N, 2)[i - 1]) for i in range(N))
     assert abs(per - 10.0) <= 1e-4
+
+
+def test_threaded_baseline_legs(vio, synth):
+    """The CPU-baseline leg's threaded oracle (oracle_set_threads > 1): the tracker loops are per-pixel
+    / per-point independent, so 4 threads are bitwise the 1-thread result; the BA solve reorders its
+    sums (Schur partials per thread), so it agrees to roundoff amplification only."""
+    L = oracle_lib.load()
+    a, b, _ = synth.config1(640, 320)
+    H, W = a.shape
+    mask = np.full((H, W), 255, np.uint8)
+    kp = vio.default_klt_params()
+    try:
+        outs = []
+        for T in (1, 4):
+            L.oracle_set_threads(T)
+            pts = oracle_lib.gftt(a, mask, 200, float(np.float32(0.01)), 10.0)
+            nxt, st, err = oracle_lib.klt_track(a, b, pts, kp)
+            outs.append((pts, nxt, st, err, oracle_lib.min_eig_map(b), oracle_lib.pyr_down(b)))
+        for x, y in zip(*outs):
+            np.testing.assert_array_equal(x, y)
+        p = vio.BaProblem(synth.config3(), variant=vio.VIO_BA_VI, max_iterations=5, fixed_iterations=1)
+        res = []
+        for T in (1, 4):
+            L.oracle_set_threads(T)
+            res.append(oracle_lib.ba_solve(vio, p))
+        assert res[0]["iterations"] == res[1]["iterations"]
+        assert abs(res[0]["final_cost"] - res[1]["final_cost"]) <= 1e-9 * res[0]["final_cost"]
+        np.testing.assert_allclose(res[0]["lm_xyz"], res[1]["lm_xyz"], rtol=0, atol=1e-6)
+    finally:
+        L.oracle_set_threads(1)
