@@ -34,6 +34,7 @@ EXPORTS = [
     "vio_load_camera_timestamps", "vio_load_imu_csv", "erp_resize_area", "erp_resize_area_device",
     "erp_resize_area_kernel_ms", "erp_tracker_upload_resized",
     "vio_ba_record_bytes", "vio_ba_batch_record_bytes", "vio_ba_batch_pack", "vio_ba_record_unpack",
+    "vio_ba_gather", "vio_ba_write_back",
 ]
 
 
@@ -105,6 +106,9 @@ def lib():
     L.vio_ba_batch_record_bytes.argtypes = [vp, C.POINTER(C.c_size_t)]
     L.vio_ba_batch_pack.argtypes = [vp, vp, C.c_int]
     L.vio_ba_record_unpack.argtypes = [vp, C.POINTER(abi.VioBaOutput)]
+    L.vio_ba_gather.argtypes = [C.POINTER(abi.VioMapView), C.c_int, C.c_int, C.c_int, C.POINTER(abi.VioBaGatherOut)]
+    L.vio_ba_write_back.argtypes = [C.POINTER(abi.VioMapView), C.c_int, C.POINTER(abi.VioBaGatherOut),
+                                    C.POINTER(abi.VioBaOutput), C.POINTER(abi.VioBaMapUpdate)]
     _lib = L
     return L
 
@@ -524,3 +528,24 @@ class BaBatch:
             self.close()
         except Exception:
             pass
+
+
+def ba_gather(view, variant, fix_first=True, fix_last=False):
+    """vio_ba_gather (host): the Optimizer entry point's problem assembly on an abi.MapView.
+    Returns the abi.GatherOut (its .result() dict, its .window(view) BaProblem window)."""
+    g = abi.GatherOut(view, variant)
+    rc = lib().vio_ba_gather(C.byref(view.c), int(variant), int(bool(fix_first)), int(bool(fix_last)), C.byref(g.c))
+    if rc != 0:
+        raise VioError(f"vio_ba_gather failed ({rc})")
+    return g
+
+
+def ba_write_back(view, variant, gather, out):
+    """vio_ba_write_back (host): what the entry point writes into the graph, from the gather and the
+    solver's BaOutput (None for a gather with status > 0).  Returns the abi.MapUpdate result dict."""
+    u = abi.MapUpdate(view)
+    rc = lib().vio_ba_write_back(C.byref(view.c), int(variant), C.byref(gather.c),
+                                 C.byref(out.c) if out is not None else None, C.byref(u.c))
+    if rc != 0:
+        raise VioError(f"vio_ba_write_back failed ({rc})")
+    return u.result()

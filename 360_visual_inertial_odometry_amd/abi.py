@@ -314,3 +314,164 @@ def preint_records(out):
     res["dt_total"] = flat[:, off:off + 8].copy().view(np.float64).reshape(n)
     return res
 
+
+
+# ---------------------------------------------------------------------------------------------
+# Problem assembly / write-back on the flat Frame / Feature / MapPoint graph (vio_ba_gather,
+# vio_ba_write_back; Optimizer.cpp gather filters and write-back rules)
+VIO_GATHER_OK, VIO_GATHER_FEW_FRAMES, VIO_GATHER_NO_MAPPOINTS, VIO_GATHER_FEW_OBS = 0, 1, 2, 3
+_i64p = C.POINTER(C.c_int64)
+
+
+class VioMapView(C.Structure):
+    _fields_ = [
+        ("num_frames", C.c_int32), ("num_mappoints", C.c_int32),
+        ("frame_Twb", _f32p), ("frame_Tcb", _f32p),
+        ("feat_begin", _i32p), ("feat_uv", _f32p), ("feat_valid", _u8p), ("feat_mp", _i32p),
+        ("mp_key", _i64p), ("mp_bad", _u8p), ("mp_marg", _u8p), ("mp_pos", _f32p),
+        ("mp_obs_begin", _i32p), ("mp_obs_frame", _i32p), ("mp_obs_feat", _i32p),
+        ("width", C.c_int32), ("height", C.c_int32), ("boundary_margin", C.c_int32), ("_pad", C.c_int32),
+    ]
+
+
+class VioBaGatherOut(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32), ("num_lm", C.c_int32), ("num_obs", C.c_int32),
+        ("cap_lm", C.c_int32), ("cap_obs", C.c_int32), ("_pad", C.c_int32),
+        ("lm_mp", _i32p), ("lm_const", _u8p), ("lm_marg", _u8p), ("lm_xyz", _f64p),
+        ("obs_kf", _i32p), ("obs_lm", _i32p), ("obs_uv", _f32p), ("obs_feat", _i32p),
+        ("kf_const", _u8p), ("kf_in_problem", _u8p),
+        ("T_wb_init", C.POINTER(VioPose)), ("T_cb", C.POINTER(VioPose)),
+    ]
+
+
+class VioBaMapUpdate(C.Structure):
+    _fields_ = [
+        ("frame_Twb", _f32p), ("frame_set", _u8p), ("frame_vel", _f32p), ("bias", _f32p),
+        ("mp_pos", _f32p), ("mp_set", _u8p), ("mp_set_bad", _u8p),
+        ("success", C.c_int32), ("num_inliers", C.c_int32), ("num_outliers", C.c_int32),
+        ("num_poses_optimized", C.c_int32), ("num_points_optimized", C.c_int32), ("num_iterations", C.c_int32),
+        ("initial_cost", C.c_double), ("final_cost", C.c_double),
+    ]
+
+
+class MapView:
+    """Owns the numpy arrays of a flat graph (dict with the vio_map_view fields; frame_Twb /
+    frame_Tcb (F,4,4) float32, feat_begin (F+1,), feat_uv (G,2), feat_valid / feat_mp (G,), mp_key /
+    mp_bad / mp_marg (M,), mp_pos (M,3), optionally mp_obs_begin (M+1,) / mp_obs_frame / mp_obs_feat,
+    width, height, boundary_margin) and the vio_map_view pointing at them."""
+
+    def __init__(self, g):
+        self.F = int(len(g["feat_begin"]) - 1)
+        self.M = int(len(g["mp_key"]))
+        self.frame_Twb = np.ascontiguousarray(g["frame_Twb"], np.float32).reshape(-1)
+        self.frame_Tcb = np.ascontiguousarray(g["frame_Tcb"], np.float32).reshape(-1)
+        self.feat_begin = np.ascontiguousarray(g["feat_begin"], np.int32)
+        self.feat_uv = np.ascontiguousarray(g["feat_uv"], np.float32).reshape(-1)
+        self.feat_valid = np.ascontiguousarray(g["feat_valid"], np.uint8)
+        self.feat_mp = np.ascontiguousarray(g["feat_mp"], np.int32)
+        self.mp_key = np.ascontiguousarray(g["mp_key"], np.int64)
+        self.mp_bad = np.ascontiguousarray(g["mp_bad"], np.uint8)
+        self.mp_marg = np.ascontiguousarray(g["mp_marg"], np.uint8)
+        self.mp_pos = np.ascontiguousarray(g["mp_pos"], np.float32).reshape(-1)
+        has_obs = g.get("mp_obs_begin") is not None
+        self.mp_obs_begin = np.ascontiguousarray(g["mp_obs_begin"], np.int32) if has_obs else None
+        self.mp_obs_frame = np.ascontiguousarray(g["mp_obs_frame"], np.int32) if has_obs else None
+        self.mp_obs_feat = np.ascontiguousarray(g["mp_obs_feat"], np.int32) if has_obs else None
+        v = VioMapView()
+        v.num_frames, v.num_mappoints = self.F, self.M
+        v.frame_Twb, v.frame_Tcb = _ptr(self.frame_Twb, C.c_float), _ptr(self.frame_Tcb, C.c_float)
+        v.feat_begin, v.feat_uv = _ptr(self.feat_begin, C.c_int32), _ptr(self.feat_uv, C.c_float)
+        v.feat_valid, v.feat_mp = _ptr(self.feat_valid, C.c_uint8), _ptr(self.feat_mp, C.c_int32)
+        v.mp_key, v.mp_bad = _ptr(self.mp_key, C.c_int64), _ptr(self.mp_bad, C.c_uint8)
+        v.mp_marg, v.mp_pos = _ptr(self.mp_marg, C.c_uint8), _ptr(self.mp_pos, C.c_float)
+        v.mp_obs_begin = _ptr(self.mp_obs_begin, C.c_int32)
+        v.mp_obs_frame = _ptr(self.mp_obs_frame, C.c_int32)
+        v.mp_obs_feat = _ptr(self.mp_obs_feat, C.c_int32)
+        v.width, v.height, v.boundary_margin = int(g["width"]), int(g["height"]), int(g.get("boundary_margin", 20))
+        self.c = v
+
+    def obs_capacity(self, variant):
+        if variant == VIO_BA_LOCAL:
+            return int(self.mp_obs_begin[-1]) if self.mp_obs_begin is not None else 0
+        return int(self.feat_begin[-1])
+
+
+class GatherOut:
+    """Caller-owned buffers of one vio_ba_gather call."""
+
+    def __init__(self, view, variant):
+        F, M = view.F, view.M
+        cap_lm = M if variant != VIO_PNP else int(view.feat_begin[-1])
+        cap_obs = view.obs_capacity(variant)
+        self.lm_mp = np.zeros(max(cap_lm, 1), np.int32)
+        self.lm_const = np.zeros(max(cap_lm, 1), np.uint8)
+        self.lm_marg = np.zeros(max(cap_lm, 1), np.uint8)
+        self.lm_xyz = np.zeros(3 * max(cap_lm, 1))
+        self.obs_kf = np.zeros(max(cap_obs, 1), np.int32)
+        self.obs_lm = np.zeros(max(cap_obs, 1), np.int32)
+        self.obs_uv = np.zeros(2 * max(cap_obs, 1), np.float32)
+        self.obs_feat = np.zeros(max(cap_obs, 1), np.int32)
+        self.kf_const = np.zeros(max(F, 1), np.uint8)
+        self.kf_in_problem = np.zeros(max(F, 1), np.uint8)
+        self.T_wb_init = (VioPose * max(F, 1))()
+        self.T_cb = (VioPose * max(F, 1))()
+        o = VioBaGatherOut()
+        o.cap_lm, o.cap_obs = cap_lm, cap_obs
+        o.lm_mp, o.lm_const = _ptr(self.lm_mp, C.c_int32), _ptr(self.lm_const, C.c_uint8)
+        o.lm_marg, o.lm_xyz = _ptr(self.lm_marg, C.c_uint8), _ptr(self.lm_xyz, C.c_double)
+        o.obs_kf, o.obs_lm = _ptr(self.obs_kf, C.c_int32), _ptr(self.obs_lm, C.c_int32)
+        o.obs_uv, o.obs_feat = _ptr(self.obs_uv, C.c_float), _ptr(self.obs_feat, C.c_int32)
+        o.kf_const, o.kf_in_problem = _ptr(self.kf_const, C.c_uint8), _ptr(self.kf_in_problem, C.c_uint8)
+        o.T_wb_init = C.cast(self.T_wb_init, C.POINTER(VioPose))
+        o.T_cb = C.cast(self.T_cb, C.POINTER(VioPose))
+        self.F = F
+        self.c = o
+
+    def result(self):
+        o = self.c
+        L, N = o.num_lm, o.num_obs
+        return {"status": o.status, "lm_mp": self.lm_mp[:L].copy(), "lm_const": self.lm_const[:L].copy(),
+                "lm_marg": self.lm_marg[:L].copy(), "lm_xyz": self.lm_xyz[:3 * L].reshape(-1, 3).copy(),
+                "obs_kf": self.obs_kf[:N].copy(), "obs_lm": self.obs_lm[:N].copy(),
+                "obs_uv": self.obs_uv[:2 * N].reshape(-1, 2).copy(), "obs_feat": self.obs_feat[:N].copy(),
+                "kf_const": self.kf_const[:self.F].copy(), "kf_in_problem": self.kf_in_problem[:self.F].copy(),
+                "T_wb_init": poses_from_c(self.T_wb_init, self.F), "T_cb": poses_from_c(self.T_cb, self.F)}
+
+    def window(self, view):
+        """The gathered problem as a BaProblem window dict (cols / rows from the view)."""
+        r = self.result()
+        return {"T_wb_init": r["T_wb_init"], "T_cb": r["T_cb"], "kf_const": r["kf_const"],
+                "lm_const": r["lm_const"], "lm_marg": r["lm_marg"], "lm_xyz": r["lm_xyz"],
+                "obs_kf": r["obs_kf"], "obs_lm": r["obs_lm"], "obs_uv": r["obs_uv"],
+                "cols": float(view.c.width), "rows": float(view.c.height)}
+
+
+class MapUpdate:
+    def __init__(self, view):
+        F, M = view.F, view.M
+        self.frame_Twb = np.zeros(16 * max(F, 1), np.float32)
+        self.frame_set = np.zeros(max(F, 1), np.uint8)
+        self.frame_vel = np.zeros(3 * max(F, 1), np.float32)
+        self.bias = np.zeros(6, np.float32)
+        self.mp_pos = np.zeros(3 * max(M, 1), np.float32)
+        self.mp_set = np.zeros(max(M, 1), np.uint8)
+        self.mp_set_bad = np.zeros(max(M, 1), np.uint8)
+        u = VioBaMapUpdate()
+        u.frame_Twb, u.frame_set = _ptr(self.frame_Twb, C.c_float), _ptr(self.frame_set, C.c_uint8)
+        u.frame_vel, u.bias = _ptr(self.frame_vel, C.c_float), _ptr(self.bias, C.c_float)
+        u.mp_pos, u.mp_set = _ptr(self.mp_pos, C.c_float), _ptr(self.mp_set, C.c_uint8)
+        u.mp_set_bad = _ptr(self.mp_set_bad, C.c_uint8)
+        self.F, self.M = F, M
+        self.c = u
+
+    def result(self):
+        u = self.c
+        F, M = self.F, self.M
+        return {"frame_Twb": self.frame_Twb[:16 * F].reshape(-1, 4, 4).copy(), "frame_set": self.frame_set[:F].copy(),
+                "frame_vel": self.frame_vel[:3 * F].reshape(-1, 3).copy(), "bias": self.bias.copy(),
+                "mp_pos": self.mp_pos[:3 * M].reshape(-1, 3).copy(), "mp_set": self.mp_set[:M].copy(),
+                "mp_set_bad": self.mp_set_bad[:M].copy(),
+                "success": u.success, "num_inliers": u.num_inliers, "num_outliers": u.num_outliers,
+                "num_poses_optimized": u.num_poses_optimized, "num_points_optimized": u.num_points_optimized,
+                "num_iterations": u.num_iterations, "initial_cost": u.initial_cost, "final_cost": u.final_cost}

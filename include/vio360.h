@@ -232,6 +232,104 @@ int vio_ba_batch_pack(vio_ba_batch* b, void* dst, int on_device);
    trace are not carried: left untouched) */
 int vio_ba_record_unpack(const void* record, vio_ba_output* out);
 
+/*
+ * Problem assembly and write-back of the Optimizer entry points (SURVEY §8 a3 host half / a4) on a
+ * flat view of the reference's Frame / Feature / MapPoint graph.  Host-only, no device work.
+ *
+ * The view holds the frames vector handed to RunBA / RunVIBA / RunLocalBA (window order; for
+ * SolvePnP the one frame) and the MapPoints their features reference:
+ *   frame f's features are [feat_begin[f], feat_begin[f+1]) in Frame::GetFeatures() order; feature
+ *   g has GetPixelCoord() = feat_uv[2g..2g+1], IsValid() = feat_valid[g] (a null Feature: 0) and
+ *   GetMapPoint() = feat_mp[g] (an index into the MapPoint table, -1 for none);
+ *   MapPoint m has IsBad() = mp_bad[m], IsMarginalized() = mp_marg[m], GetPosition() = mp_pos[3m..];
+ *   mp_key[m] orders the MapPoints as the reference's std::set<shared_ptr<MapPoint>> does (pointer
+ *   order there, any unique key here, e.g. the MapPoint id); RunLocalBA also walks
+ *   MapPoint::GetObservations(): entries [mp_obs_begin[m], mp_obs_begin[m+1]) with the observing
+ *   frame's slot in this view (-1: expired weak_ptr or a frame outside the window) and the
+ *   feature index inside that frame.
+ * IsNearBoundary (Optimizer.cpp:41-46 -> Camera.cpp:134-139): margin > 0 and x < margin or
+ * x > width - margin or y < margin or y > height - margin, in f32.
+ */
+typedef struct {
+    int32_t num_frames;
+    int32_t num_mappoints;
+    const float* frame_Twb;      /* 16 per frame: Frame::GetTwb(), row-major 4x4 */
+    const float* frame_Tcb;      /* 16 per frame: Frame::GetTCB(), row-major 4x4 */
+    const int32_t* feat_begin;   /* num_frames + 1 */
+    const float* feat_uv;
+    const uint8_t* feat_valid;
+    const int32_t* feat_mp;
+    const int64_t* mp_key;
+    const uint8_t* mp_bad;
+    const uint8_t* mp_marg;
+    const float* mp_pos;
+    const int32_t* mp_obs_begin; /* num_mappoints + 1 (RunLocalBA only, else may be NULL) */
+    const int32_t* mp_obs_frame;
+    const int32_t* mp_obs_feat;
+    int32_t width, height;       /* Camera / Frame size (CameraParameters cols, rows) */
+    int32_t boundary_margin;     /* Optimizer::m_boundary_margin (20, Optimizer.cpp:33) */
+    int32_t _pad;
+} vio_map_view;
+
+/* vio_ba_gather status (> 0: the reference returns its default, unsuccessful result) */
+enum {
+    VIO_GATHER_OK = 0,
+    VIO_GATHER_FEW_FRAMES = 1,   /* frames.size() < 2 (Optimizer.cpp:307-310, 497-500, 729-732) */
+    VIO_GATHER_NO_MAPPOINTS = 2, /* mappoints.empty() (:328-331, 519-522, 757-760) */
+    VIO_GATHER_FEW_OBS = 3       /* SolvePnP: observations.size() < 6 (:127-130) */
+};
+
+/* The assembled problem, caller-owned arrays.  Capacities: landmarks <= num_mappoints; observations
+   <= feat_begin[num_frames] (RunBA / RunVIBA / SolvePnP) or mp_obs_begin[num_mappoints] (RunLocalBA). */
+typedef struct {
+    int32_t status;              /* VIO_GATHER_* */
+    int32_t num_lm, num_obs;
+    int32_t cap_lm, cap_obs;     /* in */
+    int32_t _pad;
+    int32_t* lm_mp;              /* cap_lm: landmark -> MapPoint index, std::set order */
+    uint8_t* lm_const;           /* cap_lm: SetParameterBlockConstant (RunLocalBA: marginalised) */
+    uint8_t* lm_marg;            /* cap_lm: marginalised (exempt from SetBad / PnP outliers) */
+    double* lm_xyz;              /* 3 cap_lm: GetPosition() cast to f64 */
+    int32_t* obs_kf;             /* cap_obs: frame slot */
+    int32_t* obs_lm;             /* cap_obs */
+    float* obs_uv;               /* 2 cap_obs */
+    int32_t* obs_feat;           /* cap_obs: global feature index g (AddResidualBlock order) */
+    uint8_t* kf_const;           /* num_frames */
+    uint8_t* kf_in_problem;      /* num_frames: the pose block has a residual (poses_in_problem, :848-852) */
+    vio_pose* T_wb_init;         /* num_frames (may be NULL): GetTwb().cast<double>() */
+    vio_pose* T_cb;              /* num_frames (may be NULL): GetTCB().cast<double>() */
+} vio_ba_gather_out;
+
+/* MapPoint / frame collection + residual-block filters of one entry point (variant VIO_BA_LOCAL:
+   Optimizer.cpp:726-851; VIO_BA_FULL: :303-409 with fix_first / fix_last; VIO_BA_VI: :493-636
+   (fix_first; the IMU factors, velocities and biases are the caller's direct copies); VIO_PNP:
+   :83-130, frame 0 only, every MapPoint constant).  Fills `out` and returns VIO_OK (check
+   out->status) or VIO_EINVAL. */
+int vio_ba_gather(const vio_map_view* map, int variant, int fix_first, int fix_last, vio_ba_gather_out* out);
+
+/* What the entry point writes back into the graph after the solve (caller-owned arrays; NULL
+   skipped).  Frames: SetTwb(T.matrix().cast<float>()) where frame_set; VIO_BA_VI: SetVelocity for
+   every frame, SetGyroBias / SetAccelBias (bias = gyro | accel) for every frame.  MapPoints:
+   SetBad() where mp_set_bad, SetPosition() where mp_set.  result: BAResult / PnPResult fields. */
+typedef struct {
+    float* frame_Twb;            /* 16 per frame, row-major */
+    uint8_t* frame_set;          /* num_frames */
+    float* frame_vel;            /* 3 per frame */
+    float* bias;                 /* 6 */
+    float* mp_pos;               /* 3 per MapPoint */
+    uint8_t* mp_set;             /* num_mappoints */
+    uint8_t* mp_set_bad;         /* num_mappoints */
+    int32_t success, num_inliers, num_outliers, num_poses_optimized, num_points_optimized, num_iterations;
+    double initial_cost, final_cost;
+} vio_ba_map_update;
+
+/* Write-back rules (RunBA :459-474, RunVIBA :684-712, RunLocalBA :917-954, SolvePnP :272-297): `g`
+   is the gather of the same view and variant, `res` the solver's output for the problem built from
+   it (T_wb, lm_xyz, lm_bad, summary; vel/bg/ba for VIO_BA_VI).  A gather with status > 0 writes
+   nothing and gives the reference's default result. */
+int vio_ba_write_back(const vio_map_view* map, int variant, const vio_ba_gather_out* g, const vio_ba_output* res,
+                      vio_ba_map_update* upd);
+
 /* ----------------------------------------------------------------------------------------- */
 /* ERP feature tracking                                                                       */
 

@@ -48,6 +48,16 @@ STRUCTS = {
     "erp_klt_params": ("ErpKltParams", ["win", "max_level", "epsilon", "min_eig_threshold"]),
     "erp_tracker_params": ("ErpTrackerParams", ["ransac_iters", "ransac_seed", "quality", "min_dist",
                                                 "boundary_margin", "polar_ratio"]),
+    "vio_map_view": ("VioMapView", ["num_frames", "num_mappoints", "frame_Twb", "frame_Tcb", "feat_begin", "feat_uv",
+                                    "feat_valid", "feat_mp", "mp_key", "mp_bad", "mp_marg", "mp_pos", "mp_obs_begin",
+                                    "mp_obs_frame", "mp_obs_feat", "width", "height", "boundary_margin"]),
+    "vio_ba_gather_out": ("VioBaGatherOut", ["status", "num_lm", "num_obs", "cap_lm", "cap_obs", "lm_mp", "lm_const",
+                                             "lm_marg", "lm_xyz", "obs_kf", "obs_lm", "obs_uv", "obs_feat", "kf_const",
+                                             "kf_in_problem", "T_wb_init", "T_cb"]),
+    "vio_ba_map_update": ("VioBaMapUpdate", ["frame_Twb", "frame_set", "frame_vel", "bias", "mp_pos", "mp_set",
+                                             "mp_set_bad", "success", "num_inliers", "num_outliers",
+                                             "num_poses_optimized", "num_points_optimized", "num_iterations",
+                                             "initial_cost", "final_cost"]),
 }
 
 
