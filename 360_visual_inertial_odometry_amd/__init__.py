@@ -34,7 +34,7 @@ EXPORTS = [
     "vio_load_camera_timestamps", "vio_load_imu_csv", "erp_resize_area", "erp_resize_area_device",
     "erp_resize_area_kernel_ms", "erp_tracker_upload_resized",
     "vio_ba_record_bytes", "vio_ba_batch_record_bytes", "vio_ba_batch_pack", "vio_ba_record_unpack",
-    "vio_ba_gather", "vio_ba_write_back",
+    "vio_ba_gather", "vio_ba_write_back", "vio_imu_init_solve",
 ]
 
 
@@ -109,6 +109,7 @@ def lib():
     L.vio_ba_gather.argtypes = [C.POINTER(abi.VioMapView), C.c_int, C.c_int, C.c_int, C.POINTER(abi.VioBaGatherOut)]
     L.vio_ba_write_back.argtypes = [C.POINTER(abi.VioMapView), C.c_int, C.POINTER(abi.VioBaGatherOut),
                                     C.POINTER(abi.VioBaOutput), C.POINTER(abi.VioBaMapUpdate)]
+    L.vio_imu_init_solve.argtypes = [vp, C.POINTER(abi.VioImuInitProblem), C.POINTER(abi.VioImuInitResult), C.c_int]
     _lib = L
     return L
 
@@ -153,6 +154,19 @@ class Context:
         outs = [BaOutput(p.K, p.L, p.N) for p in problems]
         O = (abi.VioBaOutput * n)(*[o.c for o in outs])
         self.check(lib().vio_ba_solve_batched(self.h, P, O, n), "vio_ba_solve_batched")
+        return [o.result() for o in outs]
+
+    # ---- IMU initialisation ----
+    def imu_init(self, problems):
+        """vio_imu_init_solve: Optimizer::OptimizeIMUInit for a list of abi.ImuInitProblem in one
+        launch (one workgroup each); returns the result dicts."""
+        n = len(problems)
+        P = (abi.VioImuInitProblem * max(n, 1))(*[p.c for p in problems])
+        outs = [abi.ImuInitResult(p.F) for p in problems]
+        R = (abi.VioImuInitResult * max(n, 1))(*[o.c for o in outs])
+        self.check(lib().vio_imu_init_solve(self.h, P, R, n), "vio_imu_init_solve")
+        for k, o in enumerate(outs):
+            o.c = R[k]
         return [o.result() for o in outs]
 
 

@@ -475,3 +475,62 @@ class MapUpdate:
                 "success": u.success, "num_inliers": u.num_inliers, "num_outliers": u.num_outliers,
                 "num_poses_optimized": u.num_poses_optimized, "num_points_optimized": u.num_points_optimized,
                 "num_iterations": u.num_iterations, "initial_cost": u.initial_cost, "final_cost": u.final_cost}
+
+
+# ---------------------------------------------------------------------------------------------
+# IMU initialisation (vio_imu_init_solve; Optimizer::OptimizeIMUInit)
+VIO_IMU_INIT_OK, VIO_IMU_INIT_FEW_FRAMES, VIO_IMU_INIT_NO_PREINT, VIO_IMU_INIT_NO_FACTORS = 0, 1, 2, 3
+
+
+class VioImuInitProblem(C.Structure):
+    _fields_ = [
+        ("num_frames", C.c_int32), ("max_iterations", C.c_int32),
+        ("T_wb", C.POINTER(VioPose)), ("preint", C.POINTER(VioPreint)), ("preint_valid", _u8p),
+        ("gravity_magnitude", C.c_double), ("huber_delta", C.c_double), ("bias_prior_weight", C.c_double),
+    ]
+
+
+class VioImuInitResult(C.Structure):
+    _fields_ = [
+        ("success", C.c_int32), ("status", C.c_int32), ("iterations", C.c_int32 * 2), ("termination", C.c_int32 * 2),
+        ("gravity", C.c_double * 3), ("Rwg", C.c_double * 9), ("gravity_dir", C.c_double * 2), ("scale", C.c_double),
+        ("gyro_bias", C.c_double * 3), ("accel_bias", C.c_double * 3), ("initial_cost", C.c_double),
+        ("final_cost", C.c_double), ("velocities", _f64p),
+    ]
+
+
+class ImuInitProblem:
+    """frames: dict with T_wb (F,4,4) and preint (list of F, entry 0 None / ignored; an entry None for
+    a frame without preintegration)."""
+
+    def __init__(self, frames, max_iterations=50, gravity_magnitude=9.81, huber_delta=4.0, bias_prior_weight=1.0):
+        self.F = int(len(frames["T_wb"]))
+        self.T_wb = poses_to_c(frames["T_wb"])
+        pre = list(frames["preint"])
+        self.preint, self.valid = preints_to_c([None] + pre[1:] if self.F else [])
+        p = VioImuInitProblem()
+        p.num_frames = self.F
+        p.max_iterations = max_iterations
+        p.T_wb = C.cast(self.T_wb, C.POINTER(VioPose))
+        p.preint = C.cast(self.preint, C.POINTER(VioPreint))
+        p.preint_valid = _ptr(self.valid, C.c_uint8)
+        p.gravity_magnitude, p.huber_delta, p.bias_prior_weight = gravity_magnitude, huber_delta, bias_prior_weight
+        self.c = p
+
+
+class ImuInitResult:
+    def __init__(self, F):
+        self.F = F
+        self.vel = np.zeros(3 * max(F, 1))
+        r = VioImuInitResult()
+        r.velocities = _ptr(self.vel, C.c_double)
+        self.c = r
+
+    def result(self):
+        r = self.c
+        return {"success": r.success, "status": r.status, "iterations": list(r.iterations),
+                "termination": list(r.termination), "gravity": np.array(r.gravity[:]),
+                "Rwg": np.array(r.Rwg[:]).reshape(3, 3), "gravity_dir": np.array(r.gravity_dir[:]),
+                "scale": r.scale, "gyro_bias": np.array(r.gyro_bias[:]), "accel_bias": np.array(r.accel_bias[:]),
+                "initial_cost": r.initial_cost, "final_cost": r.final_cost,
+                "velocities": self.vel[: 3 * self.F].reshape(-1, 3).copy()}

@@ -37,6 +37,8 @@ enum { kSlotTriIn = 11, kSlotTriOut = 12 };
 enum { kSlotResizeSrc = 13, kSlotResizeDst = 14 };
 // staging of vio_ba_batch_pack to host memory
 enum { kSlotRecords = 15 };
+// vio_imu_init_solve inputs, outputs and per-problem scratch
+enum { kSlotImuInit = 16 };
 
 #define VIO_HIP(ctx, expr)                                  \
     do {                                                    \

@@ -476,6 +476,51 @@ int vio_imu_preintegrate_device(vio_ctx* ctx, const vio_imu_data* imu, int n_imu
 int vio_imu_preintegrate_kernel_ms(vio_ctx* ctx, double* ms);
 
 /* ------------------------------------------------------------------------------------------ */
+/* IMU initialisation: Optimizer::OptimizeIMUInit (src/optimization/            */
+/* Optimizer.cpp:972-1257) — stage 1 gravity direction (2) + scale, stage 2 velocities + shared */
+/* biases with BiasPriorFactor (Factors.h:366-396), both over InertialGravityScaleFactor        */
+/* (Factors.cpp:981-1293) with HuberLoss(sqrt(16)), DENSE_QR, default Solver::Options.          */
+/* Reproduced quirks: the pose blocks are constant zero perturbations in both stages and the    */
+/* factor applies SE3d::exp to them without the keyframe poses, so every factor sees identity  */
+/* poses (Factors.cpp:1024-1042, Optimizer.cpp:1084-1092); the factor's square-root            */
+/* information is built but never applied to the residual.  One workgroup per problem.          */
+
+enum {
+    VIO_IMU_INIT_OK = 0,
+    VIO_IMU_INIT_FEW_FRAMES = 1,   /* frames.size() < 3 (:977-981) */
+    VIO_IMU_INIT_NO_PREINT = 2,    /* a frame after the first lacks its preintegration (:984-989) */
+    VIO_IMU_INIT_NO_FACTORS = 3    /* stage 1 kept no factor (0.001 <= dt <= 2.0, :1060-1086) */
+};
+
+typedef struct {
+    int32_t num_frames;          /* keyframes, 3 .. 64 */
+    int32_t max_iterations;      /* per stage: 50 (Solver::Options default) */
+    const vio_pose* T_wb;        /* num_frames: GetTwb().cast<double>() (velocity initialisation) */
+    const vio_preint* preint;    /* num_frames: entry i = frame i's preintegration from the last keyframe */
+    const uint8_t* preint_valid; /* num_frames (entry 0 ignored) */
+    double gravity_magnitude;    /* 9.81 */
+    double huber_delta;          /* sqrt(16) = 4 */
+    double bias_prior_weight;    /* 1.0 */
+} vio_imu_init_problem;
+
+typedef struct {
+    int32_t success;             /* IMUInitResult::success */
+    int32_t status;              /* VIO_IMU_INIT_* */
+    int32_t iterations[2];       /* Summary::iterations.size() of stage 1 / 2 */
+    int32_t termination[2];      /* VIO_TERM_* of stage 1 / 2 */
+    double gravity[3];           /* R_wg (0, 0, -9.81) */
+    double Rwg[9];               /* row-major */
+    double gravity_dir[2];       /* the stage-1 parameters (theta_x, theta_y) */
+    double scale;
+    double gyro_bias[3], accel_bias[3];
+    double initial_cost;         /* stage 1 Summary::initial_cost */
+    double final_cost;           /* stage 2 Summary::final_cost */
+    double* velocities;          /* caller-owned 3 * num_frames, may be NULL */
+} vio_imu_init_result;
+
+int vio_imu_init_solve(vio_ctx* ctx, const vio_imu_init_problem* probs, vio_imu_init_result* results, int n);
+
+/* ------------------------------------------------------------------------------------------ */
 /* Two-view triangulation: Estimator::TriangulateSinglePoint                   */
 /* (src/processing/Estimator.cpp:1082-1137) for n candidates in one launch.                   */
 

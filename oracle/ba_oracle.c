@@ -2122,3 +2122,416 @@ void oracle_lm_radius_schedule(double initial_radius, double max_radius, const d
         radii[i] = s.radius;
     }
 }
+
+/* ========================================================================================= */
+/* IMU initialisation: Optimizer::OptimizeIMUInit (src/optimization/Optimizer.cpp:972-1257)   */
+/* over InertialGravityScaleFactor (src/optimization/Factors.cpp:981-1293) and BiasPriorFactor */
+/* (src/optimization/Factors.h:366-396), LM + DENSE_QR with the default Solver::Options.       */
+/* ========================================================================================= */
+
+/* SO3d::Log (LieUtils.cpp:221-272) */
+static void so3d_log(const double* R, double* w) {
+    const double tr = R[0] + R[4] + R[8];
+    const double c = fmax(-1.0, fmin(1.0, (tr - 1.0) * 0.5));
+    const double th = acos(c);
+    if (th < EPS_D) { /* Veed(R - I) */
+        w[0] = R[7]; w[1] = R[2]; w[2] = R[3];
+        return;
+    }
+    const double s = sin(th);
+    if (fabs(s) < EPS_D) {
+        int mi = 0;
+        if (R[4] > R[0]) mi = 1;
+        if (R[8] > R[4 * mi]) mi = 2;
+        double ax[3];
+        ax[mi] = sqrt((R[4 * mi] + 1.0) * 0.5);
+        for (int i = 0; i < 3; ++i)
+            if (i != mi) ax[i] = R[3 * mi + i] / (2.0 * ax[mi]);
+        const double sk[3] = {(R[7] - R[5]) * 0.5, (R[2] - R[6]) * 0.5, (R[3] - R[1]) * 0.5};
+        if (ax[0] * sk[0] + ax[1] * sk[1] + ax[2] * sk[2] < 0) { ax[0] = -ax[0]; ax[1] = -ax[1]; ax[2] = -ax[2]; }
+        w[0] = ax[0] * th; w[1] = ax[1] * th; w[2] = ax[2] * th;
+        return;
+    }
+    const double f = th / (2.0 * s);
+    w[0] = f * (R[7] - R[5]); w[1] = f * (R[2] - R[6]); w[2] = f * (R[3] - R[1]);
+}
+
+/* InertialGravityScaleFactor::log_SO3 (Factors.cpp:1235-1241): SVD re-orthonormalisation, the
+   SO3d constructor's second one, SO3d::Log */
+static void igs_log_so3(const double* R, double* w) {
+    double R1[9], R2[9];
+    oracle_nearest_rotation(R, R1);
+    oracle_nearest_rotation(R1, R2);
+    so3d_log(R2, w);
+}
+
+/* InertialGravityScaleFactor::right_jacobian_SO3 (Factors.cpp:1207-1220): I - skew/2 below 1e-6 */
+static void igs_right_jac(const double* phi, double* J) {
+    double P[9];
+    hat3(phi, P);
+    const double th = norm3(phi);
+    if (th < 1e-6) {
+        for (int i = 0; i < 9; ++i) J[i] = ((i % 4 == 0) ? 1.0 : 0.0) - 0.5 * P[i];
+        return;
+    }
+    double P2[9];
+    m3_mul(P, P, P2);
+    const double c = cos(th), s = sin(th);
+    for (int i = 0; i < 9; ++i) J[i] = ((i % 4 == 0) ? 1.0 : 0.0) - P[i] * (1.0 - c) / (th * th) + P2[i] * (th - s) / (th * th * th);
+}
+
+/* Eigen's 3x3 inverse (cofactors, det along column 0) */
+static void inv3_eigen(const double* m, double* r) {
+#define M3(i, j) m[3 * (i) + (j)]
+#define COF(i, j) (M3(((i) + 1) % 3, ((j) + 1) % 3) * M3(((i) + 2) % 3, ((j) + 2) % 3) - \
+                   M3(((i) + 1) % 3, ((j) + 2) % 3) * M3(((i) + 2) % 3, ((j) + 1) % 3))
+    const double c0[3] = {COF(0, 0), COF(1, 0), COF(2, 0)};
+    const double det = c0[0] * M3(0, 0) + c0[1] * M3(1, 0) + c0[2] * M3(2, 0);
+    const double id = 1.0 / det;
+    for (int j = 0; j < 3; ++j) r[j] = c0[j] * id;
+    for (int i = 1; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) r[3 * i + j] = COF(j, i) * id;
+#undef COF
+#undef M3
+}
+
+/* gravity_dir_to_rotation (Factors.cpp:1243-1266) */
+static void igs_gdir_rot(const double* gd, double* R) {
+    const double w[3] = {gd[0], gd[1], 0.0};
+    const double d2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    const double d = sqrt(d2);
+    double W[9], W2[9];
+    hat3(w, W);
+    m3_mul(W, W, W2);
+    for (int i = 0; i < 9; ++i) {
+        const double I = (i % 4 == 0) ? 1.0 : 0.0;
+        R[i] = d < 1e-5 ? I + W[i] + 0.5 * W2[i] : I + W[i] * sin(d) / d + W2[i] * (1.0 - cos(d)) / d2;
+    }
+}
+
+typedef struct {
+    double dR[9], dV[3], dP[3], JRg[9], JVg[9], JVa[9], JPg[9], JPa[9], bg0[3], ba0[3], dt;
+    int i; /* links frame i -> i + 1 */
+} igs_factor;
+
+typedef struct {
+    int F, stage, nf, n, m;
+    igs_factor* fac;
+    double gm, huber, prior_w;
+    /* parameter values */
+    double* vel; /* 3F */
+    double bg[3], ba[3], gdir[2], scale;
+    /* stage-2 layout: offset of vel_k / bg / ba in x (first appearance), -1 if absent */
+    int* vel_off;
+    int bg_off, ba_off;
+    double* J;   /* m x n (corrected), row-major */
+    double* r;   /* m */
+    double* Js;  /* m x n scratch */
+} igs_ctx;
+
+/* InertialGravityScaleFactor::Evaluate (Factors.cpp:1015-1180) at identity poses: residual (9) and
+   the Jacobian blocks of vel_i, bg, ba, vel_j (3 cols each), gravity_dir (2), scale (1) */
+static void igs_eval_factor(const igs_ctx* c, const igs_factor* f, double* r, double* Jvi, double* Jbg, double* Jba,
+                            double* Jvj, double* Jgd, double* Jsc) {
+    const double* vi = c->vel + 3 * f->i;
+    const double* vj = c->vel + 3 * (f->i + 1);
+    const double s = c->scale, dt = f->dt;
+    double Rwg[9], g[3];
+    igs_gdir_rot(c->gdir, Rwg);
+    for (int k = 0; k < 3; ++k) g[k] = Rwg[3 * k + 2] * -c->gm;
+    double dR[9], dV[3], dP[3], dbg[3], dba[3];
+    memcpy(dR, f->dR, sizeof dR); memcpy(dV, f->dV, sizeof dV); memcpy(dP, f->dP, sizeof dP);
+    for (int k = 0; k < 3; ++k) { dbg[k] = c->bg[k] - f->bg0[k]; dba[k] = c->ba[k] - f->ba0[k]; }
+    if (norm3(dbg) > 1e-6 || norm3(dba) > 1e-6) {
+        double w[3], E[9], M[9];
+        m3_vec(f->JRg, dbg, w);
+        so3_exp(w, E);
+        m3_mul(dR, E, M);
+        memcpy(dR, M, sizeof M);
+        double a[3], b[3];
+        m3_vec(f->JVg, dbg, a); m3_vec(f->JVa, dba, b);
+        for (int k = 0; k < 3; ++k) dV[k] = dV[k] + a[k] + b[k];
+        m3_vec(f->JPg, dbg, a); m3_vec(f->JPa, dba, b);
+        for (int k = 0; k < 3; ++k) dP[k] = dP[k] + a[k] + b[k];
+    }
+    double eR[9];
+    m3_tr(dR, eR); /* delta_R^T * R_bwi * R_wbj with identity poses */
+    double er[3];
+    igs_log_so3(eR, er);
+    for (int k = 0; k < 3; ++k) {
+        r[k] = er[k];
+        r[3 + k] = (s * (vj[k] - vi[k]) - g[k] * dt) - dV[k];
+        r[6 + k] = (s * (0.0 - vi[k] * dt) - 0.5 * g[k] * dt * dt) - dP[k];
+    }
+    if (!Jvi) return;
+    /* 9x3 row-major blocks */
+    memset(Jvi, 0, 27 * sizeof(double)); memset(Jbg, 0, 27 * sizeof(double)); memset(Jba, 0, 27 * sizeof(double));
+    memset(Jvj, 0, 27 * sizeof(double)); memset(Jgd, 0, 18 * sizeof(double)); memset(Jsc, 0, 9 * sizeof(double));
+    for (int k = 0; k < 3; ++k) {
+        Jvi[3 * (3 + k) + k] = -s;
+        Jvi[3 * (6 + k) + k] = -s * dt;
+        Jvj[3 * (3 + k) + k] = s;
+    }
+    double Jr[9], Jri[9], Jb[9], t1[9], t2[9], t3[9], w[3], eRt[9];
+    igs_right_jac(er, Jr);
+    inv3_eigen(Jr, Jri);
+    m3_vec(f->JRg, dbg, w);
+    igs_right_jac(w, Jb);
+    m3_tr(eR, eRt);
+    for (int i = 0; i < 9; ++i) t1[i] = -Jri[i];
+    m3_mul(t1, eRt, t2);
+    m3_mul(t2, Jb, t3);
+    m3_mul(t3, f->JRg, t1);
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+            Jbg[3 * a + b] = t1[3 * a + b];
+            Jbg[3 * (3 + a) + b] = -f->JVg[3 * a + b];
+            Jbg[3 * (6 + a) + b] = -f->JPg[3 * a + b];
+            Jba[3 * (3 + a) + b] = -f->JVa[3 * a + b];
+            Jba[3 * (6 + a) + b] = -f->JPa[3 * a + b];
+        }
+    /* dg/dtheta = R_wg * [[0, -gm], [gm, 0], [0, 0]] */
+    for (int k = 0; k < 3; ++k) {
+        const double d0 = Rwg[3 * k + 1] * c->gm, d1 = Rwg[3 * k] * -c->gm;
+        Jgd[2 * (3 + k)] = -d0 * dt;
+        Jgd[2 * (3 + k) + 1] = -d1 * dt;
+        Jgd[2 * (6 + k)] = -0.5 * d0 * dt * dt;
+        Jgd[2 * (6 + k) + 1] = -0.5 * d1 * dt * dt;
+        Jsc[3 + k] = vj[k] - vi[k];
+        Jsc[6 + k] = 0.0 - vi[k] * dt;
+    }
+}
+
+static void igs_unpack(igs_ctx* c, const double* x) {
+    if (c->stage == 1) {
+        c->gdir[0] = x[0]; c->gdir[1] = x[1]; c->scale = x[2];
+        return;
+    }
+    for (int k = 0; k < c->F; ++k)
+        if (c->vel_off[k] >= 0) memcpy(c->vel + 3 * k, x + c->vel_off[k], 3 * sizeof(double));
+    memcpy(c->bg, x + c->bg_off, 3 * sizeof(double));
+    memcpy(c->ba, x + c->ba_off, 3 * sizeof(double));
+}
+
+static int igs_eval(void* user, const double* x, double* cost, int want_jac, double* g, double* colsq) {
+    igs_ctx* c = (igs_ctx*)user;
+    const int n = c->n;
+    igs_unpack(c, x);
+    double total = 0.0;
+    if (want_jac) memset(c->J, 0, sizeof(double) * (size_t)c->m * n);
+    for (int q = 0; q < c->nf; ++q) {
+        double r[9], B[6][27];
+        igs_eval_factor(c, &c->fac[q], r, want_jac ? B[0] : NULL, B[1], B[2], B[3], B[4], B[5]);
+        double sq = 0;
+        for (int i = 0; i < 9; ++i) sq += r[i] * r[i];
+        double rho[3];
+        oracle_huber(c->huber, sq, rho);
+        total += 0.5 * rho[0];
+        double rs, asq, sr1;
+        oracle_corrector(sq, rho, &rs, &asq, &sr1);
+        if (want_jac) {
+            /* scatter the free columns: stage 1 gdir(2), scale; stage 2 vel_i, bg, ba, vel_j */
+            double* row = c->J + (size_t)9 * q * n;
+            if (c->stage == 1) {
+                for (int i = 0; i < 9; ++i) { row[i * n] = B[4][2 * i]; row[i * n + 1] = B[4][2 * i + 1]; row[i * n + 2] = B[5][i]; }
+            } else {
+                const int offs[4] = {c->vel_off[c->fac[q].i], c->bg_off, c->ba_off, c->vel_off[c->fac[q].i + 1]};
+                for (int b = 0; b < 4; ++b)
+                    for (int i = 0; i < 9; ++i)
+                        for (int j = 0; j < 3; ++j) row[i * n + offs[b] + j] = B[b][3 * i + j];
+            }
+            /* Corrector::CorrectJacobian over the block's columns (residual_block.cc:178-189) */
+            for (int col = 0; col < n; ++col) {
+                if (asq == 0.0) {
+                    for (int i = 0; i < 9; ++i) row[i * n + col] *= sr1;
+                } else {
+                    double rtj = 0;
+                    for (int i = 0; i < 9; ++i) rtj += row[i * n + col] * r[i];
+                    for (int i = 0; i < 9; ++i) row[i * n + col] = sr1 * (row[i * n + col] - asq * r[i] * rtj);
+                }
+            }
+            for (int i = 0; i < 9; ++i) c->r[9 * q + i] = r[i] * rs;
+        }
+    }
+    if (c->stage == 2) { /* BiasPriorFactor x2 (gyro, accel), no loss */
+        for (int b = 0; b < 2; ++b) {
+            const double* v = b ? c->ba : c->bg;
+            const int off = b ? c->ba_off : c->bg_off;
+            double sq = 0, r[3];
+            for (int k = 0; k < 3; ++k) { r[k] = c->prior_w * (v[k] - 0.0); sq += r[k] * r[k]; }
+            total += 0.5 * sq;
+            if (want_jac) {
+                const int row0 = 9 * c->nf + 3 * b;
+                for (int k = 0; k < 3; ++k) {
+                    c->J[(size_t)(row0 + k) * n + off + k] = c->prior_w;
+                    c->r[row0 + k] = r[k];
+                }
+            }
+        }
+    }
+    if (want_jac) {
+        memset(g, 0, sizeof(double) * n);
+        memset(colsq, 0, sizeof(double) * n);
+        for (int i = 0; i < c->m; ++i)
+            for (int j = 0; j < n; ++j) {
+                g[j] += c->J[(size_t)i * n + j] * c->r[i];
+                colsq[j] += c->J[(size_t)i * n + j] * c->J[(size_t)i * n + j];
+            }
+    }
+    *cost = total;
+    return 1;
+}
+
+static int igs_solve(void* user, const double* s, const double* D, double* y) {
+    igs_ctx* c = (igs_ctx*)user;
+    for (int i = 0; i < c->m; ++i)
+        for (int j = 0; j < c->n; ++j) c->Js[(size_t)i * c->n + j] = c->J[(size_t)i * c->n + j] * s[j];
+    return dense_qr_lm_solve(c->m, c->n, c->Js, c->r, D, y);
+}
+
+static double igs_model(void* user, const double* s, const double* h) {
+    igs_ctx* c = (igs_ctx*)user;
+    double mc = 0;
+    for (int i = 0; i < c->m; ++i) {
+        double jh = 0;
+        for (int j = 0; j < c->n; ++j) jh += c->J[(size_t)i * c->n + j] * (s[j] * h[j]);
+        mc -= jh * (c->r[i] + jh / 2.0);
+    }
+    return mc;
+}
+
+int oracle_imu_init(const vio_imu_init_problem* p, vio_imu_init_result* out) {
+    if (!p || !out) return VIO_EINVAL;
+    double* vel_out = out->velocities;
+    memset(out, 0, sizeof *out);
+    out->velocities = vel_out;
+    out->scale = 1.0;
+    out->gravity[2] = (double)-9.81f;
+    out->Rwg[0] = out->Rwg[4] = out->Rwg[8] = 1.0;
+    const int F = p->num_frames;
+    if (F < 3) { out->status = VIO_IMU_INIT_FEW_FRAMES; return VIO_OK; }
+    if (!p->preint || !p->preint_valid || !p->T_wb) return VIO_EINVAL;
+    for (int i = 1; i < F; ++i)
+        if (!p->preint_valid[i]) { out->status = VIO_IMU_INIT_NO_PREINT; return VIO_OK; }
+    igs_ctx c;
+    memset(&c, 0, sizeof c);
+    c.F = F;
+    c.gm = p->gravity_magnitude;
+    c.huber = p->huber_delta;
+    c.prior_w = p->bias_prior_weight;
+    c.scale = 1.0;
+    c.vel = (double*)calloc(3 * (size_t)F, sizeof(double));
+    c.vel_off = (int*)malloc(sizeof(int) * F);
+    c.fac = (igs_factor*)calloc(F, sizeof(igs_factor));
+    /* velocity initialisation from the preintegration: R_wb_prev * delta_V (:1025-1036) */
+    for (int i = 1; i < F; ++i) {
+        const vio_preint* q = &p->preint[i];
+        if (q->dt_total > 0.001) {
+            double dv[3] = {q->delta_V[0], q->delta_V[1], q->delta_V[2]};
+            m3_vec(p->T_wb[i - 1].R, dv, c.vel + 3 * i);
+        }
+    }
+    /* factors i -> i+1 with 0.001 <= dt <= 2.0 (:1058-1066) */
+    for (int i = 0; i < F - 1; ++i) {
+        const vio_preint* q = &p->preint[i + 1];
+        if (q->dt_total < 0.001 || q->dt_total > 2.0) continue;
+        igs_factor* f = &c.fac[c.nf++];
+        f->i = i;
+        f->dt = q->dt_total;
+        for (int k = 0; k < 9; ++k) {
+            f->dR[k] = q->delta_R[k];
+            f->JRg[k] = q->J_Rg[k]; f->JVg[k] = q->J_Vg[k]; f->JVa[k] = q->J_Va[k];
+            f->JPg[k] = q->J_Pg[k]; f->JPa[k] = q->J_Pa[k];
+        }
+        for (int k = 0; k < 3; ++k) {
+            f->dV[k] = q->delta_V[k]; f->dP[k] = q->delta_P[k];
+            f->bg0[k] = q->gyro_bias[k]; f->ba0[k] = q->accel_bias[k];
+        }
+    }
+    if (c.nf == 0) {
+        out->status = VIO_IMU_INIT_NO_FACTORS;
+        free(c.vel); free(c.vel_off); free(c.fac);
+        return VIO_OK;
+    }
+    lm_options opt;
+    oracle_lm_default_options(&opt);
+    opt.max_iterations = p->max_iterations;
+    lm_summary* sum = (lm_summary*)malloc(sizeof(lm_summary));
+    /* stage 1: gravity_dir + scale */
+    {
+        c.stage = 1;
+        c.n = 3;
+        c.m = 9 * c.nf;
+        c.J = (double*)calloc((size_t)c.m * c.n, sizeof(double));
+        c.Js = (double*)calloc((size_t)c.m * c.n, sizeof(double));
+        c.r = (double*)calloc(c.m, sizeof(double));
+        double x[3] = {c.gdir[0], c.gdir[1], c.scale};
+        lm_problem P = {3, &c, igs_eval, igs_solve, igs_model};
+        oracle_lm_minimize(&P, &opt, x, sum);
+        igs_unpack(&c, x);
+        out->initial_cost = sum->initial_cost;
+        out->iterations[0] = sum->iterations;
+        out->termination[0] = sum->termination;
+        free(c.J); free(c.Js); free(c.r);
+    }
+    /* stage 2: velocities + biases (+ the two bias priors), in order of first appearance */
+    {
+        c.stage = 2;
+        int off = 0;
+        for (int k = 0; k < F; ++k) c.vel_off[k] = -1;
+        c.bg_off = c.ba_off = -1;
+        for (int q = 0; q < c.nf; ++q) {
+            const int i = c.fac[q].i;
+            if (c.vel_off[i] < 0) { c.vel_off[i] = off; off += 3; }
+            if (c.bg_off < 0) { c.bg_off = off; off += 3; }
+            if (c.ba_off < 0) { c.ba_off = off; off += 3; }
+            if (c.vel_off[i + 1] < 0) { c.vel_off[i + 1] = off; off += 3; }
+        }
+        c.n = off;
+        c.m = 9 * c.nf + 6;
+        c.J = (double*)calloc((size_t)c.m * c.n, sizeof(double));
+        c.Js = (double*)calloc((size_t)c.m * c.n, sizeof(double));
+        c.r = (double*)calloc(c.m, sizeof(double));
+        double* x = (double*)calloc(c.n, sizeof(double));
+        for (int k = 0; k < F; ++k)
+            if (c.vel_off[k] >= 0) memcpy(x + c.vel_off[k], c.vel + 3 * k, 3 * sizeof(double));
+        memcpy(x + c.bg_off, c.bg, 3 * sizeof(double));
+        memcpy(x + c.ba_off, c.ba, 3 * sizeof(double));
+        lm_problem P = {c.n, &c, igs_eval, igs_solve, igs_model};
+        oracle_lm_minimize(&P, &opt, x, sum);
+        igs_unpack(&c, x);
+        out->final_cost = sum->final_cost;
+        out->iterations[1] = sum->iterations;
+        out->termination[1] = sum->termination;
+        free(x); free(c.J); free(c.Js); free(c.r);
+    }
+    /* results (:1212-1238): R_wg = AngleAxisd(|w|, w/|w|) for w = (theta_x, theta_y, 0) */
+    const double om[3] = {c.gdir[0], c.gdir[1], 0.0};
+    const double ang = sqrt(om[0] * om[0] + om[1] * om[1] + om[2] * om[2]);
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (!(ang < 1e-6)) {
+        const double ax[3] = {om[0] / ang, om[1] / ang, om[2] / ang};
+        const double sn = sin(ang), cs = cos(ang);
+        const double sa[3] = {sn * ax[0], sn * ax[1], sn * ax[2]};
+        const double ca[3] = {(1.0 - cs) * ax[0], (1.0 - cs) * ax[1], (1.0 - cs) * ax[2]};
+        double t = ca[0] * ax[1];
+        R[1] = t - sa[2]; R[3] = t + sa[2];
+        t = ca[0] * ax[2];
+        R[2] = t + sa[1]; R[6] = t - sa[1];
+        t = ca[1] * ax[2];
+        R[5] = t - sa[0]; R[7] = t + sa[0];
+        R[0] = ca[0] * ax[0] + cs; R[4] = ca[1] * ax[1] + cs; R[8] = ca[2] * ax[2] + cs;
+    }
+    memcpy(out->Rwg, R, sizeof R);
+    for (int k = 0; k < 3; ++k) out->gravity[k] = R[3 * k + 2] * -9.81;
+    out->gravity_dir[0] = c.gdir[0];
+    out->gravity_dir[1] = c.gdir[1];
+    out->scale = c.scale;
+    memcpy(out->gyro_bias, c.bg, sizeof c.bg);
+    memcpy(out->accel_bias, c.ba, sizeof c.ba);
+    if (vel_out) memcpy(vel_out, c.vel, sizeof(double) * 3 * F);
+    out->success = 1;
+    out->status = VIO_IMU_INIT_OK;
+    free(sum); free(c.vel); free(c.vel_off); free(c.fac);
+    return VIO_OK;
+}

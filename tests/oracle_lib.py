@@ -119,3 +119,13 @@ def pixel_to_bearing(u, v, W, H):
     b = np.zeros(3, np.float32)
     L.oracle_pixel_to_bearing(C.c_float(u), C.c_float(v), W, H, _p(b))
     return b
+
+
+def imu_init(vio, prob):
+    """oracle_imu_init on an abi.ImuInitProblem; the same result dict as Context.imu_init."""
+    L = load()
+    out = vio.abi.ImuInitResult(prob.F)
+    rc = L.oracle_imu_init(C.byref(prob.c), C.byref(out.c))
+    if rc != 0:
+        raise RuntimeError(f"oracle_imu_init rc={rc}")
+    return out.result()
