@@ -58,6 +58,9 @@ struct GbaArgs {
     double* Yo;               // [N][18]
     double* S;                // [nfp][nfp]
     double* Linv;             // [nfp/64][64][64]
+    hipStream_t side;         // look-ahead stream of the Cholesky (nullptr: plain schedule)
+    hipEvent_t ev[2];
+    int* flags;               // [32 (2 nfp/64 + 1)] persistent triangular-solve flags, one per 128 B (+ timeout word)
 };
 
 hipError_t gba_launch_setup(const GbaArgs& A, hipStream_t s);

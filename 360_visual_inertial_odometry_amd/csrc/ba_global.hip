@@ -553,16 +553,24 @@ __global__ void __launch_bounds__(256) chol_trsm_kernel(double* S, int n, int k,
             }
 }
 
-// trailing update: A_ij -= A_ik A_jk^T for k < j <= i (lower block triangle), one tile per block
-__global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k, int nblk) {
+// trailing update: A_ij -= A_ik A_jk^T for k < j <= i (lower block triangle), one tile per block.
+// part 0: every tile; part 1: the first trailing column only (j = k+1, the next step's diagonal
+// block and panel); part 2: the rest (j >= k+2) — the look-ahead split of gba_launch_cholesky.
+__global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k, int part) {
     __shared__ double As[NB][NB + 1];
     __shared__ double Bs[NB][NB + 1];
     // blockIdx.x -> (i, j) with 0 <= jj <= ii < m, i = k+1+ii, j = k+1+jj
     const long long t = blockIdx.x;
-    int ii = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-    while ((long long)(ii + 1) * (ii + 2) / 2 <= t) ++ii;
-    while ((long long)ii * (ii + 1) / 2 > t) --ii;
-    const int jj = (int)(t - (long long)ii * (ii + 1) / 2);
+    int ii = 0, jj = 0;
+    if (part == 1) {
+        ii = (int)t;
+    } else {
+        ii = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+        while ((long long)(ii + 1) * (ii + 2) / 2 <= t) ++ii;
+        while ((long long)ii * (ii + 1) / 2 > t) --ii;
+        jj = (int)(t - (long long)ii * (ii + 1) / 2);
+        if (part == 2) { ++ii; ++jj; }  // the triangle below-right of the first trailing column
+    }
     const int i = k + 1 + ii, j = k + 1 + jj;
     const double* Aik = S + (size_t)i * NB * n + (size_t)k * NB;
     const double* Ajk = S + (size_t)j * NB * n + (size_t)k * NB;
@@ -659,6 +667,220 @@ __global__ void __launch_bounds__(256) trsv_bwd_kernel(const double* S, int n, i
     part[g][cl] = s;
     __syncthreads();
     if (g == 0 && c < k * NB) y[c] -= (part[0][cl] + part[1][cl]) + (part[2][cl] + part[3][cl]);
+}
+
+// ------------------------------------------------------------------------------------------
+// Persistent triangular solves: one workgroup per 64-row block, all blocks resident at once
+// (nblk <= 256 workgroups of 256 threads, no LDS to speak of), each block publishing its solution
+// slice through a flag.  Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, sc1 form): the
+// slice is stored with agent-scope relaxed (sc1, write-through) stores, every storing wave waits
+// vmcnt(0), a workgroup barrier, then one lane stores the flag sc1; the consumer polls the flag with
+// sc1 loads from one lane, joins a barrier and loads the slice with sc1 global loads.  Flags sit
+// one per 128-B line.  The arithmetic is the per-step kernels' above, in the same order (each row /
+// column dot reduced the same way, the updates applied in the same k order), so the results are
+// bitwise theirs; what goes is 2 x nblk launches and the idle tail of every step.
+constexpr int FLAG_STRIDE = 32;  // ints: one flag per 128-B line
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) int gint;
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __hip_atomic_load((gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool flag_wait(int* f) {
+    // bounded spin: a producer that never arrives ends the wait instead of hanging the GPU
+    for (int it = 0; it < (1 << 24); ++it) {
+        if (__hip_atomic_load((gint*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+__device__ __forceinline__ void flag_publish(int* f) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store((gint*)f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Two 64-row blocks per workgroup (TG): a hand-off per pair instead of per block; the second
+// block's dependency on the first is resolved inside the workgroup.  The diagonal inverses are
+// staged in LDS before the first wait (they are final), the off-diagonal rows of every step are
+// loaded before its wait.
+constexpr int TG = 2;
+constexpr int LIS = NB + 1;  // odd LDS row stride
+
+// forward: workgroup j owns row blocks r = TG j + rl: b_r -= L_rk y_k for k = 0 .. r-1 (k order,
+// each row dot as the four 16-column group sums ((p0 + p1) + (p2 + p3)), the backward layout),
+// y_r = Linv_rr b_r.  flags[FLAG_STRIDE k] != 0: y_k is final.  flags[FLAG_STRIDE 2 nblk]: set on a
+// timed-out wait.
+__global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* S, int n, const double* Linv,
+                                                                  double* b, double* y, int* flags) {
+    __shared__ double bs[TG * NB];
+    __shared__ double yk[NB];
+    __shared__ double part[TG][4][64];
+    __shared__ double LiS[TG][NB * LIS];
+    __shared__ int ok_s;
+    const int nblk = n / NB, r0 = TG * blockIdx.x, nl = min(TG, nblk - r0);
+    const int rw = threadIdx.x & 63, g = threadIdx.x >> 6;  // row in the block, 16-column group
+    for (int e = threadIdx.x; e < nl * NB; e += 256) bs[e] = b[r0 * NB + e];
+    for (int rl = 0; rl < nl; ++rl) {
+        const double* Li = Linv + (size_t)(r0 + rl) * NB * NB;
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = Li[threadIdx.x + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            LiS[rl][(e >> 6) * LIS + (e & 63)] = v[u];
+        }
+    }
+    if (threadIdx.x == 0) ok_s = 1;
+    __syncthreads();
+    for (int k = 0; k < r0; ++k) {
+        double v[TG][16];
+#pragma unroll
+        for (int rl = 0; rl < TG; ++rl)
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                v[rl][u] = rl < nl ? S[(size_t)((r0 + rl) * NB + rw) * n + (size_t)k * NB + g * 16 + u] : 0.0;
+        if (threadIdx.x == 0 && !flag_wait(flags + FLAG_STRIDE * k)) { ok_s = 0; flags[FLAG_STRIDE * 2 * nblk] = 1; }
+        __syncthreads();
+        if (!ok_s) return;
+        if (threadIdx.x < NB) yk[threadIdx.x] = ld_sc1(y + k * NB + threadIdx.x);
+        __syncthreads();
+#pragma unroll
+        for (int rl = 0; rl < TG; ++rl) {
+            double t = 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) t += v[rl][u] * yk[g * 16 + u];
+            part[rl][g][rw] = t;
+        }
+        __syncthreads();
+        if (g < nl) bs[g * NB + rw] -= (part[g][0][rw] + part[g][1][rw]) + (part[g][2][rw] + part[g][3][rw]);
+        __syncthreads();
+    }
+    for (int rl = 0; rl < nl; ++rl) {
+        const int r = r0 + rl;
+        // the later local blocks' rows of L_.r (final): loaded now, applied after y_r
+        double v[TG - 1][16];
+#pragma unroll
+        for (int b2 = 0; b2 < TG - 1; ++b2)
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int rb = rl + 1 + b2;
+                v[b2][u] = rb < nl ? S[(size_t)((r0 + rb) * NB + rw) * n + (size_t)r * NB + g * 16 + u] : 0.0;
+            }
+        if (threadIdx.x < NB) {
+            double t = 0.0;
+            for (int q = 0; q <= (int)threadIdx.x; ++q) t += LiS[rl][threadIdx.x * LIS + q] * bs[rl * NB + q];
+            st_sc1(y + r * NB + threadIdx.x, t);
+            yk[threadIdx.x] = t;
+            b[r * NB + threadIdx.x] = bs[rl * NB + threadIdx.x];
+        }
+        flag_publish(flags + FLAG_STRIDE * r);
+#pragma unroll
+        for (int b2 = 0; b2 < TG - 1; ++b2) {
+            double t = 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) t += v[b2][u] * yk[g * 16 + u];
+            part[b2][g][rw] = t;
+        }
+        __syncthreads();
+        for (int b2 = 0; b2 < TG - 1; ++b2) {
+            const int rb = rl + 1 + b2;
+            if (g == 0 && rb < nl)
+                bs[rb * NB + rw] -= (part[b2][0][rw] + part[b2][1][rw]) + (part[b2][2][rw] + part[b2][3][rw]);
+        }
+        __syncthreads();
+    }
+}
+
+// backward: workgroup j owns column blocks c = nblk - 1 - (TG j + cl) (the last ones first):
+// y_c -= L_kc^T x_k for k = nblk-1 .. c+1 (k order, each as the four 16-row group sums
+// ((p0 + p1) + (p2 + p3))), x_c = Linv_cc^T y_c.  flags[FLAG_STRIDE (nblk + k)] != 0: x_k is final.
+__global__ void __launch_bounds__(256) trsv_bwd_persistent_kernel(const double* S, int n, const double* Linv,
+                                                                  double* y, double* x, int* flags) {
+    __shared__ double ys[TG * NB];  // ys[cl NB + i]: column block c_hi - cl
+    __shared__ double xk[NB];
+    __shared__ double part[TG][4][64];
+    __shared__ double LiS[TG][NB * LIS];
+    __shared__ int ok_s;
+    const int nblk = n / NB, c_hi = nblk - 1 - TG * blockIdx.x, nl = min(TG, c_hi + 1);
+    const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+    for (int e = threadIdx.x; e < nl * NB; e += 256) ys[e] = y[(c_hi - e / NB) * NB + (e % NB)];
+    for (int bl = 0; bl < nl; ++bl) {
+        const double* Li = Linv + (size_t)(c_hi - bl) * NB * NB;
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = Li[threadIdx.x + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            LiS[bl][(e >> 6) * LIS + (e & 63)] = v[u];
+        }
+    }
+    if (threadIdx.x == 0) ok_s = 1;
+    __syncthreads();
+    for (int k = nblk - 1; k > c_hi; --k) {
+        double v[TG][16];
+#pragma unroll
+        for (int bl = 0; bl < TG; ++bl)
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                v[bl][u] = bl < nl ? S[(size_t)(k * NB + g * 16 + u) * n + (size_t)(c_hi - bl) * NB + cl] : 0.0;
+        if (threadIdx.x == 0 && !flag_wait(flags + FLAG_STRIDE * (nblk + k))) {
+            ok_s = 0;
+            flags[FLAG_STRIDE * 2 * nblk] = 1;
+        }
+        __syncthreads();
+        if (!ok_s) return;
+        if (threadIdx.x < NB) xk[threadIdx.x] = ld_sc1(x + k * NB + threadIdx.x);
+        __syncthreads();
+#pragma unroll
+        for (int bl = 0; bl < TG; ++bl) {
+            double t = 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) t += v[bl][u] * xk[g * 16 + u];
+            part[bl][g][cl] = t;
+        }
+        __syncthreads();
+        if (g < nl) ys[g * NB + cl] -= (part[g][0][cl] + part[g][1][cl]) + (part[g][2][cl] + part[g][3][cl]);
+        __syncthreads();
+    }
+    for (int bl = 0; bl < nl; ++bl) {
+        const int c = c_hi - bl;
+        // the rows of block c against the later local column blocks (final): loaded now
+        double v[TG - 1][16];
+#pragma unroll
+        for (int b2 = 0; b2 < TG - 1; ++b2)
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int cb = bl + 1 + b2;
+                v[b2][u] = cb < nl ? S[(size_t)(c * NB + g * 16 + u) * n + (size_t)(c_hi - cb) * NB + cl] : 0.0;
+            }
+        if (threadIdx.x < NB) {
+            double t = 0.0;
+            for (int q = threadIdx.x; q < NB; ++q) t += LiS[bl][q * LIS + threadIdx.x] * ys[bl * NB + q];
+            st_sc1(x + c * NB + threadIdx.x, t);
+            xk[threadIdx.x] = t;
+            y[c * NB + threadIdx.x] = ys[bl * NB + threadIdx.x];
+        }
+        flag_publish(flags + FLAG_STRIDE * (nblk + c));
+#pragma unroll
+        for (int b2 = 0; b2 < TG - 1; ++b2) {
+            double t = 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) t += v[b2][u] * xk[g * 16 + u];
+            part[b2][g][cl] = t;
+        }
+        __syncthreads();
+        for (int b2 = 0; b2 < TG - 1; ++b2) {
+            const int cb = bl + 1 + b2;
+            if (g == 0 && cb < nl)
+                ys[cb * NB + cl] -= (part[b2][0][cl] + part[b2][1][cl]) + (part[b2][2][cl] + part[b2][3][cl]);
+        }
+        __syncthreads();
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -823,25 +1045,66 @@ hipError_t gba_launch_step_prep(const GbaArgs& A, double radius, double* partial
     hipLaunchKernelGGL(gba_rhs_kernel, dim3((A.K + GT / 64 - 1) / (GT / 64)), dim3(GT), 0, s, A);
     return hipGetLastError();
 }
+// Blocked right-looking Cholesky with a one-step look-ahead: after the panel of step k, the first
+// trailing column (the next diagonal block and panel) is updated on the main stream, which then
+// factors block k+1 and its panel while the rest of step k's trailing update runs on a side stream;
+// the main stream joins it before the next first-column update.  Every tile sees the same updates
+// in the same k order as the plain schedule (bitwise the same factor).
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
     // > 64 KB of LDS: opt in (per call: the attribute is per device and the call is host-only)
     const hipError_t ea = hipFuncSetAttribute((const void*)chol_diag_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)CHOL_DIAG_LDS);
     if (ea != hipSuccess) return ea;
-    for (int k = 0; k < nblk; ++k) {
-        hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv, fail);
-        const int m = nblk - k - 1;
-        if (m > 0) {
-            hipLaunchKernelGGL(chol_trsm_kernel, dim3(m), dim3(256), 0, s, A.S, n, k, (const double*)A.Linv);
-            hipLaunchKernelGGL(chol_syrk_kernel, dim3((unsigned)((long long)m * (m + 1) / 2)), dim3(256), 0, s, A.S, n,
-                               k, nblk);
+    hipStream_t r = A.side;
+    hipEvent_t ev_panel = A.ev[0], ev_rest = A.ev[1];
+    if (!r || !ev_panel || !ev_rest) {  // no side stream: the plain schedule
+        for (int k = 0; k < nblk; ++k) {
+            hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv, fail);
+            const int m = nblk - k - 1;
+            if (m > 0) {
+                hipLaunchKernelGGL(chol_trsm_kernel, dim3(m), dim3(256), 0, s, A.S, n, k, (const double*)A.Linv);
+                hipLaunchKernelGGL(chol_syrk_kernel, dim3((unsigned)((long long)m * (m + 1) / 2)), dim3(256), 0, s,
+                                   A.S, n, k, 0);
+            }
         }
+        return hipGetLastError();
     }
+    hipError_t e;
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, 0, A.Linv, fail);
+    if (nblk > 1) hipLaunchKernelGGL(chol_trsm_kernel, dim3(nblk - 1), dim3(256), 0, s, A.S, n, 0, (const double*)A.Linv);
+    bool rest_pending = false;
+    for (int k = 0; k + 1 < nblk; ++k) {
+        const int m = nblk - k - 1;  // trailing block rows of step k
+        if ((e = hipEventRecord(ev_panel, s)) != hipSuccess) return e;  // panel k final
+        hipLaunchKernelGGL(chol_syrk_kernel, dim3(m), dim3(256), 0, s, A.S, n, k, 1);
+        if (m >= 2) {
+            if ((e = hipStreamWaitEvent(r, ev_panel, 0)) != hipSuccess) return e;
+            hipLaunchKernelGGL(chol_syrk_kernel, dim3((unsigned)((long long)(m - 1) * m / 2)), dim3(256), 0, r, A.S, n,
+                               k, 2);
+            if ((e = hipEventRecord(ev_rest, r)) != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k + 1, A.Linv, fail);
+        if (m - 1 > 0)
+            hipLaunchKernelGGL(chol_trsm_kernel, dim3(m - 1), dim3(256), 0, s, A.S, n, k + 1, (const double*)A.Linv);
+        rest_pending = m >= 2;
+        if (rest_pending && (e = hipStreamWaitEvent(s, ev_rest, 0)) != hipSuccess) return e;
+    }
+    (void)rest_pending;
     return hipGetLastError();
 }
 hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
+    if (A.flags && nblk >= 1 && nblk <= 256) {  // every block resident: the persistent solves
+        hipError_t e = hipMemsetAsync(A.flags, 0, sizeof(int) * FLAG_STRIDE * (2 * (size_t)nblk + 1), s);
+        if (e != hipSuccess) return e;
+        const unsigned g = (unsigned)((nblk + TG - 1) / TG);
+        hipLaunchKernelGGL(trsv_fwd_persistent_kernel, dim3(g), dim3(256), 0, s, (const double*)A.S, n,
+                           (const double*)A.Linv, A.bf, A.yv, A.flags);
+        hipLaunchKernelGGL(trsv_bwd_persistent_kernel, dim3(g), dim3(256), 0, s, (const double*)A.S, n,
+                           (const double*)A.Linv, A.yv, A.xf, A.flags);
+        return hipGetLastError();
+    }
     for (int k = 0; k < nblk; ++k) {
         int rows = n - (k + 1) * NB;
         int nb = rows > 0 ? (rows + 15) / 16 : 1;

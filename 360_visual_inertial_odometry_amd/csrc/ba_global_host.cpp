@@ -212,9 +212,21 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     uint8_t *d_outl, *d_bad;
     double* d_chi2;
     if ((rc = B.alloc(&partial, 3 * nblk_max + 3 * (size_t)K)) || (rc = B.alloc(&scal, 16)) ||
-        (rc = B.alloc(&dfail, 4)) || (rc = B.alloc(&d_outl, Ns)) || (rc = B.alloc(&d_bad, Ls)) ||
+        (rc = B.alloc(&dfail, 4)) || (rc = B.alloc(&A.flags, 32 * (2 * ((size_t)nfp / 64) + 1))) || (rc = B.alloc(&d_outl, Ns)) || (rc = B.alloc(&d_bad, Ls)) ||
         (rc = B.alloc(&d_chi2, Ns)))
         return rc;
+    // look-ahead stream + events of the Cholesky (released with the solve)
+    struct SideGuard {
+        GbaArgs* a;
+        ~SideGuard() {
+            if (a->side) (void)hipStreamDestroy(a->side);
+            for (hipEvent_t& e : a->ev)
+                if (e) (void)hipEventDestroy(e);
+        }
+    } side_guard{&A};
+    if (hipStreamCreateWithFlags(&A.side, hipStreamNonBlocking) != hipSuccess) A.side = nullptr;
+    for (hipEvent_t& e : A.ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
     GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));
     GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0.data(), sizeof(double) * 3 * L, hipMemcpyHostToDevice, st));
     GBA_CHECK(gba_launch_setup(A, st));
