@@ -34,35 +34,66 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 }
 
 // ------------------------------------------------------------------------------------------
-// pyrDown.  Block = 64x4 outputs; LDS tile of (2*64+4) x (2*4+4) source pixels.
-constexpr int PD_BX = 64, PD_BY = 4;
-constexpr int PD_TW = 2 * PD_BX + 4, PD_TH = 2 * PD_BY + 4;
+// pyrDown.  Block = 64 x 16 outputs; LDS tile of the (2*16+4) source rows, columns
+// [2 ox - 16, 2 ox + 144) (16-B aligned: interior tiles stage it with 16-B loads, border tiles
+// gather REFLECT_101 bytes); each thread makes four adjacent outputs and stores them as one word.
+constexpr int PD_BX = 64, PD_BY = 16;
+constexpr int PD_TW = 160, PD_TH = 2 * PD_BY + 4;
 
 __global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLevelPair dst) {
-    __shared__ uint8_t tile[PD_TH][PD_TW + 4];
+    __shared__ uint8_t tile[PD_TH][PD_TW];
     const int f = blockIdx.z;
     const uint8_t* s = f == 0 ? src.p0 : src.p1;
     uint8_t* d = f == 0 ? dst.p0 : dst.p1;
     const int sw = src.w, sh = src.h, sp = src.pitch;
     const int dw = dst.w, dh = dst.h, dp = dst.pitch;
     const int ox = blockIdx.x * PD_BX, oy = blockIdx.y * PD_BY;
-    const int sx0 = 2 * ox - 2, sy0 = 2 * oy - 2;
-    for (int e = threadIdx.x; e < PD_TW * PD_TH; e += 256) {
-        int ty = e / PD_TW, tx = e % PD_TW;
-        tile[ty][tx] = s[(size_t)reflect101(sy0 + ty, sh) * sp + reflect101(sx0 + tx, sw)];
+    const int cx0 = 2 * ox - 16, sy0 = 2 * oy - 2;  // tile column 0 = source x cx0
+    const bool interior = cx0 >= 0 && cx0 + PD_TW <= sp && 2 * ox + 2 * PD_BX + 2 <= sw && sy0 >= 0 &&
+                          sy0 + PD_TH <= sh;
+    if (interior) {
+        constexpr int NCH = PD_TH * (PD_TW / 16);
+        uint4 v[(NCH + 255) / 256];
+#pragma unroll
+        for (int it = 0; it < (NCH + 255) / 256; ++it) {
+            const int e = threadIdx.x + 256 * it;
+            if (e < NCH) v[it] = *reinterpret_cast<const uint4*>(s + (size_t)(sy0 + e / (PD_TW / 16)) * sp + cx0 + 16 * (e % (PD_TW / 16)));
+        }
+#pragma unroll
+        for (int it = 0; it < (NCH + 255) / 256; ++it) {
+            const int e = threadIdx.x + 256 * it;
+            if (e < NCH) *reinterpret_cast<uint4*>(&tile[e / (PD_TW / 16)][16 * (e % (PD_TW / 16))]) = v[it];
+        }
+    } else {
+        for (int e = threadIdx.x; e < PD_TH * (2 * PD_BX + 4); e += 256) {
+            const int ty = e / (2 * PD_BX + 4), tx = e % (2 * PD_BX + 4);  // source x = 2 ox - 2 + tx
+            tile[ty][tx + 14] = s[(size_t)reflect101(sy0 + ty, sh) * sp + reflect101(2 * ox - 2 + tx, sw)];
+        }
     }
     __syncthreads();
-    const int tx = threadIdx.x % PD_BX, ty = threadIdx.x / PD_BX;
-    const int x = ox + tx, y = oy + ty;
-    if (x >= dw || y >= dh) return;
-    int tot = 0;
+    const int q = threadIdx.x % (PD_BX / 4), ty = threadIdx.x / (PD_BX / 4);  // outputs 4q .. 4q+3 of row ty
+    const int y = oy + ty;
+    if (y >= dh) return;
+    uint32_t packed = 0;
 #pragma unroll
-    for (int ky = 0; ky < 5; ++ky) {
-        const uint8_t* r = &tile[2 * ty + ky][2 * tx];
-        int rs = r[0] + 4 * r[1] + 6 * r[2] + 4 * r[3] + r[4];
-        tot += (ky == 0 || ky == 4 ? 1 : (ky == 2 ? 6 : 4)) * rs;
+    for (int j = 0; j < 4; ++j) {
+        const int tx = 4 * q + j;
+        int tot = 0;
+#pragma unroll
+        for (int ky = 0; ky < 5; ++ky) {
+            const uint8_t* r = &tile[2 * ty + ky][2 * tx + 14];
+            const int rs = r[0] + 4 * r[1] + 6 * r[2] + 4 * r[3] + r[4];
+            tot += (ky == 0 || ky == 4 ? 1 : (ky == 2 ? 6 : 4)) * rs;
+        }
+        packed |= (uint32_t)((tot + 128) >> 8) << (8 * j);
     }
-    d[(size_t)y * dp + x] = (uint8_t)((tot + 128) >> 8);
+    const int x = ox + 4 * q;
+    if (x + 3 < dw && ((dp & 3) == 0)) {
+        *reinterpret_cast<uint32_t*>(d + (size_t)y * dp + x) = packed;
+    } else {
+        for (int j = 0; j < 4; ++j)
+            if (x + j < dw) d[(size_t)y * dp + x + j] = (uint8_t)(packed >> (8 * j));
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1323,6 +1354,7 @@ __global__ void __launch_bounds__(256) gftt_reset_kernel(GfArgs G, int* scal) {
     if (t == 0) {
         scal[2] = scal[3] = scal[4] = 0;             // max_ord, n_cand, n_out
         scal[6] = scal[7] = scal[8] = scal[9] = 0;   // n_top, cut[2], incomplete
+        scal[10] = scal[11] = 0;                     // lmax overflow, flatten counter
     }
     for (unsigned int i = t; i < GF_BUCKETS; i += stride) G.hist[i] = 0u;
     for (unsigned int i = t; i < G.topk_cap; i += stride) G.topk[i] = 0ull;
@@ -1354,6 +1386,352 @@ __global__ void __launch_bounds__(128) disc_mask_kernel(DiscArgs D) {
             uint32_t m = (b1 - b0 == 31) ? 0xffffffffu : (((1u << (b1 - b0 + 1)) - 1u) << b0);
             atomicOr(&D.bits[(size_t)y * D.words + wi], m);
             x = (wi + 1) << 5;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// GFTT, local-maximum path (no explicit mask).  The candidate test of pass 2 — v > thr after
+// THRESH_TOZERO and v == the 3x3 dilation — is, for v > thr, the same as v >= each of its eight
+// raw neighbours (a neighbour u <= thr is zeroed but then u < v anyway).  So the 3x3 local maxima
+// do not depend on the threshold and the mask's static part (polar rows, side margins) is known
+// up front: pass 1 keeps them per tile together with the tile's maximum over the static region,
+// concurrently with LK / RANSAC.  After the disc mask: the masked maximum is the largest tile
+// maximum of the tiles no disc touches, raised by an exact recount of the touched tiles whose
+// maximum could exceed it; candidates are the kept local maxima above the threshold outside the
+// discs.  The eigenvalue map is never materialised.
+constexpr int LM_SRC_W = 96;                     // 16-B aligned source span [ox-16, ox+80)
+constexpr int LM_CW = LM_TX + 4, LM_EW = LM_TX + 2;  // cov x [ox-2, ox+66), eig x [ox-1, ox+65)
+
+template <int TY>  // tile height: eig rows [oy-1, oy+TY+1), cov rows [oy-2, oy+TY+2), source [oy-3, oy+TY+3)
+struct LmShared {
+    static constexpr int CH = TY + 4, EH = TY + 2, SH = TY + 6;
+    uint8_t src[SH][LM_SRC_W];
+    float cov[CH][LM_CW][3];
+    float eig[EH][LM_EW];
+};
+
+__device__ __forceinline__ bool lm_static_in(const GfArgs& G, int x, int y) {
+    return y >= G.top_rows && y < G.bottom_start && x >= G.margin && x < G.W - G.margin;
+}
+__device__ __forceinline__ bool lm_disc(const GfArgs& G, int x, int y) {
+    return G.disc_bits && ((G.disc_bits[(size_t)y * G.disc_words + (x >> 5)] >> (x & 31)) & 1u);
+}
+
+// eig at the LM_EW x LM_EH positions of the tile at (ox, oy) into S.eig (the gf_eig_tile
+// arithmetic: Sobel on reflect101 neighbours, f32 products, f64 3x3 box sums in ky / kx order)
+template <int TY>
+__device__ void lm_eig_tile(const GfArgs& G, int ox, int oy, LmShared<TY>& S) {
+    constexpr int LM_CH = LmShared<TY>::CH, LM_EH = LmShared<TY>::EH, LM_SH = LmShared<TY>::SH;
+    const int W = G.W, H = G.H;
+    const bool interior = ox - 16 >= 0 && ox + 80 <= G.pitch && ox + LM_TX + 3 <= W && oy - 3 >= 0 &&
+                          oy + TY + 3 <= H;
+    if (interior) {  // 16-B loads: LM_SH rows x 6 chunks
+        constexpr int NCH = LM_SH * (LM_SRC_W / 16);
+        static_assert(NCH <= 256, "one 16-B load per thread");
+        if (threadIdx.x < NCH) {
+            const int row = threadIdx.x / (LM_SRC_W / 16), ch = threadIdx.x % (LM_SRC_W / 16);
+            const uint4 v = *reinterpret_cast<const uint4*>(G.img + (size_t)(oy - 3 + row) * G.pitch + ox - 16 + 16 * ch);
+            *reinterpret_cast<uint4*>(&S.src[row][16 * ch]) = v;
+        }
+        __syncthreads();
+    }
+    const float scale = (float)(1.0 / 3060.0);
+    for (int e = threadIdx.x; e < LM_CW * LM_CH; e += 256) {
+        const int cy = e / LM_CW, cx = e % LM_CW;
+        int sx, sy;
+        if (interior) {  // image x = ox-2+cx: source columns x-1, x, x+1 at cx+13 .. cx+15
+            const uint8_t* r0 = S.src[cy];
+            const uint8_t* r1 = S.src[cy + 1];
+            const uint8_t* r2 = S.src[cy + 2];
+            const int c0 = cx + 13, c1 = cx + 14, c2 = cx + 15;
+            sx = (r0[c2] - r0[c0]) + 2 * (r1[c2] - r1[c0]) + (r2[c2] - r2[c0]);
+            sy = (r2[c0] + 2 * r2[c1] + r2[c2]) - (r0[c0] + 2 * r0[c1] + r0[c2]);
+        } else {  // image border: reflect101 about the image, read the frame directly
+            const int X = reflect101(ox - 2 + cx, W), Y = reflect101(oy - 2 + cy, H);
+            const uint8_t* r0 = G.img + (size_t)reflect101(Y - 1, H) * G.pitch;
+            const uint8_t* r1 = G.img + (size_t)Y * G.pitch;
+            const uint8_t* r2 = G.img + (size_t)reflect101(Y + 1, H) * G.pitch;
+            const int gxm = reflect101(X - 1, W), gxp = reflect101(X + 1, W);
+            sx = (r0[gxp] - r0[gxm]) + 2 * (r1[gxp] - r1[gxm]) + (r2[gxp] - r2[gxm]);
+            sy = (r2[gxm] + 2 * r2[X] + r2[gxp]) - (r0[gxm] + 2 * r0[X] + r0[gxp]);
+        }
+        const float dx = (float)sx * scale, dy = (float)sy * scale;
+        S.cov[cy][cx][0] = dx * dx;
+        S.cov[cy][cx][1] = dx * dy;
+        S.cov[cy][cx][2] = dy * dy;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < LM_EW * LM_EH; e += 256) {
+        const int ey = e / LM_EW, ex = e % LM_EW;
+        const int X = ox - 1 + ex, Y = oy - 1 + ey;
+        if (X < 0 || Y < 0 || X >= W || Y >= H) {
+            S.eig[ey][ex] = 0.f;
+            continue;
+        }
+        double s0 = 0, s1 = 0, s2 = 0;
+        if (X >= 1 && X < W - 1 && Y >= 1 && Y < H - 1) {
+            for (int ky = 0; ky < 3; ++ky)
+                for (int kx = 0; kx < 3; ++kx) {
+                    const float* c = S.cov[ey + ky][ex + kx];
+                    s0 += c[0]; s1 += c[1]; s2 += c[2];
+                }
+        } else {
+            for (int ky = -1; ky <= 1; ++ky) {
+                const int yy = reflect101(Y + ky, H) - (oy - 2);
+                for (int kx = -1; kx <= 1; ++kx) {
+                    const int xx = reflect101(X + kx, W) - (ox - 2);
+                    const float* c = S.cov[yy][xx];
+                    s0 += c[0]; s1 += c[1]; s2 += c[2];
+                }
+            }
+        }
+        const float a = (float)s0 * 0.5f, b = (float)s1, c = (float)s2 * 0.5f;
+        S.eig[ey][ex] = (a + c) - sqrtf((a - c) * (a - c) + b * b);
+    }
+    __syncthreads();
+}
+
+// block max of an ordered-int value (every thread passes its value; thread 0 gets the result)
+__device__ __forceinline__ uint32_t lm_block_max(uint32_t m, uint32_t* red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    const uint32_t t = max(max(red[0], red[1]), max(red[2], red[3]));
+    __syncthreads();
+    return t;
+}
+
+// pass 1: per tile, the 3x3 local maxima inside the static region and the region's maximum
+__global__ void __launch_bounds__(256) gftt_lmax_kernel(GfArgs G) {
+    __shared__ LmShared<LM_TY> S;
+    __shared__ unsigned long long keys[LM_CAP];
+    __shared__ unsigned int s_cnt;
+    __shared__ uint32_t red[4];
+    const int ox = blockIdx.x * LM_TX, oy = blockIdx.y * LM_TY;
+    const int tile = blockIdx.y * G.tiles_x + blockIdx.x;
+    if (threadIdx.x == 0) s_cnt = 0;
+    lm_eig_tile<LM_TY>(G, ox, oy, S);
+    uint32_t m = 0, kmax = 0;
+    const int lane = threadIdx.x & 63;
+    for (int e = threadIdx.x; e < LM_TX * LM_TY; e += 256) {
+        const int ty = e / LM_TX, tx = e % LM_TX;
+        const int X = ox + tx, Y = oy + ty;
+        bool c = false;
+        float v = 0.f;
+        if (X < G.W && Y < G.H && lm_static_in(G, X, Y)) {
+            v = S.eig[ty + 1][tx + 1];
+            m = max(m, ord_f32(v));
+            if (v > 0.f && X >= 1 && X < G.W - 1 && Y >= 1 && Y < G.H - 1) {
+                c = true;
+                for (int ky = 0; ky < 3; ++ky)
+                    for (int kx = 0; kx < 3; ++kx) c = c && !(S.eig[ty + ky][tx + kx] > v);
+            }
+        }
+        const unsigned long long bal = __ballot(c);
+        const int cnt = __popcll(bal);
+        unsigned int base = 0;
+        if (cnt) {
+            const int leader = __ffsll((long long)bal) - 1;
+            if (lane == leader) base = atomicAdd(&s_cnt, (unsigned int)cnt);  // LDS
+            base = __shfl(base, leader, 64);
+        }
+        if (c) {
+            const unsigned int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+            if (pos < LM_CAP) keys[pos] = ((unsigned long long)__float_as_uint(v) << 32) | (unsigned int)(Y * G.W + X);
+            kmax = max(kmax, __float_as_uint(v) >> 20);  // histogram bucket of the key
+        }
+    }
+    m = lm_block_max(m, red);
+    kmax = lm_block_max(kmax, red);
+    const unsigned int n = s_cnt;
+    unsigned long long* out = G.lmax + (size_t)tile * LM_CAP;
+    for (unsigned int i = threadIdx.x; i < min(n, (unsigned int)LM_CAP); i += 256) out[i] = keys[i];
+    if (threadIdx.x == 0) {
+        G.lmax_n[tile] = n;
+        G.tile_max[tile] = m;
+        G.tile_kmax[tile] = kmax;
+    }
+}
+
+// the masked maximum, part 1: tiles no disc touches contribute their static-region maximum
+// (one wave per tile; one atomic per workgroup)
+__global__ void __launch_bounds__(256) gftt_tmax_kernel(GfArgs G) {
+    __shared__ uint32_t red[4];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tile = blockIdx.x * 4 + wid;
+    const int n_tiles = G.tiles_x * G.tiles_y;
+    uint32_t m = 0;
+    if (tile < n_tiles) {
+        const int ox = (tile % G.tiles_x) * LM_TX, oy = (tile / G.tiles_x) * LM_TY;
+        const int x0 = max(ox, G.margin), x1 = min(min(ox + LM_TX, G.W), G.W - G.margin);  // [x0, x1)
+        const int y0 = max(oy, G.top_rows), y1 = min(min(oy + LM_TY, G.H), G.bottom_start);
+        bool hit = false;
+        if (G.disc_bits && x0 < x1 && y0 < y1) {
+            const int w0 = x0 >> 5, w1 = (x1 - 1) >> 5, nw = w1 - w0 + 1;
+            for (int q = lane; q < (y1 - y0) * nw; q += 64) {
+                const int y = y0 + q / nw, w = w0 + q % nw;
+                uint32_t bits = G.disc_bits[(size_t)y * G.disc_words + w];
+                const int lo = max(x0 - 32 * w, 0), hi = min(x1 - 32 * w, 32);  // [lo, hi) inside the word
+                const uint32_t rm = (hi - lo == 32) ? 0xffffffffu : (((1u << (hi - lo)) - 1u) << lo);
+                hit |= (bits & rm) != 0u;
+            }
+        }
+        const bool dirty = __ballot(hit) != 0ull;
+        if (lane == 0) G.tile_dirty[tile] = dirty ? 1 : 0;
+        if (!dirty) m = G.tile_max[tile];
+    }
+    m = lm_block_max(m, red);
+    if (threadIdx.x == 0 && m) atomicMax(G.max_ord, m);
+}
+
+// the masked maximum, part 2: a touched tile whose static maximum exceeds the running maximum is
+// recounted exactly over static-region pixels outside the discs, in LM_TY / 8 strips of 64 x 8
+constexpr int LM_STRIP = 8;
+__global__ void __launch_bounds__(256) gftt_dirty_kernel(GfArgs G) {
+    __shared__ LmShared<LM_STRIP> S;
+    __shared__ uint32_t red[4];
+    __shared__ int s_go;
+    constexpr int NS = LM_TY / LM_STRIP;
+    const int tile = blockIdx.x / NS, strip = blockIdx.x % NS;
+    if (threadIdx.x == 0) s_go = G.tile_dirty[tile] && G.tile_max[tile] > *(volatile uint32_t*)G.max_ord;
+    __syncthreads();
+    if (!s_go) return;
+    const int ox = (tile % G.tiles_x) * LM_TX, oy = (tile / G.tiles_x) * LM_TY + strip * LM_STRIP;
+    if (oy >= G.H) return;
+    lm_eig_tile<LM_STRIP>(G, ox, oy, S);
+    uint32_t m = 0;
+    for (int e = threadIdx.x; e < LM_TX * LM_STRIP; e += 256) {
+        const int ty = e / LM_TX, tx = e % LM_TX;
+        const int X = ox + tx, Y = oy + ty;
+        if (X < G.W && Y < G.H && lm_static_in(G, X, Y) && !lm_disc(G, X, Y)) m = max(m, ord_f32(S.eig[ty + 1][tx + 1]));
+    }
+    m = lm_block_max(m, red);
+    if (threadIdx.x == 0 && m) atomicMax(G.max_ord, m);
+}
+
+__device__ __forceinline__ float lm_threshold(const GfArgs& G) {
+    const uint32_t mo = *G.max_ord;
+    double maxv = mo ? (double)unord_f32(mo) : 0.0;  // minMaxLoc over the mask, 0 when empty
+    if (maxv < 0.0) maxv = 0.0;
+    return (float)(maxv * G.quality);
+}
+__device__ __forceinline__ bool lm_survives(const GfArgs& G, unsigned long long k, float thr) {
+    const float v = __uint_as_float((unsigned int)(k >> 32));
+    const unsigned int a = (unsigned int)k;
+    return v > thr && !lm_disc(G, (int)(a % (unsigned int)G.W), (int)(a / (unsigned int)G.W));
+}
+
+// candidates = kept local maxima above the threshold outside the discs: their response histogram
+// and count (grid-stride over the tiles, one wave per tile and step)
+__global__ void __launch_bounds__(256) gftt_lm_hist_kernel(GfArgs G) {
+    __shared__ unsigned int h[GF_BUCKETS];
+    __shared__ unsigned int s_n;
+    for (int b = threadIdx.x; b < GF_BUCKETS; b += 256) h[b] = 0;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    const float thr = lm_threshold(G);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n_tiles = G.tiles_x * G.tiles_y;
+    unsigned int cnt = 0;
+    for (int tile = blockIdx.x * 4 + wid; tile < n_tiles; tile += gridDim.x * 4) {
+        const unsigned int nk = G.lmax_n[tile];
+        if (nk > LM_CAP && lane == 0) *G.lmax_over = 1;
+        const unsigned long long* keys = G.lmax + (size_t)tile * LM_CAP;
+        for (unsigned int i = lane; i < min(nk, (unsigned int)LM_CAP); i += 64) {
+            const unsigned long long k = keys[i];
+            if (lm_survives(G, k, thr)) {
+                atomicAdd(&h[(unsigned int)(k >> 52)], 1u);
+                ++cnt;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) cnt += (unsigned int)__shfl_xor((int)cnt, off, 64);
+    if (lane == 0 && cnt) atomicAdd(&s_n, cnt);
+    __syncthreads();
+    for (int b = threadIdx.x; b < GF_BUCKETS; b += 256)
+        if (h[b]) atomicAdd(&G.hist[b], h[b]);
+    if (threadIdx.x == 0 && s_n) atomicAdd(G.n_cand, s_n);
+}
+
+// the candidates at or above the cut bucket into the top-K buffer: gathered in LDS per workgroup,
+// one counter atomic per workgroup (a returning atomic per wave serialises on the one word)
+constexpr int LM_TOPK_LDS = 2048;
+__global__ void __launch_bounds__(256) gftt_lm_topk_kernel(GfArgs G) {
+    __shared__ unsigned long long buf[LM_TOPK_LDS];
+    __shared__ unsigned int s_n, s_base;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    const float thr = lm_threshold(G);
+    const unsigned int cut = (unsigned int)G.cut[0];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n_tiles = G.tiles_x * G.tiles_y;
+    for (int tile = blockIdx.x * 4 + wid; tile < n_tiles; tile += gridDim.x * 4) {
+        if (G.tile_kmax[tile] < cut) continue;  // no key of the tile reaches the cut bucket
+        const unsigned int nk = min(G.lmax_n[tile], (unsigned int)LM_CAP);
+        const unsigned long long* keys = G.lmax + (size_t)tile * LM_CAP;
+        for (unsigned int i0 = 0; i0 < nk; i0 += 64) {  // wave-uniform trip count
+            const unsigned int i = i0 + lane;
+            unsigned long long k = 0ull;
+            bool take = false;
+            if (i < nk) {
+                k = keys[i];
+                take = (unsigned int)(k >> 52) >= cut && lm_survives(G, k, thr);
+            }
+            const unsigned long long bal = __ballot(take);
+            if (!bal) continue;
+            const int leader = __ffsll((long long)bal) - 1;
+            unsigned int base = 0;
+            if (lane == leader) base = atomicAdd(&s_n, (unsigned int)__popcll(bal));  // LDS
+            base = __shfl(base, leader, 64);
+            if (take) {
+                const unsigned int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+                if (pos < LM_TOPK_LDS) {
+                    buf[pos] = k;
+                } else {  // the workgroup's buffer is full: straight to the global list
+                    const unsigned int g = atomicAdd(G.n_top, 1u);
+                    if (g < G.topk_cap) G.topk[g] = k;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned int n = min(s_n, (unsigned int)LM_TOPK_LDS);
+    if (n == 0) return;
+    if (threadIdx.x == 0) s_base = atomicAdd(G.n_top, n);
+    __syncthreads();
+    for (unsigned int i = threadIdx.x; i < n; i += 256)
+        if (s_base + i < G.topk_cap) G.topk[s_base + i] = buf[i];
+}
+
+// exact fallback of this path: every surviving candidate into the flat candidate list
+__global__ void __launch_bounds__(256) gftt_lm_flatten_kernel(GfArgs G) {
+    const float thr = lm_threshold(G);
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n_tiles = G.tiles_x * G.tiles_y;
+    for (int tile = blockIdx.x * 4 + wid; tile < n_tiles; tile += gridDim.x * 4) {
+        const unsigned int nk = min(G.lmax_n[tile], (unsigned int)LM_CAP);
+        const unsigned long long* keys = G.lmax + (size_t)tile * LM_CAP;
+        for (unsigned int i0 = 0; i0 < nk; i0 += 64) {
+            const unsigned int i = i0 + lane;
+            unsigned long long k = 0ull;
+            bool take = false;
+            if (i < nk) {
+                k = keys[i];
+                take = lm_survives(G, k, thr);
+            }
+            const unsigned long long bal = __ballot(take);
+            if (!bal) continue;
+            const int leader = __ffsll((long long)bal) - 1;
+            unsigned int base = 0;
+            if (lane == leader) base = atomicAdd(G.n_flat, (unsigned int)__popcll(bal));
+            base = __shfl(base, leader, 64);
+            if (take) {
+                const unsigned int pos = base + __popcll(bal & ((1ull << lane) - 1ull));
+                if (pos < G.cand_cap) G.cand[pos] = k;
+            }
         }
     }
 }
@@ -1418,6 +1796,35 @@ hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, h
     else
         hipLaunchKernelGGL(gftt_select_kernel<false>, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
                            (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
+    return hipGetLastError();
+}
+hipError_t launch_gftt_lmax(const GfArgs& g, hipStream_t st) {
+    hipLaunchKernelGGL(gftt_lmax_kernel, dim3(g.tiles_x, g.tiles_y), dim3(256), 0, st, g);
+    return hipGetLastError();
+}
+// after pass 1 and the disc mask: masked maximum (clean tiles, then the touched tiles that could
+// raise it), candidate histogram, cut, top-K, sort, greedy selection
+hipError_t launch_gftt_after_lmax(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {
+    const int n_tiles = g.tiles_x * g.tiles_y;
+    hipLaunchKernelGGL(gftt_tmax_kernel, dim3((n_tiles + 3) / 4), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gftt_dirty_kernel, dim3(n_tiles * (LM_TY / LM_STRIP)), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gftt_lm_hist_kernel, dim3(256), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gftt_cut_kernel, dim3(1), dim3(GC_THREADS), 0, st, g);
+    hipLaunchKernelGGL(gftt_lm_topk_kernel, dim3(256), dim3(256), 0, st, g);
+    size_t tb = sort_tmp_bytes;
+    hipError_t e =
+        hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.topk, g.topk_sorted, (int)g.topk_cap, 0, 64, st);
+    if (e != hipSuccess) return e;
+    if (g.grid_global)
+        hipLaunchKernelGGL(gftt_select_kernel<true>, dim3(1), dim3(GS_THREADS), 0, st, g,
+                           (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
+    else
+        hipLaunchKernelGGL(gftt_select_kernel<false>, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
+                           (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
+    return hipGetLastError();
+}
+hipError_t launch_gftt_flatten(const GfArgs& g, hipStream_t st) {
+    hipLaunchKernelGGL(gftt_lm_flatten_kernel, dim3(256), dim3(256), 0, st, g);
     return hipGetLastError();
 }
 // exact fallback: sort every candidate slot (unused slots hold 0 and sort to the end) and redo the

@@ -81,6 +81,13 @@ struct erp_tracker {
     unsigned long long *d_topk = nullptr, *d_topk_sorted = nullptr;
     unsigned int topk_cap = 0;
     GfArgs last_gf{};           // arguments of the last enqueued GFTT (exact fallback)
+    // local-maximum path: per-tile local maxima, counts, static-region maxima, disc flags
+    unsigned long long* d_lmax = nullptr;
+    unsigned int* d_lmax_n = nullptr;
+    uint32_t* d_tile_max = nullptr;
+    uint8_t* d_tile_dirty = nullptr;
+    uint32_t* d_tile_kmax = nullptr;
+    int tiles_x = 0, tiles_y = 0;
     hipEvent_t ev[6] = {};
     // the GFTT eigenvalue map runs on a side stream, overlapped with pyramids / LK / RANSAC
     hipStream_t side = nullptr;
@@ -143,6 +150,14 @@ int ensure_gftt(erp_tracker* t, double min_dist) {
         if ((rc = dalloc(t, &t->d_hist, sizeof(unsigned int) * GF_BUCKETS)) != VIO_OK) return rc;
         if ((rc = dalloc(t, &t->d_topk, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
         if ((rc = dalloc(t, &t->d_topk_sorted, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
+        t->tiles_x = (t->W + LM_TX - 1) / LM_TX;
+        t->tiles_y = (t->H + LM_TY - 1) / LM_TY;
+        const size_t nt = (size_t)t->tiles_x * t->tiles_y;
+        if ((rc = dalloc(t, &t->d_lmax, sizeof(unsigned long long) * LM_CAP * nt)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_lmax_n, sizeof(unsigned int) * nt)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_tile_max, sizeof(uint32_t) * nt)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_tile_dirty, nt)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_tile_kmax, sizeof(uint32_t) * nt)) != VIO_OK) return rc;
     }
     if (min_dist >= 1) {
         int cell = (int)std::lrint(min_dist);
@@ -264,12 +279,27 @@ RansacArgs ransac_args(erp_tracker* t, int n, int mode, int iters, uint32_t seed
     return r;
 }
 
-// GFTT arguments for the eigenvalue-map pass only
-GfArgs gf_map_args(const erp_tracker* t, const uint8_t* img, int pitch) {
+// the analytic mask's static part: Camera::CreatePolarMask (Camera.cpp:100-118) + the left/right
+// boundary mask (FeatureTracker.cpp:49-58)
+void gf_static_region(const erp_tracker* t, int margin, float polar, GfArgs& g) {
+    g.top_rows = (int)((float)t->H * polar);
+    g.bottom_start = (int)((float)t->H * (1.0f - polar));
+    g.margin = margin;
+}
+void gf_lmax_fields(erp_tracker* t, GfArgs& g) {
+    g.lmax = t->d_lmax; g.lmax_n = t->d_lmax_n; g.tile_max = t->d_tile_max; g.tile_dirty = t->d_tile_dirty;
+    g.tile_kmax = t->d_tile_kmax;
+    g.tiles_x = t->tiles_x; g.tiles_y = t->tiles_y;
+    g.lmax_over = t->d_scal + 10;
+    g.n_flat = (unsigned int*)(t->d_scal + 11);
+}
+// GFTT arguments of the mask-independent pass 1 (local maxima + static-region tile maxima)
+GfArgs gf_lmax_args(erp_tracker* t, const uint8_t* img, int pitch, int margin, float polar) {
     GfArgs g;
     std::memset(&g, 0, sizeof g);
     g.img = img; g.W = t->W; g.H = t->H; g.pitch = pitch;
-    g.eig = t->d_eig;
+    gf_static_region(t, margin, polar, g);
+    gf_lmax_fields(t, g);
     return g;
 }
 
@@ -282,10 +312,8 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     std::memset(&g, 0, sizeof g);
     g.img = img; g.W = t->W; g.H = t->H; g.pitch = pitch;
     g.mask = mask; g.mask_pitch = mask_pitch;
-    // Camera::CreatePolarMask (Camera.cpp:100-118) + the left/right boundary mask (FeatureTracker.cpp:49-58)
-    g.top_rows = (int)((float)t->H * polar);
-    g.bottom_start = (int)((float)t->H * (1.0f - polar));
-    g.margin = margin;
+    gf_static_region(t, margin, polar, g);
+    if (!mask) gf_lmax_fields(t, g);  // analytic mask: the local-maximum path
     g.disc_bits = discs ? t->d_disc : nullptr;
     g.disc_words = t->disc_words;
     g.quality = quality; g.min_dist = min_dist; g.max_corners = max_corners;
@@ -318,8 +346,13 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     // scalars [2] max_ord [3] n_cand [4] n_out [6] n_top [7..8] cut [9] incomplete
     t->last_gf = g;
     hipError_t e = launch_gftt_reset(g, t->d_scal, t->ctx->stream);
-    if (e == hipSuccess && !eig_ready) e = launch_gftt_eig(g, t->ctx->stream);
-    if (e == hipSuccess) e = launch_gftt(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+    if (g.lmax) {
+        if (e == hipSuccess && !eig_ready) e = launch_gftt_lmax(g, t->ctx->stream);
+        if (e == hipSuccess) e = launch_gftt_after_lmax(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+    } else {
+        if (e == hipSuccess && !eig_ready) e = launch_gftt_eig(g, t->ctx->stream);
+        if (e == hipSuccess) e = launch_gftt(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+    }
     if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt kernels");
     return VIO_OK;
 }
@@ -334,17 +367,29 @@ int upload_frame(erp_tracker* t, int slot, const uint8_t* img, int stride) {
 
 int read_corners(erp_tracker* t, float* out_xy, int* n_out) {
     int n = 0, inc = 0;
-    int sc[10];
+    int sc[12];
     VIO_HIP(t->ctx, hipMemcpyAsync(sc, t->d_scal, sizeof(sc), hipMemcpyDeviceToHost, t->ctx->stream));
     VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    if (t->last_gf.lmax && sc[10]) {  // a tile held more local maxima than its slots: the map path
+        GfArgs g = t->last_gf;
+        g.lmax = nullptr;
+        hipError_t e = launch_gftt_reset(g, t->d_scal, t->ctx->stream);
+        if (e == hipSuccess) e = launch_gftt_eig(g, t->ctx->stream);
+        if (e == hipSuccess) e = launch_gftt(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt map path");
+        t->last_gf = g;
+        VIO_HIP(t->ctx, hipMemcpyAsync(sc, t->d_scal, sizeof(sc), hipMemcpyDeviceToHost, t->ctx->stream));
+        VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    }
     if ((unsigned int)sc[3] > t->cand_cap) {  // NMS survivors beyond the candidate buffer: the corner set
         set_error(t->ctx, "GFTT candidate buffer overflow");  // would differ from goodFeaturesToTrack
         return VIO_ENOSYS;
     }
     inc = sc[9];
     if (inc) {  // the top-K subset did not decide: exact pass over every candidate
-        hipError_t e = launch_gftt_full(t->last_gf, (unsigned int)sc[3], t->d_sort_tmp, t->sort_tmp_bytes,
-                                        t->ctx->stream);
+        hipError_t e = t->last_gf.lmax ? launch_gftt_flatten(t->last_gf, t->ctx->stream) : hipSuccess;
+        if (e == hipSuccess)
+            e = launch_gftt_full(t->last_gf, (unsigned int)sc[3], t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt exact fallback");
         VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal + 9, 0, sizeof(int), t->ctx->stream));
     }
@@ -463,8 +508,8 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         hipError_t e = launch_ransac_raw(p->ransac_seed, t->d_raw, t->side);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac_raw_kernel");
         VIO_HIP(t->ctx, hipEventRecord(t->raw_done, t->side));
-        e = launch_gftt_eig(gf_map_args(t, t->lvl[1][0], t->lp[0]), t->side);
-        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_eig_kernel");
+        e = launch_gftt_lmax(gf_lmax_args(t, t->lvl[1][0], t->lp[0], p->boundary_margin, p->polar_ratio), t->side);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_lmax_kernel");
     }
     VIO_HIP(t->ctx, hipEventRecord(t->join, t->side));
     if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK

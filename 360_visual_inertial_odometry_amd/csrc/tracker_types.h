@@ -83,7 +83,21 @@ struct GfArgs {
     int* cut;                       // device scalar: [0] cut bucket [1] everything selected
     unsigned int topk_cap, topk_target;
     int* incomplete;                // device scalar
+    // local-maximum path (analytic mask: polar rows / side margins / discs; no explicit mask):
+    // pass 1 (mask independent, side stream) keeps per LM_TX x LM_TY tile the 3x3 local maxima of
+    // the eigenvalue map inside the static region (fixed slots of LM_CAP keys) and the tile's
+    // maximum over that region; the map itself is never written
+    unsigned long long* lmax;       // [n_tiles][LM_CAP]
+    unsigned int* lmax_n;           // [n_tiles] local maxima of the tile (> LM_CAP: overflow)
+    uint32_t* tile_max;             // [n_tiles] ordered-int max over the tile's static region (0: none)
+    uint8_t* tile_dirty;            // [n_tiles] a disc covers part of the tile's static region
+    uint32_t* tile_kmax;            // [n_tiles] histogram bucket of the tile's strongest local maximum
+    int tiles_x, tiles_y;
+    int* lmax_over;                 // device scalar: some tile overflowed its slots
+    unsigned int* n_flat;           // device scalar: fill counter of the flattened candidate list
 };
+
+constexpr int LM_TX = 64, LM_TY = 32, LM_CAP = 1024;
 
 constexpr int GF_BUCKETS = 2048;    // float bits >> 20 of a positive response
 
@@ -111,6 +125,11 @@ hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, h
 hipError_t launch_gftt_full(const GfArgs& g, unsigned int count, void* sort_tmp, size_t sort_tmp_bytes,
                             hipStream_t st);  // sorts the first `count` candidates (n_cand read back)
 hipError_t launch_gftt_reset(const GfArgs& g, int* scal, hipStream_t st);
+// local-maximum path: pass 1 (mask independent) and everything after the mask is known
+hipError_t launch_gftt_lmax(const GfArgs& g, hipStream_t st);
+hipError_t launch_gftt_after_lmax(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st);
+// exact fallback of the local-maximum path: flatten the surviving candidates, then launch_gftt_full
+hipError_t launch_gftt_flatten(const GfArgs& g, hipStream_t st);
 size_t gftt_sort_tmp_bytes(unsigned int cap);
 hipError_t gftt_select_set_lds(size_t bytes);
 
