@@ -34,10 +34,10 @@ __device__ __forceinline__ int reflect101(int p, int n) {
 }
 
 // ------------------------------------------------------------------------------------------
-// pyrDown.  Block = 64 x 16 outputs; LDS tile of the (2*16+4) source rows, columns
-// [2 ox - 16, 2 ox + 144) (16-B aligned: interior tiles stage it with 16-B loads, border tiles
-// gather REFLECT_101 bytes); each thread makes four adjacent outputs and stores them as one word.
-constexpr int PD_BX = 64, PD_BY = 16;
+// pyrDown.  Block = 64 x 8 outputs; LDS tile of the (2*8+4) REFLECT_101 source rows, columns
+// [2 ox - 16, 2 ox + 144), staged with one 16-B load per thread (the few reflected columns at the
+// left / right image edge are patched bytewise); each thread makes two adjacent outputs.
+constexpr int PD_BX = 64, PD_BY = 8;
 constexpr int PD_TW = 160, PD_TH = 2 * PD_BY + 4;
 
 __global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLevelPair dst) {
@@ -49,35 +49,39 @@ __global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLeve
     const int dw = dst.w, dh = dst.h, dp = dst.pitch;
     const int ox = blockIdx.x * PD_BX, oy = blockIdx.y * PD_BY;
     const int cx0 = 2 * ox - 16, sy0 = 2 * oy - 2;  // tile column 0 = source x cx0
-    const bool interior = cx0 >= 0 && cx0 + PD_TW <= sp && 2 * ox + 2 * PD_BX + 2 <= sw && sy0 >= 0 &&
-                          sy0 + PD_TH <= sh;
-    if (interior) {
+    {  // 16-B chunks of the REFLECT_101 rows; chunks beyond the pitch are skipped
         constexpr int NCH = PD_TH * (PD_TW / 16);
         uint4 v[(NCH + 255) / 256];
 #pragma unroll
         for (int it = 0; it < (NCH + 255) / 256; ++it) {
             const int e = threadIdx.x + 256 * it;
-            if (e < NCH) v[it] = *reinterpret_cast<const uint4*>(s + (size_t)(sy0 + e / (PD_TW / 16)) * sp + cx0 + 16 * (e % (PD_TW / 16)));
+            const int x0 = cx0 + 16 * (e % (PD_TW / 16));
+            if (e < NCH && x0 >= 0 && x0 + 16 <= sp)
+                v[it] = *reinterpret_cast<const uint4*>(s + (size_t)reflect101(sy0 + e / (PD_TW / 16), sh) * sp + x0);
         }
 #pragma unroll
         for (int it = 0; it < (NCH + 255) / 256; ++it) {
             const int e = threadIdx.x + 256 * it;
-            if (e < NCH) *reinterpret_cast<uint4*>(&tile[e / (PD_TW / 16)][16 * (e % (PD_TW / 16))]) = v[it];
+            const int x0 = cx0 + 16 * (e % (PD_TW / 16));
+            if (e < NCH && x0 >= 0 && x0 + 16 <= sp)
+                *reinterpret_cast<uint4*>(&tile[e / (PD_TW / 16)][16 * (e % (PD_TW / 16))]) = v[it];
         }
-    } else {
+    }
+    if (2 * ox - 2 < 0 || 2 * ox + 2 * PD_BX + 2 > sw) {  // left / right image edge: reflected columns
+        __syncthreads();
         for (int e = threadIdx.x; e < PD_TH * (2 * PD_BX + 4); e += 256) {
-            const int ty = e / (2 * PD_BX + 4), tx = e % (2 * PD_BX + 4);  // source x = 2 ox - 2 + tx
-            tile[ty][tx + 14] = s[(size_t)reflect101(sy0 + ty, sh) * sp + reflect101(2 * ox - 2 + tx, sw)];
+            const int ty = e / (2 * PD_BX + 4), x = 2 * ox - 2 + e % (2 * PD_BX + 4);
+            if (x < 0 || x >= sw) tile[ty][x - cx0] = s[(size_t)reflect101(sy0 + ty, sh) * sp + reflect101(x, sw)];
         }
     }
     __syncthreads();
-    const int q = threadIdx.x % (PD_BX / 4), ty = threadIdx.x / (PD_BX / 4);  // outputs 4q .. 4q+3 of row ty
+    const int q = threadIdx.x % (PD_BX / 2), ty = threadIdx.x / (PD_BX / 2);  // outputs 2q, 2q+1 of row ty
     const int y = oy + ty;
     if (y >= dh) return;
     uint32_t packed = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int tx = 4 * q + j;
+    for (int j = 0; j < 2; ++j) {
+        const int tx = 2 * q + j;
         int tot = 0;
 #pragma unroll
         for (int ky = 0; ky < 5; ++ky) {
@@ -87,11 +91,11 @@ __global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLeve
         }
         packed |= (uint32_t)((tot + 128) >> 8) << (8 * j);
     }
-    const int x = ox + 4 * q;
-    if (x + 3 < dw && ((dp & 3) == 0)) {
-        *reinterpret_cast<uint32_t*>(d + (size_t)y * dp + x) = packed;
+    const int x = ox + 2 * q;
+    if (x + 1 < dw && ((dp & 1) == 0)) {
+        *reinterpret_cast<uint16_t*>(d + (size_t)y * dp + x) = (uint16_t)packed;
     } else {
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 2; ++j)
             if (x + j < dw) d[(size_t)y * dp + x + j] = (uint8_t)(packed >> (8 * j));
     }
 }
@@ -1424,38 +1428,35 @@ template <int TY>
 __device__ void lm_eig_tile(const GfArgs& G, int ox, int oy, LmShared<TY>& S) {
     constexpr int LM_CH = LmShared<TY>::CH, LM_EH = LmShared<TY>::EH, LM_SH = LmShared<TY>::SH;
     const int W = G.W, H = G.H;
-    const bool interior = ox - 16 >= 0 && ox + 80 <= G.pitch && ox + LM_TX + 3 <= W && oy - 3 >= 0 &&
-                          oy + TY + 3 <= H;
-    if (interior) {  // 16-B loads: LM_SH rows x 6 chunks
+    {  // 16-B chunks of the REFLECT_101 source rows (chunks beyond the pitch skipped), then the
+       // columns outside the image patched with their reflected pixels
         constexpr int NCH = LM_SH * (LM_SRC_W / 16);
         static_assert(NCH <= 256, "one 16-B load per thread");
-        if (threadIdx.x < NCH) {
-            const int row = threadIdx.x / (LM_SRC_W / 16), ch = threadIdx.x % (LM_SRC_W / 16);
-            const uint4 v = *reinterpret_cast<const uint4*>(G.img + (size_t)(oy - 3 + row) * G.pitch + ox - 16 + 16 * ch);
-            *reinterpret_cast<uint4*>(&S.src[row][16 * ch]) = v;
+        const int x0 = ox - 16 + 16 * (threadIdx.x % (LM_SRC_W / 16));
+        const bool ld = threadIdx.x < NCH && x0 >= 0 && x0 + 16 <= G.pitch;
+        uint4 v;
+        if (ld) v = *reinterpret_cast<const uint4*>(G.img + (size_t)reflect101(oy - 3 + threadIdx.x / (LM_SRC_W / 16), H) * G.pitch + x0);
+        if (ld) *reinterpret_cast<uint4*>(&S.src[threadIdx.x / (LM_SRC_W / 16)][16 * (threadIdx.x % (LM_SRC_W / 16))]) = v;
+        if (ox - 3 < 0 || ox + LM_TX + 3 > W) {
+            __syncthreads();
+            for (int e = threadIdx.x; e < LM_SH * (LM_TX + 6); e += 256) {
+                const int r = e / (LM_TX + 6), x = ox - 3 + e % (LM_TX + 6);
+                if (x < 0 || x >= W) S.src[r][x - (ox - 16)] = G.img[(size_t)reflect101(oy - 3 + r, H) * G.pitch + reflect101(x, W)];
+            }
         }
         __syncthreads();
     }
     const float scale = (float)(1.0 / 3060.0);
     for (int e = threadIdx.x; e < LM_CW * LM_CH; e += 256) {
+        // image x = ox-2+cx: source columns x-1, x, x+1 at cx+13 .. cx+15 (REFLECT_101 pixels; cov
+        // positions outside the image are never read: the box below reflects its positions)
         const int cy = e / LM_CW, cx = e % LM_CW;
-        int sx, sy;
-        if (interior) {  // image x = ox-2+cx: source columns x-1, x, x+1 at cx+13 .. cx+15
-            const uint8_t* r0 = S.src[cy];
-            const uint8_t* r1 = S.src[cy + 1];
-            const uint8_t* r2 = S.src[cy + 2];
-            const int c0 = cx + 13, c1 = cx + 14, c2 = cx + 15;
-            sx = (r0[c2] - r0[c0]) + 2 * (r1[c2] - r1[c0]) + (r2[c2] - r2[c0]);
-            sy = (r2[c0] + 2 * r2[c1] + r2[c2]) - (r0[c0] + 2 * r0[c1] + r0[c2]);
-        } else {  // image border: reflect101 about the image, read the frame directly
-            const int X = reflect101(ox - 2 + cx, W), Y = reflect101(oy - 2 + cy, H);
-            const uint8_t* r0 = G.img + (size_t)reflect101(Y - 1, H) * G.pitch;
-            const uint8_t* r1 = G.img + (size_t)Y * G.pitch;
-            const uint8_t* r2 = G.img + (size_t)reflect101(Y + 1, H) * G.pitch;
-            const int gxm = reflect101(X - 1, W), gxp = reflect101(X + 1, W);
-            sx = (r0[gxp] - r0[gxm]) + 2 * (r1[gxp] - r1[gxm]) + (r2[gxp] - r2[gxm]);
-            sy = (r2[gxm] + 2 * r2[X] + r2[gxp]) - (r0[gxm] + 2 * r0[X] + r0[gxp]);
-        }
+        const uint8_t* r0 = S.src[cy];
+        const uint8_t* r1 = S.src[cy + 1];
+        const uint8_t* r2 = S.src[cy + 2];
+        const int c0 = cx + 13, c1 = cx + 14, c2 = cx + 15;
+        const int sx = (r0[c2] - r0[c0]) + 2 * (r1[c2] - r1[c0]) + (r2[c2] - r2[c0]);
+        const int sy = (r2[c0] + 2 * r2[c1] + r2[c2]) - (r0[c0] + 2 * r0[c1] + r0[c2]);
         const float dx = (float)sx * scale, dy = (float)sy * scale;
         S.cov[cy][cx][0] = dx * dx;
         S.cov[cy][cx][1] = dx * dy;

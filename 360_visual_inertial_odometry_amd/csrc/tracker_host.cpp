@@ -504,15 +504,19 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
     // the eigenvalue map of the current frame does not depend on tracking: side stream
     VIO_HIP(t->ctx, hipEventRecord(t->fork, st));
     VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->fork, 0));
-    {  // the RANSAC draws' raw stream depends on the seed only; then the eigenvalue map
+    {  // the RANSAC draws' raw stream depends on the seed only
         hipError_t e = launch_ransac_raw(p->ransac_seed, t->d_raw, t->side);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac_raw_kernel");
         VIO_HIP(t->ctx, hipEventRecord(t->raw_done, t->side));
-        e = launch_gftt_lmax(gf_lmax_args(t, t->lvl[1][0], t->lp[0], p->boundary_margin, p->polar_ratio), t->side);
+    }
+    if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK
+    {  // GFTT pass 1 shares the chip with the latency-bound LK / RANSAC, not with the pyramids
+        VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->ev[1], 0));
+        hipError_t e =
+            launch_gftt_lmax(gf_lmax_args(t, t->lvl[1][0], t->lp[0], p->boundary_margin, p->polar_ratio), t->side);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_lmax_kernel");
     }
     VIO_HIP(t->ctx, hipEventRecord(t->join, t->side));
-    if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK
     VIO_HIP(t->ctx, hipEventRecord(t->ev[2], st));
     RansacArgs r = ransac_args(t, n, 1, p->ransac_iters, p->ransac_seed, p->ransac_thresh_rad, p->polar_ratio,
                                p->boundary_margin, t->d_pts, t->d_next);
