@@ -35,6 +35,8 @@ EXPORTS = [
     "erp_resize_area_kernel_ms", "erp_tracker_upload_resized",
     "vio_ba_record_bytes", "vio_ba_batch_record_bytes", "vio_ba_batch_pack", "vio_ba_record_unpack",
     "vio_ba_gather", "vio_ba_write_back", "vio_imu_init_solve",
+    "vio_mono_init_solve", "vio_mono_init_kernel_ms", "vio_mono_init_samples", "vio_init_select_features",
+    "vio_init_parallax", "vio_init_compose",
 ]
 
 
@@ -110,6 +112,14 @@ def lib():
     L.vio_ba_write_back.argtypes = [C.POINTER(abi.VioMapView), C.c_int, C.POINTER(abi.VioBaGatherOut),
                                     C.POINTER(abi.VioBaOutput), C.POINTER(abi.VioBaMapUpdate)]
     L.vio_imu_init_solve.argtypes = [vp, C.POINTER(abi.VioImuInitProblem), C.POINTER(abi.VioImuInitResult), C.c_int]
+    L.vio_mono_init_solve.argtypes = [vp, vp, vp, C.c_int, vp, C.POINTER(abi.VioMonoInitParams),
+                                      C.POINTER(abi.VioMonoInitResult), vp, vp]
+    L.vio_mono_init_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    L.vio_mono_init_samples.argtypes = [C.c_uint32, C.c_int, C.c_int, vp]
+    L.vio_init_select_features.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           vp, C.POINTER(C.c_int)]
+    L.vio_init_parallax.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.POINTER(C.c_float)]
+    L.vio_init_compose.argtypes = [vp, vp, vp, vp, vp, vp, C.c_int]
     _lib = L
     return L
 
@@ -169,6 +179,28 @@ class Context:
             o.c = R[k]
         return [o.result() for o in outs]
 
+
+    # ---- monocular initialisation ----
+    def mono_init(self, bearings1, bearings2, samples, params=None):
+        """vio_mono_init_solve: Initializer::TryMonocularInitialization's numeric core on device.
+        bearings1/2 (n,3) f32 unit bearings, samples (iters,8) int32 (mono_init_samples).  Returns
+        (result dict, inlier mask (n,) u8, points (n,3) f32 in camera-1 coordinates, scaled)."""
+        b1 = np.ascontiguousarray(bearings1, np.float32).reshape(-1, 3)
+        b2 = np.ascontiguousarray(bearings2, np.float32).reshape(-1, 3)
+        n = len(b1)
+        S = np.ascontiguousarray(samples, np.int32).reshape(-1, 8)
+        P = params if params is not None else abi.mono_init_params(ransac_iterations=len(S))
+        R = abi.VioMonoInitResult()
+        M = np.zeros(max(n, 1), np.uint8)
+        X = np.zeros((max(n, 1), 3), np.float32)
+        self.check(lib().vio_mono_init_solve(self.h, _p(b1), _p(b2), n, _p(S), C.byref(P), C.byref(R), _p(M), _p(X)),
+                   "vio_mono_init_solve")
+        return abi.mono_init_result_dict(R), M[:n], X[:n]
+
+    def mono_init_kernel_ms(self):
+        ms = C.c_double()
+        self.check(lib().vio_mono_init_kernel_ms(self.h, C.byref(ms)), "vio_mono_init_kernel_ms")
+        return ms.value
 
     # ---- IMU preintegration ----
     def imu_preintegrate(self, samples, t_start, t_end, gyro_bias=None, accel_bias=None, noise=None):
@@ -352,6 +384,59 @@ def _p(a):
 def ransac_threshold(deg=2.0):
     """threshold_rad = m_ransac_threshold * M_PI / 180.0f (FeatureTracker.cpp:305), as float."""
     return float(np.float32(np.float64(np.float32(deg)) * np.pi / np.float64(np.float32(180.0))))
+
+
+def mono_init_samples(seed, n, iters=200):
+    """Initializer::ComputeEssentialMatrix's sample stream (8 distinct indices per hypothesis) with an
+    injected seed (the reference seeds from std::random_device)."""
+    out = np.zeros((max(iters, 1), 8), np.int32)
+    rc = lib().vio_mono_init_samples(int(seed) & 0xffffffff, int(n), int(iters), _p(out))
+    if rc:
+        raise VioError(f"vio_mono_init_samples failed ({rc})")
+    return out[:iters]
+
+
+def init_select_features(uv, obs_count, width, height, grid_cols=20, grid_rows=10, min_observations=10,
+                         min_features=100):
+    """Initializer::SelectFeaturesForInit on flat arrays; returns the selected feature indices."""
+    uv = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+    oc = np.ascontiguousarray(obs_count, np.int32)
+    n = len(uv)
+    out = np.zeros(max(n, 1), np.int32)
+    m = C.c_int()
+    rc = lib().vio_init_select_features(_p(uv), _p(oc), n, width, height, grid_cols, grid_rows, min_observations,
+                                        min_features, _p(out), C.byref(m))
+    if rc:
+        raise VioError(f"vio_init_select_features failed ({rc})")
+    return out[:m.value]
+
+
+def init_parallax(ids1, uv1, ids2, uv2):
+    """Initializer::ComputeParallax: median pixel displacement of id-matched features."""
+    i1 = np.ascontiguousarray(ids1, np.int32)
+    i2 = np.ascontiguousarray(ids2, np.int32)
+    u1 = np.ascontiguousarray(uv1, np.float32).reshape(-1, 2)
+    u2 = np.ascontiguousarray(uv2, np.float32).reshape(-1, 2)
+    out = C.c_float()
+    rc = lib().vio_init_parallax(_p(i1), _p(u1), len(i1), _p(i2), _p(u2), len(i2), C.byref(out))
+    if rc:
+        raise VioError(f"vio_init_parallax failed ({rc})")
+    return out.value
+
+
+def init_compose(T_BC, R, t, points=None):
+    """Initializer.cpp:174-224: returns (T_wb1, T_wb2, world points or None)."""
+    T = np.ascontiguousarray(T_BC, np.float32).reshape(4, 4)
+    Rm = np.ascontiguousarray(R, np.float32).reshape(3, 3)
+    tv = np.ascontiguousarray(t, np.float32).reshape(3)
+    T1 = np.zeros((4, 4), np.float32)
+    T2 = np.zeros((4, 4), np.float32)
+    X = None if points is None else np.array(points, np.float32).reshape(-1, 3).copy()
+    rc = lib().vio_init_compose(_p(T), _p(Rm), _p(tv), _p(T1), _p(T2), None if X is None else _p(X),
+                                0 if X is None else len(X))
+    if rc:
+        raise VioError(f"vio_init_compose failed ({rc})")
+    return T1, T2, X
 
 
 def ransac_samples(seed, n, iters=1000):

@@ -534,3 +534,45 @@ class ImuInitResult:
                 "scale": r.scale, "gyro_bias": np.array(r.gyro_bias[:]), "accel_bias": np.array(r.accel_bias[:]),
                 "initial_cost": r.initial_cost, "final_cost": r.final_cost,
                 "velocities": self.vel[: 3 * self.F].reshape(-1, 3).copy()}
+
+
+# ---------------------------------------------------------------------------------------------
+# Monocular initialisation (vio_mono_init_solve; Initializer::TryMonocularInitialization)
+VIO_INIT_OK, VIO_INIT_TOO_FEW_BEARINGS, VIO_INIT_ESSENTIAL_FAILED, VIO_INIT_POSE_FAILED = 0, 1, 2, 3
+VIO_INIT_TRIANGULATION, VIO_INIT_VALIDATION = 4, 5
+
+
+class VioMonoInitParams(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32), ("min_features", C.c_int32), ("ransac_iterations", C.c_int32),
+        ("ransac_threshold", C.c_float), ("max_reprojection_error", C.c_float),
+    ]
+
+
+class VioMonoInitResult(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32), ("best_hypothesis", C.c_int32), ("num_inliers", C.c_int32),
+        ("pose_candidate", C.c_int32), ("candidate_good", C.c_int32 * 4), ("num_triangulated", C.c_int32),
+        ("num_valid", C.c_int32), ("mean_reproj_error", C.c_float), ("scale_factor", C.c_float),
+        ("E", C.c_float * 9), ("R", C.c_float * 9), ("t", C.c_float * 3),
+    ]
+
+
+def mono_init_params(width=960, height=480, min_features=100, ransac_iterations=200, ransac_threshold=0.1,
+                     max_reprojection_error=5.0):
+    """Defaults: config/default_config.yaml:33-41 (initialization.*) at the demo's 960x480."""
+    p = VioMonoInitParams()
+    p.width, p.height, p.min_features, p.ransac_iterations = width, height, min_features, ransac_iterations
+    p.ransac_threshold, p.max_reprojection_error = ransac_threshold, max_reprojection_error
+    return p
+
+
+def mono_init_result_dict(r):
+    return {
+        "status": r.status, "best_hypothesis": r.best_hypothesis, "num_inliers": r.num_inliers,
+        "pose_candidate": r.pose_candidate, "candidate_good": list(r.candidate_good),
+        "num_triangulated": r.num_triangulated, "num_valid": r.num_valid,
+        "mean_reproj_error": r.mean_reproj_error, "scale_factor": r.scale_factor,
+        "E": np.array(r.E, np.float32).reshape(3, 3), "R": np.array(r.R, np.float32).reshape(3, 3),
+        "t": np.array(r.t, np.float32),
+    }

@@ -502,6 +502,8 @@ void vio_ctx_destroy(vio_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->rsz_ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->init_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -21,6 +21,8 @@ struct vio_ctx {
     hipEvent_t tri_ev[2] = {nullptr, nullptr};
     // INTER_AREA resize kernel timing (created on first use)
     hipEvent_t rsz_ev[2] = {nullptr, nullptr};
+    // monocular initialisation kernels timing (created on first use)
+    hipEvent_t init_ev[2] = {nullptr, nullptr};
 };
 
 namespace vio360 {
@@ -39,6 +41,8 @@ enum { kSlotResizeSrc = 13, kSlotResizeDst = 14 };
 enum { kSlotRecords = 15 };
 // vio_imu_init_solve inputs, outputs and per-problem scratch
 enum { kSlotImuInit = 16 };
+// vio_mono_init_solve inputs, outputs and scratch
+enum { kSlotMonoInit = 17 };
 
 #define VIO_HIP(ctx, expr)                                  \
     do {                                                    \

@@ -14,6 +14,7 @@
  *                         (src/processing/FeatureTracker.cpp:228-251)
  *   erp_gftt              cv::goodFeaturesToTrack call in FeatureTracker::DetectNewFeatures
  *                         (src/processing/FeatureTracker.cpp:208-226)
+ *   vio_mono_init_solve   Initializer::TryMonocularInitialization (src/processing/Initializer.cpp:47-291)
  *   erp_rot_ransac        FeatureTracker::RejectOutliersRotationRANSAC / EstimateRotation /
  *                         ComputeRotationInliers (src/processing/FeatureTracker.cpp:253-379)
  *
@@ -563,6 +564,80 @@ int erp_resize_area_device(vio_ctx* ctx, const uint8_t* src, int W, int H, int s
                            int dW, int dH, int dst_stride);
 /* device time (ms) of the last resize kernel on this context (waits for it) */
 int erp_resize_area_kernel_ms(vio_ctx* ctx, double* ms);
+
+
+/* ------------------------------------------------------------------------------------------ */
+/* Monocular initialisation: Initializer::TryMonocularInitialization           */
+/* (src/processing/Initializer.cpp:47-291) — essential-matrix RANSAC (:458-621), pose recovery */
+/* (:623-697, :785-835), mid-point triangulation (:699-783), validation (:889-995), scale      */
+/* normalisation (:997-1048).  Config: initialization.* (config/default_config.yaml:33-41).    */
+
+typedef struct {
+    int32_t width, height;          /* m_camera_width / m_camera_height (reprojection pixels) */
+    int32_t min_features;           /* initialization.min_features (100) */
+    int32_t ransac_iterations;      /* initialization.ransac_iterations (200) */
+    float ransac_threshold;         /* initialization.ransac_threshold (0.1) on |b2^T E b1| */
+    float max_reprojection_error;   /* initialization.max_reprojection_error (5.0 px) */
+} vio_mono_init_params;
+
+/* status: where TryMonocularInitialization returned false (0 = success) */
+#define VIO_INIT_OK 0
+#define VIO_INIT_TOO_FEW_BEARINGS 1   /* fewer than 5 bearing pairs (:117-120) */
+#define VIO_INIT_ESSENTIAL_FAILED 2   /* best RANSAC inlier count < min_features (:579-581) */
+#define VIO_INIT_POSE_FAILED 3        /* no cheirality candidate with >= min_features good points (:688-690) */
+#define VIO_INIT_TRIANGULATION 4      /* triangulated points < min_features (:151-154) */
+#define VIO_INIT_VALIDATION 5         /* validated points < min_features, or none (:962-992) */
+
+typedef struct {
+    int32_t status;                 /* VIO_INIT_* */
+    int32_t best_hypothesis;        /* first RANSAC iteration with the (strictly) largest inlier count */
+    int32_t num_inliers;            /* its inlier count */
+    int32_t pose_candidate;         /* chosen (R, t) candidate 0..3 (:659-663) */
+    int32_t candidate_good[4];      /* TestPoseCandidate good-point counts */
+    int32_t num_triangulated;       /* TriangulatePoints successes */
+    int32_t num_valid;              /* ValidateInitialization valid_count */
+    float mean_reproj_error;        /* ValidateInitialization mean_error (px) */
+    float scale_factor;             /* NormalizeScale: 1 / median distance */
+    float E[9];                     /* refined essential matrix, row-major */
+    float R[9];                     /* R_c2c1 (frame 1 -> frame 2), row-major */
+    float t[3];                     /* t_c2c1 after scale normalisation */
+} vio_mono_init_result;
+
+/*
+ * bearings1/2: n unit bearings (Feature::GetBearing, f32 xyz) of the selected features in the
+ * first / last frame of the window; samples: ransac_iterations x 8 indices (the reference draws
+ * them from mt19937 seeded by std::random_device, :477-494 — inject vio_mono_init_samples).
+ * Outputs (host, caller-owned): res; inlier_mask (n, may be NULL) = the best hypothesis' inliers;
+ * points (3n f32, may be NULL) = the scaled mid-point triangulations in camera-1 coordinates
+ * (zero where triangulation failed), before the T_BC transform of :220-224.  1 <= n <= 4096.
+ * The 8x9 / nx9 null vectors and the 3x3 SVDs are f64 Jacobi on the f32-built systems (reference:
+ * Eigen f32 JacobiSVD); per-point arithmetic is the reference's f32.  Blocking.
+ */
+int vio_mono_init_solve(vio_ctx* ctx, const float* bearings1, const float* bearings2, int n, const int32_t* samples,
+                        const vio_mono_init_params* params, vio_mono_init_result* res, uint8_t* inlier_mask,
+                        float* points);
+/* device time (ms) of the last vio_mono_init_solve's kernels on this context (waits for them) */
+int vio_mono_init_kernel_ms(vio_ctx* ctx, double* ms);
+/* the reference's RANSAC sample stream with an injected seed: iters x 8 distinct indices drawn by
+   std::mt19937(seed) + std::uniform_int_distribution<>(0, n-1) with duplicate rejection (:477-494) */
+int vio_mono_init_samples(uint32_t seed, int n, int iters, int32_t* out);
+
+/* Host helpers of the same path (no device work). */
+/* Initializer::SelectFeaturesForInit (:351-433) on a flat view of the last frame's features:
+   uv (n x 2 pixel coords), obs_count (n, Feature::GetObservationCount).  Writes the selected
+   feature indices in the reference's order to out_idx (capacity n), *n_out = count (0 when fewer
+   than min_features candidates have >= min_observations observations). */
+int vio_init_select_features(const float* uv, const int32_t* obs_count, int n, int width, int height, int grid_cols,
+                             int grid_rows, int min_observations, int min_features, int32_t* out_idx, int* n_out);
+/* Initializer::ComputeParallax (:293-349): median pixel displacement of features matched by id
+   (first match in frame 2 for each frame-1 feature); 0 when nothing matches. */
+int vio_init_parallax(const int32_t* ids1, const float* uv1, int n1, const int32_t* ids2, const float* uv2, int n2,
+                      float* parallax);
+/* Frame poses of :184-204 from T_BC (4x4 row-major, camera-to-body) and the result's R, t:
+   T_wb1 = I, T_wb2 = T_BC * T_c1c2^-1 * T_BC^-1 (f32); also maps points (3n, camera-1 frame) to
+   the world frame in place (p <- R_BC p + t_BC, :217-224) when points != NULL. */
+int vio_init_compose(const float* T_BC, const float* R, const float* t, float* T_wb1, float* T_wb2, float* points,
+                     int n);
 
 #ifdef __cplusplus
 }

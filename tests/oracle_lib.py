@@ -129,3 +129,19 @@ def imu_init(vio, prob):
     if rc != 0:
         raise RuntimeError(f"oracle_imu_init rc={rc}")
     return out.result()
+
+
+def mono_init(vio, b1, b2, samples, params):
+    """oracle/init_oracle.c (TryMonocularInitialization restated) with the C-ABI's structs."""
+    L = load()
+    b1 = np.ascontiguousarray(b1, np.float32).reshape(-1, 3)
+    b2 = np.ascontiguousarray(b2, np.float32).reshape(-1, 3)
+    S = np.ascontiguousarray(samples, np.int32).reshape(-1, 8)
+    n = len(b1)
+    R = vio.abi.VioMonoInitResult()
+    M = np.zeros(max(n, 1), np.uint8)
+    X = np.zeros((max(n, 1), 3), np.float32)
+    L.oracle_mono_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_void_p]
+    L.oracle_mono_init(_p(b1), _p(b2), n, _p(S), C.byref(params), C.byref(R), _p(M), _p(X))
+    return vio.abi.mono_init_result_dict(R), M[:n], X[:n]

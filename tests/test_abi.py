@@ -54,6 +54,11 @@ STRUCTS = {
     "vio_ba_gather_out": ("VioBaGatherOut", ["status", "num_lm", "num_obs", "cap_lm", "cap_obs", "lm_mp", "lm_const",
                                              "lm_marg", "lm_xyz", "obs_kf", "obs_lm", "obs_uv", "obs_feat", "kf_const",
                                              "kf_in_problem", "T_wb_init", "T_cb"]),
+    "vio_mono_init_params": ("VioMonoInitParams", ["width", "height", "min_features", "ransac_iterations",
+                                                   "ransac_threshold", "max_reprojection_error"]),
+    "vio_mono_init_result": ("VioMonoInitResult", ["status", "best_hypothesis", "num_inliers", "pose_candidate",
+                                                   "candidate_good", "num_triangulated", "num_valid",
+                                                   "mean_reproj_error", "scale_factor", "E", "R", "t"]),
     "vio_ba_map_update": ("VioBaMapUpdate", ["frame_Twb", "frame_set", "frame_vel", "bias", "mp_pos", "mp_set",
                                              "mp_set_bad", "success", "num_inliers", "num_outliers",
                                              "num_poses_optimized", "num_points_optimized", "num_iterations",

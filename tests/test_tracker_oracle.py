@@ -137,8 +137,9 @@ def test_pixel_to_bearing(vio):
         assert np.allclose(b, ref, atol=2e-7)
 
 
-def py_mt19937_samples(seed, n, iters):
-    """Independent pure-Python mt19937 + libstdc++ Lemire uniform_int_distribution sampler."""
+def py_mt19937_samples(seed, n, iters, k=3):
+    """Independent pure-Python mt19937 + libstdc++ Lemire uniform_int_distribution sampler
+    (k distinct indices per iteration, duplicates redrawn)."""
     mt = [0] * 624
     mt[0] = seed & 0xffffffff
     for i in range(1, 624):
@@ -172,10 +173,10 @@ def py_mt19937_samples(seed, n, iters):
     out = []
     for _ in range(iters):
         got = []
-        while len(got) < 3:
-            k = uni(n)
-            if k not in got:
-                got.append(k)
+        while len(got) < k:
+            j = uni(n)
+            if j not in got:
+                got.append(j)
         out += got
     return np.array(out, np.int32)
 
