@@ -59,7 +59,10 @@ def test_failure_paths(vio, gpu_ctx):
     assert compare(vio, gpu_ctx, b1[:4], b2[:4], iters=0)[0]["status"] == A.VIO_INIT_TOO_FEW_BEARINGS
     assert compare(vio, gpu_ctx, b1, b2, min_features=301)[0]["status"] == A.VIO_INIT_ESSENTIAL_FAILED
     assert compare(vio, gpu_ctx, b1, b2, iters=0)[0]["status"] == A.VIO_INIT_ESSENTIAL_FAILED
-    assert compare(vio, gpu_ctx, b1, b2, max_reprojection_error=1e-9)[0]["status"] == A.VIO_INIT_VALIDATION
+    # validation failure on noisy bearings (a 1e-9 px bar would compare exact-zero errors, where an ulp
+    # of atan2f / asinf decides)
+    n1, n2, *_ = init_cases.make_case(n=300, seed=12, noise_deg=0.3)
+    assert compare(vio, gpu_ctx, n1, n2, max_reprojection_error=0.05)[0]["status"] == A.VIO_INIT_VALIDATION
     c1, c2, *_ = init_cases.make_case(n=300, seed=5, baseline=0.0)
     compare(vio, gpu_ctx, c1, c2)
     # few hypotheses / tiny n
