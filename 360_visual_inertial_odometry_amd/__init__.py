@@ -36,7 +36,7 @@ EXPORTS = [
     "vio_ba_record_bytes", "vio_ba_batch_record_bytes", "vio_ba_batch_pack", "vio_ba_record_unpack",
     "vio_ba_gather", "vio_ba_write_back", "vio_imu_init_solve",
     "vio_mono_init_solve", "vio_mono_init_kernel_ms", "vio_mono_init_samples", "vio_init_select_features",
-    "vio_init_parallax", "vio_init_compose",
+    "vio_init_parallax", "vio_init_compose", "vio_ctx_set_ba_route",
 ]
 
 
@@ -120,6 +120,7 @@ def lib():
                                            vp, C.POINTER(C.c_int)]
     L.vio_init_parallax.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.POINTER(C.c_float)]
     L.vio_init_compose.argtypes = [vp, vp, vp, vp, vp, vp, C.c_int]
+    L.vio_ctx_set_ba_route.argtypes = [vp, C.c_int]
     _lib = L
     return L
 
@@ -157,6 +158,12 @@ class Context:
             pass
 
     # ---- bundle adjustment ----
+    ROUTE_AUTO, ROUTE_PHASES, ROUTE_SINGLE_KERNEL = 0, 1, 2
+
+    def set_ba_route(self, route):
+        """vio_ctx_set_ba_route: execution route of later window solves on this context."""
+        self.check(lib().vio_ctx_set_ba_route(self.h, int(route)), "vio_ctx_set_ba_route")
+
     def ba_solve(self, problems):
         """Solve a list of BaProblem windows in one launch; returns list of result dicts."""
         n = len(problems)

@@ -73,11 +73,14 @@ __device__ __forceinline__ int factor_eval(const double* pc, const double* Rcb_r
         r[0] = 640.0; r[1] = 360.0;
         return 0;
     }
-    const double inv2pi = 1.0 / (2.0 * M_PI);
+    // divisions by L, 2 pi, pi and the Jacobian denominators become products with reciprocals (2
+    // divisions per evaluation instead of 8; each value moves by at most an ulp or two)
+    constexpr double inv2pi = 1.0 / (2.0 * M_PI), invpi = 1.0 / M_PI;
+    const double iL = 1.0 / L;
     double theta = atan2(x, z);
-    double phi = -asin(y / L);
-    double u = cols * (0.5 + theta / (2.0 * M_PI));
-    double v = rows * (0.5 - phi / M_PI);
+    double phi = -asin(y * iL);
+    double u = cols * (0.5 + theta * inv2pi);
+    double v = rows * (0.5 - phi * invpi);
     double du = uo - u, dv = vo - v;
     if (du > cols / 2.0) du -= cols;
     else if (du < -cols / 2.0) du += cols;
@@ -92,13 +95,15 @@ __device__ __forceinline__ int factor_eval(const double* pc, const double* Rcb_r
     if (xz2 < 1e-10 || L2 < 1e-10) return 0;
     jzero = false;
     double xzn = sqrt(xz2);
+    const double ixzn = 1.0 / xzn, ixz2 = ixzn * ixzn, iL2 = iL * iL, iL2xzn = iL2 * ixzn;
+    const double cu = cols * inv2pi, cv = rows * invpi;
     double Jc[6];
-    Jc[0] = -cols * inv2pi * z / xz2;
+    Jc[0] = -cu * z * ixz2;
     Jc[1] = 0.0;
-    Jc[2] = cols * inv2pi * x / xz2;
-    Jc[3] = rows / M_PI * (x * y) / (L2 * xzn);
-    Jc[4] = -rows / M_PI * xzn / L2;
-    Jc[5] = rows / M_PI * (y * z) / (L2 * xzn);
+    Jc[2] = cu * x * ixz2;
+    Jc[3] = cv * (x * y) * iL2xzn;
+    Jc[4] = -cv * xzn * iL2;
+    Jc[5] = cv * (y * z) * iL2xzn;
     double Jw[6];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -156,11 +161,14 @@ __device__ __forceinline__ int factor_eval_ap(const double* pc, const double* Rc
         r[0] = 640.0; r[1] = 360.0;
         return 0;
     }
-    const double inv2pi = 1.0 / (2.0 * M_PI);
+    // divisions by L, 2 pi, pi and the Jacobian denominators become products with reciprocals (2
+    // divisions per evaluation instead of 8; each value moves by at most an ulp or two)
+    constexpr double inv2pi = 1.0 / (2.0 * M_PI), invpi = 1.0 / M_PI;
+    const double iL = 1.0 / L;
     double theta = atan2(x, z);
-    double phi = -asin(y / L);
-    double u = cols * (0.5 + theta / (2.0 * M_PI));
-    double v = rows * (0.5 - phi / M_PI);
+    double phi = -asin(y * iL);
+    double u = cols * (0.5 + theta * inv2pi);
+    double v = rows * (0.5 - phi * invpi);
     double du = uo - u, dv = vo - v;
     if (du > cols / 2.0) du -= cols;
     else if (du < -cols / 2.0) du += cols;
@@ -174,13 +182,15 @@ __device__ __forceinline__ int factor_eval_ap(const double* pc, const double* Rc
     if (xz2 < 1e-10 || L2 < 1e-10) return 0;
     jzero = false;
     double xzn = sqrt(xz2);
+    const double ixzn = 1.0 / xzn, ixz2 = ixzn * ixzn, iL2 = iL * iL, iL2xzn = iL2 * ixzn;
+    const double cu = cols * inv2pi, cv = rows * invpi;
     double Jc[6];
-    Jc[0] = -cols * inv2pi * z / xz2;
+    Jc[0] = -cu * z * ixz2;
     Jc[1] = 0.0;
-    Jc[2] = cols * inv2pi * x / xz2;
-    Jc[3] = rows / M_PI * (x * y) / (L2 * xzn);
-    Jc[4] = -rows / M_PI * xzn / L2;
-    Jc[5] = rows / M_PI * (y * z) / (L2 * xzn);
+    Jc[2] = cu * x * ixz2;
+    Jc[3] = cv * (x * y) * iL2xzn;
+    Jc[4] = -cv * xzn * iL2;
+    Jc[5] = cv * (y * z) * iL2xzn;
     double Jw[6];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {

@@ -389,24 +389,21 @@ static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
     return VIO_OK;
 }
 
-// Small batches of LocalBA / BA / VIBA windows (fewer than the chip has CUs to spare: a window's
-// observation walks then spread over many workgroups) run as the phase-kernel sequence
-// (ba_phases.inc); large batches, where one workgroup per window already fills the chip, and PnP
-// windows (outlier rounds inside one solve) run in ba_window_kernel.  Within a path a window's result
-// does not depend on the batch it is in.  Per-window phase profiling and VIO_BA_MONOLITHIC=1 put every
-// window on ba_window_kernel, VIO_BA_PHASES=1 every non-PnP window on the phase kernels (A/B runs).
-constexpr int PHASE_BATCH_MAX = 32;
+// LocalBA / BA / VIBA windows run as the phase-kernel sequence (ba_phases.inc): a window's
+// observation walks spread over many workgroups per phase, so it is the faster route at every batch
+// size measured (1 window: 1.42 vs 1.70 ms; the 256-window config-4 shard: 3.59 vs 3.75 ms per 10
+// iterations).  PnP windows (outlier rounds inside one solve) run in ba_window_kernel, the
+// single-kernel solver.  Within a route a window's result does not depend on the batch it is in.
+// vio_ctx_set_ba_route / VIO_BA_MONOLITHIC=1 / VIO_BA_PHASES=1 select a route explicitly (A/B runs,
+// tests); per-window phase profiling runs on ba_window_kernel.
 static bool env_flag(const char* name) {
     const char* e = std::getenv(name);
     return e && e[0] == '1';
 }
-static bool force_monolithic(const BaDevice& d) {
+static bool force_monolithic(const vio_ctx* ctx, const BaDevice& d) {
     static const bool mono = env_flag("VIO_BA_MONOLITHIC"), phases = env_flag("VIO_BA_PHASES");
-    if (phases) return false;  // (per-phase profiling of the phase route: ph_solve's slots 16-20)
-    if (mono || d.P.prof) return true;
-    int non_pnp = 0;
-    for (const BaWin& w : d.pk.win) non_pnp += w.is_pnp ? 0 : 1;
-    return non_pnp > PHASE_BATCH_MAX;
+    if (phases || ctx->ba_route == VIO_BA_ROUTE_PHASES) return false;
+    return mono || d.P.prof || ctx->ba_route == VIO_BA_ROUTE_SINGLE_KERNEL;
 }
 
 static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
@@ -414,7 +411,7 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     if (timed) VIO_HIP(ctx, hipEventRecord(d.ev0, ctx->stream));
     bool any_pnp = false, any_other = false;
     for (const BaWin& w : d.pk.win) (w.is_pnp ? any_pnp : any_other) = true;
-    const bool phases = any_other && !force_monolithic(d);
+    const bool phases = any_other && !force_monolithic(ctx, d);
     d.P.route = phases ? 1 : 0;
     hipError_t e = hipSuccess;
     const char* what = "ba_window_kernel launch";
@@ -460,6 +457,12 @@ struct vio_ba_batch {
 extern "C" {
 
 int vio_abi_version(void) { return VIO360_ABI_VERSION; }
+
+int vio_ctx_set_ba_route(vio_ctx* ctx, int route) {
+    if (!ctx || route < VIO_BA_ROUTE_AUTO || route > VIO_BA_ROUTE_SINGLE_KERNEL) return VIO_EINVAL;
+    ctx->ba_route = route;
+    return VIO_OK;
+}
 
 static std::string g_create_error;
 

@@ -265,6 +265,144 @@ __device__ __noinline__ void imu_eval(const vio_preint& p, const double* sqi, co
         }
 }
 
+// imu_eval with Jacobians by one whole wave: every lane evaluates the factor's common part (bias
+// correction, raw residual, the weighted rotation residual and Jr^-1 J_Rg), lane i < 9 returns residual
+// row i in r, lane j < 12 writes Jacobian column j (J row-major 9x12, [vi | bg | ba | vj]).  Each output
+// element goes through imu_eval's operations in imu_eval's order (same values); the serial chain of
+// 486 + 81 dependent multiply-adds becomes 9 + 9 per lane.
+__device__ __noinline__ void imu_eval_wave(const vio_preint& p, const double* sqi, const double* g, const double* pci,
+                                           const double* pcj, const double* vi, const double* bg, const double* ba,
+                                           const double* vj, int lane, double& r_out, double* J) {
+    const double* Rwj = pcj;
+    const double* twi = pci + 9;
+    const double* twj = pcj + 9;
+    const double* Rbwi = pci + 12;
+    const double dt = p.dt_total;
+    double DR[9], DV[3], DP[3], JRg[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) { DR[i] = (double)p.delta_R[i]; JRg[i] = (double)p.J_Rg[i]; }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { DV[i] = (double)p.delta_V[i]; DP[i] = (double)p.delta_P[i]; }
+    double dbg[3], dba[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { dbg[i] = bg[i] - (double)p.gyro_bias[i]; dba[i] = ba[i] - (double)p.accel_bias[i]; }
+    if (nrm3(dbg) > 1e-6 || nrm3(dba) > 1e-6) {
+        double w[3], E[9], M[9];
+        m3vec(JRg, dbg, w);
+        so3_exp(w, E);
+        m3mul(DR, E, M);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) DR[i] = M[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            DV[i] += (double)p.J_Vg[3 * i] * dbg[0] + (double)p.J_Vg[3 * i + 1] * dbg[1] + (double)p.J_Vg[3 * i + 2] * dbg[2]
+                   + (double)p.J_Va[3 * i] * dba[0] + (double)p.J_Va[3 * i + 1] * dba[1] + (double)p.J_Va[3 * i + 2] * dba[2];
+            DP[i] += (double)p.J_Pg[3 * i] * dbg[0] + (double)p.J_Pg[3 * i + 1] * dbg[1] + (double)p.J_Pg[3 * i + 2] * dbg[2]
+                   + (double)p.J_Pa[3 * i] * dba[0] + (double)p.J_Pa[3 * i + 1] * dba[1] + (double)p.J_Pa[3 * i + 2] * dba[2];
+        }
+    }
+    double raw[9];
+    {
+        double A[9], B[9];
+        m3tmul(DR, Rbwi, A);
+        m3mul(A, Rwj, B);
+        imu_log(B, raw);
+        double tv[3], ev[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) tv[i] = vj[i] - vi[i] - g[i] * dt;
+        m3vec(Rbwi, tv, ev);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) raw[3 + i] = ev[i] - DV[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) tv[i] = twj[i] - twi[i] - vi[i] * dt - 0.5 * g[i] * dt * dt;
+        m3vec(Rbwi, tv, ev);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) raw[6 + i] = ev[i] - DP[i];
+    }
+    // residual rows 0..2 on every lane (the bias Jacobian needs them), row `lane` on lanes < 9
+    double r3[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) s += sqi[9 * i + k] * raw[k];
+        r3[i] = s;
+    }
+    {
+        const int ri = lane < 9 ? lane : 0;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) s += sqi[9 * ri + k] * raw[k];
+        r_out = s;
+    }
+    if (lane >= 12) return;
+    const int col = lane;
+    double Jcol[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Jcol[i] = 0.0;
+    if (col < 3 || col >= 9) {  // vi (col 0..2) / vj (col 9..11): diagonal sqrt-information blocks only
+        const int j = col < 3 ? col : col - 9;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            double a = 0, b = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                a += sqi[9 * (3 + i) + 3 + k] * Rbwi[3 * k + j];
+                b += sqi[9 * (6 + i) + 6 + k] * Rbwi[3 * k + j];
+            }
+            if (col < 3) {
+                Jcol[3 + i] = -a;
+                Jcol[6 + i] = -b * dt;
+            } else {
+                Jcol[3 + i] = a;
+            }
+        }
+    } else {  // bg (col 3..5) / ba (col 6..8)
+        const int j = col < 6 ? col - 3 : col - 6;
+        double Tc[9];  // column j of T (bg) or Ta (ba)
+        if (col < 6) {
+            double mer[3] = {-r3[0], -r3[1], -r3[2]}, Jr[9], Jri[9], A[9];
+            double th = nrm3(mer);
+            if (th < 1e-6) {
+#pragma unroll
+                for (int i = 0; i < 9; ++i) Jr[i] = (i % 4 == 0) ? 1.0 : 0.0;
+            } else {
+                double P[9], P2[9];
+                hat3(mer, P);
+                m3mul(P, P, P2);
+                double th2 = th * th, a = (1.0 - cos(th)) / th2, b = (th - sin(th)) / (th2 * th);
+#pragma unroll
+                for (int i = 0; i < 9; ++i) Jr[i] = -a * P[i] + b * P2[i];
+                Jr[0] += 1; Jr[4] += 1; Jr[8] += 1;
+            }
+            inv3(Jr, Jri);
+            m3mul(Jri, JRg, A);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                Tc[i] = -A[3 * i + j];
+                Tc[3 + i] = -(double)p.J_Vg[3 * i + j];
+                Tc[6 + i] = -(double)p.J_Pg[3 * i + j];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                Tc[i] = 0.0;
+                Tc[3 + i] = -(double)p.J_Va[3 * i + j];
+                Tc[6 + i] = -(double)p.J_Pa[3 * i + j];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            double s = 0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) s += sqi[9 * i + k] * Tc[k];
+            Jcol[i] = s;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) J[12 * i + col] = Jcol[i];
+}
+
 // InertialFactorFixedGravity ctor (Factors.cpp:1310-1323): sqrt-information = chol((cov + 1e-8 I)^-1)^T,
 // identity when the inverse or its Cholesky fails.  One whole wave per factor: Gauss-Jordan with
 // partial pivoting on [Sigma | I] with lane j < 18 holding column j (9 rows in registers, pivot row

@@ -58,14 +58,18 @@ __device__ __forceinline__ int chol16_wave(double* A, int ld, double* lbt, doubl
         for (int m = 0; m < 16; ++m) lt[16 * m + i] = d[m];
     }
     wave_lds_sync();
-    // column i of Linv (lower): x[q] = Linv[q][i]; L[q][m] read as an LDS broadcast
-    double x[16];
+    // column i of Linv (lower): x[q] = Linv[q][i]; L[q][m] read as an LDS broadcast.  Column-oriented:
+    // once x[m] is known every later s[q] takes its term at once (independent FMAs, a 16-step critical
+    // path); each s[q] still subtracts its terms in ascending m, so the values are those of the
+    // row-oriented substitution bit for bit.
+    double x[16], s[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        double s = q == i ? 1.0 : 0.0;
+    for (int q = 0; q < 16; ++q) s[q] = q == i ? 1.0 : 0.0;
 #pragma unroll
-        for (int m = 0; m < q; ++m) s -= lt[16 * m + q] * x[m];
-        x[q] = s * il[q];
+    for (int m = 0; m < 16; ++m) {
+        x[m] = s[m] * il[m];
+#pragma unroll
+        for (int q = m + 1; q < 16; ++q) s[q] -= lt[16 * m + q] * x[m];
     }
     if (kk == 0) {
         double* dst = lbt + 16 * i;

@@ -23,6 +23,8 @@ struct vio_ctx {
     hipEvent_t rsz_ev[2] = {nullptr, nullptr};
     // monocular initialisation kernels timing (created on first use)
     hipEvent_t init_ev[2] = {nullptr, nullptr};
+    // window-BA execution route (vio_ctx_set_ba_route)
+    int ba_route = VIO_BA_ROUTE_AUTO;
 };
 
 namespace vio360 {

@@ -49,11 +49,19 @@ def pmc_traffic():
 
 
 def ba_traffic(args):
-    """PMC HBM bytes per ba_window_kernel launch (profiled on the default 256-window x 10-iteration step)."""
-    k, src = pmc_traffic()
-    if not k or "ba_window_kernel" not in k or args.windows != 256 or args.lm_iters != 10:
+    """PMC HBM bytes of one 256-window x 10-iteration step of the phase route: every kernel of the
+    step's graph, bytes per launch x launches per step (tools/gpu_pmc_ba.sh over tools/ba_batch_run.py
+    -> profiles/r*_pmc_traffic_ba.json; a step = one ph_setup_kernel launch)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_ba.json")))
+    if not files or args.windows != 256 or args.lm_iters != 10:
         return None
-    return k["ba_window_kernel"]["hbm_bytes_per_launch"]
+    with open(files[-1]) as f:
+        k = json.load(f)["kernels"]
+    if "ph_setup_kernel" not in k:
+        return None
+    steps = k["ph_setup_kernel"]["dispatches"]
+    return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items() if n.startswith("ph_")) / steps
 
 
 def klt_traffic():
@@ -641,11 +649,14 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK,
                 "traffic": ba_traffic(args),
-                "kernel": "ba_window_kernel",
+                "kernel": "phase-route step graph (ph_setup, ph_lin, 11 x [ph_prep, ph_schur, ph_solve, "
+                          "ph_back, ph_ctrl], ph_post)",
                 "kernel_avg_ms": kms,
                 "kernel_launches": kcount,
                 "flops_per_launch": flops_iter * args.lm_iters,
-                "note": "FP64 (vector = matrix peak on MI355X); flops by the SURVEY §8d convention",
+                "note": "FP64 (vector = matrix peak on MI355X); flops by the SURVEY §8d convention; achieved = "
+                        "flops of one step / HIP-event time of the step's graph on the batch stream; traffic = "
+                        "PMC HBM bytes of all the step's kernels",
             },
             "single_window": {
                 "config": "config 3 (one window per launch)",

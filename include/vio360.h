@@ -56,6 +56,15 @@ void vio_ctx_destroy(vio_ctx* ctx);
 const char* vio_ctx_last_error(const vio_ctx* ctx);
 int vio_abi_version(void);
 
+/* Window-BA execution route of this context's later solves / batches (both routes give the same
+   results to roundoff; within a route results do not depend on the batch):
+   AUTO (default) = phase kernels for LocalBA / BA / VIBA windows, single kernel for PnP windows;
+   PHASES / SINGLE_KERNEL force one route for every non-PnP window (PnP always runs single-kernel). */
+#define VIO_BA_ROUTE_AUTO 0
+#define VIO_BA_ROUTE_PHASES 1
+#define VIO_BA_ROUTE_SINGLE_KERNEL 2
+int vio_ctx_set_ba_route(vio_ctx* ctx, int route);
+
 /* ----------------------------------------------------------------------------------------- */
 /* Bundle adjustment / PnP                                                                    */
 

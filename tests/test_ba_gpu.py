@@ -132,8 +132,12 @@ def test_lm_trace_matches_oracle(vio, gpu_ctx, all_cases, tc):
     p = vio.BaProblem(w, variant=var, **kw)
     o = oracle_lib.ba_solve(vio, p)
     cloud = oracle_cloud(vio, w, var, **kw)
-    solo = gpu_ctx.ba_solve([p])[0]            # phase route
-    mono = gpu_ctx.ba_solve([p] * 33)[0]       # single-kernel route (batch above the phase-route size)
+    solo = gpu_ctx.ba_solve([p])[0]            # phase route (default)
+    gpu_ctx.set_ba_route(gpu_ctx.ROUTE_SINGLE_KERNEL)
+    try:
+        mono = gpu_ctx.ba_solve([p])[0]        # single-kernel route
+    finally:
+        gpu_ctx.set_ba_route(gpu_ctx.ROUTE_AUTO)
     for g in (solo, mono):
         assert len(g["trace"]["cost"]) == g["iterations"]
         compare_traces(o, g, cloud, fixed, min(min_prefix, o["iterations"]))
@@ -241,12 +245,16 @@ def test_batched_equals_single_bitwise(vio, synth, gpu_ctx):
 
 
 def test_routes_agree(vio, synth, gpu_ctx):
-    """Batches above the phase-route size (32 non-PnP windows) run in the single-kernel solver, whose
-    fixed summation orders differ from the phase kernels': the same window agrees with its solo
-    (phase-route) result to roundoff."""
+    """The single-kernel solver (vio_ctx_set_ba_route) has fixed summation orders that differ from the
+    phase kernels': a window of a 40-window single-kernel batch agrees with its solo phase-route result
+    to roundoff."""
     ws = [synth.config3(synth.SEED + i) for i in range(40)]
     probs = [vio.BaProblem(w, variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1) for w in ws]
-    big = gpu_ctx.ba_solve(probs)
+    gpu_ctx.set_ba_route(gpu_ctx.ROUTE_SINGLE_KERNEL)
+    try:
+        big = gpu_ctx.ba_solve(probs)
+    finally:
+        gpu_ctx.set_ba_route(gpu_ctx.ROUTE_AUTO)
     for i in (0, 17, 39):
         solo = gpu_ctx.ba_solve([probs[i]])[0]
         assert big[i]["iterations"] == solo["iterations"]
