@@ -37,6 +37,11 @@ EXPORTS = [
     "vio_ba_gather", "vio_ba_write_back", "vio_imu_init_solve",
     "vio_mono_init_solve", "vio_mono_init_kernel_ms", "vio_mono_init_samples", "vio_init_select_features",
     "vio_init_parallax", "vio_init_compose", "vio_ctx_set_ba_route",
+    "vio_window_create", "vio_window_destroy", "vio_window_add_mappoint", "vio_window_add_observation",
+    "vio_window_link_mappoints", "vio_window_add_keyframe", "vio_window_triangulation_candidates",
+    "vio_window_commit_triangulation", "vio_window_triangulate", "vio_window_keyframes", "vio_window_num_mappoints",
+    "vio_window_mappoint", "vio_window_mappoint_observations", "vio_window_frame_mappoints", "vio_window_map_view",
+    "vio_window_apply_update",
 ]
 
 
@@ -121,6 +126,24 @@ def lib():
     L.vio_init_parallax.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.POINTER(C.c_float)]
     L.vio_init_compose.argtypes = [vp, vp, vp, vp, vp, vp, C.c_int]
     L.vio_ctx_set_ba_route.argtypes = [vp, C.c_int]
+    L.vio_window_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.vio_window_destroy.argtypes = [vp]
+    L.vio_window_add_mappoint.argtypes = [vp, vp, C.c_int32, C.POINTER(C.c_int32)]
+    L.vio_window_add_observation.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32]
+    L.vio_window_link_mappoints.argtypes = [vp, vp, vp, vp, C.c_int, vp, C.c_int, vp]
+    L.vio_window_add_keyframe.argtypes = [vp, C.POINTER(abi.VioWindowFrame), C.POINTER(abi.VioWindowKfStats)]
+    L.vio_window_triangulation_candidates.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, C.c_int,
+                                                      C.POINTER(C.c_int)]
+    L.vio_window_commit_triangulation.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, C.c_int, vp,
+                                                  C.POINTER(C.c_int)]
+    L.vio_window_triangulate.argtypes = [vp, vp, C.c_int32, C.c_int32, C.POINTER(C.c_int)]
+    L.vio_window_keyframes.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_int)]
+    L.vio_window_num_mappoints.argtypes = [vp]
+    L.vio_window_mappoint.argtypes = [vp, C.c_int32, C.POINTER(abi.VioWindowMappointInfo)]
+    L.vio_window_mappoint_observations.argtypes = [vp, C.c_int32, vp, vp, C.c_int, C.POINTER(C.c_int)]
+    L.vio_window_frame_mappoints.argtypes = [vp, C.c_int32, vp, C.c_int, C.POINTER(C.c_int)]
+    L.vio_window_map_view.argtypes = [vp, C.c_int, C.c_int, C.POINTER(abi.VioMapView)]
+    L.vio_window_apply_update.argtypes = [vp, C.POINTER(abi.VioBaMapUpdate)]
     _lib = L
     return L
 
@@ -655,3 +678,158 @@ def ba_write_back(view, variant, gather, out):
     if rc != 0:
         raise VioError(f"vio_ba_write_back failed ({rc})")
     return u.result()
+
+
+class Window:
+    """vio_window: the Estimator's keyframe window and MapPoint graph (CreateKeyframe slide,
+    LinkMapPointsFromPreviousFrame, TriangulateNewMapPoints) on the host."""
+
+    def __init__(self, max_keyframes=10):
+        h = C.c_void_p()
+        if lib().vio_window_create(int(max_keyframes), C.byref(h)):
+            raise VioError("vio_window_create failed")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().vio_window_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _rc(rc, what):
+        if rc:
+            raise VioError(f"{what} failed ({rc})")
+
+    def add_mappoint(self, pos, reference_frame=-1):
+        p = np.ascontiguousarray(pos, np.float32).reshape(3)
+        h = C.c_int32()
+        self._rc(lib().vio_window_add_mappoint(self.h, _p(p), int(reference_frame), C.byref(h)), "add_mappoint")
+        return h.value
+
+    def add_observation(self, mp, frame_id, feat):
+        self._rc(lib().vio_window_add_observation(self.h, int(mp), int(frame_id), int(feat)), "add_observation")
+
+    def link_mappoints(self, prev_id, prev_valid, prev_mp, curr_id):
+        pi = np.ascontiguousarray(prev_id, np.int32)
+        pv = np.ascontiguousarray(prev_valid, np.uint8)
+        pm = np.ascontiguousarray(prev_mp, np.int32)
+        ci = np.ascontiguousarray(curr_id, np.int32)
+        out = np.full(max(len(ci), 1), -1, np.int32)
+        self._rc(lib().vio_window_link_mappoints(self.h, _p(pi), _p(pv), _p(pm), len(pi), _p(ci), len(ci), _p(out)),
+                 "link_mappoints")
+        return out[:len(ci)]
+
+    def add_keyframe(self, frame_id, T_wb, T_bc, feature_id, bearing, valid, mappoint, uv=None, tracks=None,
+                     width=960):
+        """tracks: list (per feature) of [(frame_id, feature_index), ...] (Feature::GetObservations)."""
+        n = len(feature_id)
+        keep = [np.ascontiguousarray(T_wb, np.float32).reshape(16), np.ascontiguousarray(T_bc, np.float32).reshape(16),
+                np.ascontiguousarray(feature_id, np.int32), np.ascontiguousarray(bearing, np.float32).reshape(-1),
+                np.ascontiguousarray(valid, np.uint8), np.ascontiguousarray(mappoint, np.int32),
+                np.ascontiguousarray(uv if uv is not None else np.zeros((n, 2)), np.float32).reshape(-1)]
+        f = abi.VioWindowFrame()
+        f.frame_id, f.num_features, f.width = int(frame_id), n, int(width)
+        f.T_wb, f.T_bc = abi._ptr(keep[0], C.c_float), abi._ptr(keep[1], C.c_float)
+        f.feature_id, f.bearing = abi._ptr(keep[2], C.c_int32), abi._ptr(keep[3], C.c_float)
+        f.valid, f.mappoint, f.uv = abi._ptr(keep[4], C.c_uint8), abi._ptr(keep[5], C.c_int32), abi._ptr(keep[6], C.c_float)
+        if tracks is not None:
+            beg = np.zeros(n + 1, np.int32)
+            fr, ft = [], []
+            for i, t in enumerate(tracks):
+                for (a, b) in t:
+                    fr.append(a)
+                    ft.append(b)
+                beg[i + 1] = len(fr)
+            keep += [beg, np.array(fr + [0], np.int32), np.array(ft + [0], np.int32)]
+            f.track_begin, f.track_frame, f.track_feat = (abi._ptr(keep[-3], C.c_int32), abi._ptr(keep[-2], C.c_int32),
+                                                          abi._ptr(keep[-1], C.c_int32))
+        st = abi.VioWindowKfStats()
+        self._rc(lib().vio_window_add_keyframe(self.h, C.byref(f), C.byref(st)), "add_keyframe")
+        return {k: getattr(st, k) for k in ("obs_added", "transferred", "deleted", "removed_frame", "num_keyframes")}
+
+    def triangulation_candidates(self, kf1, kf2):
+        n = C.c_int()
+        self._rc(lib().vio_window_triangulation_candidates(self.h, kf1, kf2, None, None, None, 0, C.byref(n)), "cand")
+        m = n.value
+        pairs = np.zeros((max(m, 1), 2), np.int32)
+        bear = np.zeros((max(m, 1), 6), np.float32)
+        T = np.zeros((2, 4, 4), np.float32)
+        self._rc(lib().vio_window_triangulation_candidates(self.h, kf1, kf2, _p(pairs), _p(bear), _p(T), m, C.byref(n)),
+                 "cand")
+        return pairs[:m], bear[:m], T
+
+    def commit_triangulation(self, kf1, kf2, pairs, points, valid):
+        pr = np.ascontiguousarray(pairs, np.int32).reshape(-1, 2)
+        X = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+        V = np.ascontiguousarray(valid, np.uint8)
+        out = np.full(max(len(pr), 1), -1, np.int32)
+        n = C.c_int()
+        self._rc(lib().vio_window_commit_triangulation(self.h, kf1, kf2, _p(pr), _p(X), _p(V), len(pr), _p(out),
+                                                       C.byref(n)), "commit")
+        return out[:len(pr)]
+
+    def triangulate(self, ctx, kf1, kf2):
+        n = C.c_int()
+        ctx.check(lib().vio_window_triangulate(self.h, ctx.h, kf1, kf2, C.byref(n)), "vio_window_triangulate")
+        return n.value
+
+    def keyframes(self):
+        n = C.c_int()
+        self._rc(lib().vio_window_keyframes(self.h, None, 0, C.byref(n)), "keyframes")
+        out = np.zeros(max(n.value, 1), np.int32)
+        self._rc(lib().vio_window_keyframes(self.h, _p(out), n.value, C.byref(n)), "keyframes")
+        return out[:n.value].tolist()
+
+    def num_mappoints(self):
+        return lib().vio_window_num_mappoints(self.h)
+
+    def mappoint(self, h):
+        info = abi.VioWindowMappointInfo()
+        self._rc(lib().vio_window_mappoint(self.h, int(h), C.byref(info)), "mappoint")
+        n = C.c_int()
+        fr = np.zeros(max(info.num_observations, 1), np.int32)
+        ft = np.zeros(max(info.num_observations, 1), np.int32)
+        self._rc(lib().vio_window_mappoint_observations(self.h, int(h), _p(fr), _p(ft), len(fr), C.byref(n)), "obs")
+        return {"pos": np.array(info.pos, np.float32), "bad": bool(info.bad), "marg": bool(info.marginalized),
+                "tri": bool(info.triangulated), "ref": info.reference_frame,
+                "obs": list(zip(fr[:n.value].tolist(), ft[:n.value].tolist()))}
+
+    def frame_mappoints(self, frame_id):
+        n = C.c_int()
+        self._rc(lib().vio_window_frame_mappoints(self.h, int(frame_id), None, 0, C.byref(n)), "frame_mappoints")
+        out = np.zeros(max(n.value, 1), np.int32)
+        self._rc(lib().vio_window_frame_mappoints(self.h, int(frame_id), _p(out), n.value, C.byref(n)), "frame_mps")
+        return out[:n.value].tolist()
+
+    def map_view(self, height=480, boundary_margin=20):
+        """vio_window_map_view, copied into an abi.MapView (for ba_gather / ba_write_back)."""
+        v = abi.VioMapView()
+        self._rc(lib().vio_window_map_view(self.h, int(height), int(boundary_margin), C.byref(v)), "map_view")
+        F, M = v.num_frames, v.num_mappoints
+        a = np.ctypeslib.as_array
+        G = int(a(v.feat_begin, shape=(F + 1,))[-1]) if F else 0
+        nob = int(a(v.mp_obs_begin, shape=(M + 1,))[-1]) if M else 0
+
+        def arr(ptr, n, dt):
+            return a(ptr, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
+        return abi.MapView({
+            "frame_Twb": arr(v.frame_Twb, 16 * F, np.float32).reshape(-1, 4, 4),
+            "frame_Tcb": arr(v.frame_Tcb, 16 * F, np.float32).reshape(-1, 4, 4),
+            "feat_begin": a(v.feat_begin, shape=(F + 1,)).copy(), "feat_uv": arr(v.feat_uv, 2 * G, np.float32),
+            "feat_valid": arr(v.feat_valid, G, np.uint8), "feat_mp": arr(v.feat_mp, G, np.int32),
+            "mp_key": arr(v.mp_key, M, np.int64), "mp_bad": arr(v.mp_bad, M, np.uint8),
+            "mp_marg": arr(v.mp_marg, M, np.uint8), "mp_pos": arr(v.mp_pos, 3 * M, np.float32),
+            "mp_obs_begin": a(v.mp_obs_begin, shape=(M + 1,)).copy(), "mp_obs_frame": arr(v.mp_obs_frame, nob, np.int32),
+            "mp_obs_feat": arr(v.mp_obs_feat, nob, np.int32),
+            "width": v.width, "height": v.height, "boundary_margin": v.boundary_margin})
+
+    def apply_update(self, upd):
+        """vio_window_apply_update with an abi.MapUpdate (or a raw VioBaMapUpdate) of the last map view."""
+        c = upd.c if hasattr(upd, "c") else upd
+        self._rc(lib().vio_window_apply_update(self.h, C.byref(c)), "apply_update")

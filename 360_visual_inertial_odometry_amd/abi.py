@@ -576,3 +576,27 @@ def mono_init_result_dict(r):
         "E": np.array(r.E, np.float32).reshape(3, 3), "R": np.array(r.R, np.float32).reshape(3, 3),
         "t": np.array(r.t, np.float32),
     }
+
+
+# ---------------------------------------------------------------------------------------------
+# Estimator window bookkeeping (vio_window_*; Estimator::CreateKeyframe / TriangulateNewMapPoints)
+_i32p = C.POINTER(C.c_int32)
+_f32p = C.POINTER(C.c_float)
+
+
+class VioWindowFrame(C.Structure):
+    _fields_ = [
+        ("frame_id", C.c_int32), ("num_features", C.c_int32), ("width", C.c_int32), ("_pad", C.c_int32),
+        ("T_wb", _f32p), ("T_bc", _f32p), ("feature_id", _i32p), ("uv", _f32p), ("bearing", _f32p),
+        ("valid", _u8p), ("mappoint", _i32p), ("track_begin", _i32p), ("track_frame", _i32p), ("track_feat", _i32p),
+    ]
+
+
+class VioWindowKfStats(C.Structure):
+    _fields_ = [("obs_added", C.c_int32), ("transferred", C.c_int32), ("deleted", C.c_int32),
+                ("removed_frame", C.c_int32), ("num_keyframes", C.c_int32), ("_pad", C.c_int32)]
+
+
+class VioWindowMappointInfo(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("bad", C.c_int32), ("marginalized", C.c_int32), ("triangulated", C.c_int32),
+                ("reference_frame", C.c_int32), ("num_observations", C.c_int32)]

@@ -15,6 +15,8 @@
  *   erp_gftt              cv::goodFeaturesToTrack call in FeatureTracker::DetectNewFeatures
  *                         (src/processing/FeatureTracker.cpp:208-226)
  *   vio_mono_init_solve   Initializer::TryMonocularInitialization (src/processing/Initializer.cpp:47-291)
+ *   vio_window_*          Estimator::CreateKeyframe window slide / TriangulateNewMapPoints
+ *                         (src/processing/Estimator.cpp:637-804, 1141-1318)
  *   erp_rot_ransac        FeatureTracker::RejectOutliersRotationRANSAC / EstimateRotation /
  *                         ComputeRotationInliers (src/processing/FeatureTracker.cpp:253-379)
  *
@@ -647,6 +649,92 @@ int vio_init_parallax(const int32_t* ids1, const float* uv1, int n1, const int32
    the world frame in place (p <- R_BC p + t_BC, :217-224) when points != NULL. */
 int vio_init_compose(const float* T_BC, const float* R, const float* t, float* T_wb1, float* T_wb2, float* points,
                      int n);
+
+
+/* ------------------------------------------------------------------------------------------ */
+/* Estimator sliding-window bookkeeping on a host-side keyframe / MapPoint graph:  */
+/* Estimator::CreateKeyframe's observation update and window slide (src/processing/Estimator.cpp: */
+/* 671-754: reference-keyframe transfer, marginalisation, SetBad, RemoveObservation),             */
+/* LinkMapPointsFromPreviousFrame (:806-843) and TriangulateNewMapPoints (:1141-1318, the          */
+/* triangulation itself on device through vio_triangulate).  MapPoints are handles 0, 1, ... in   */
+/* creation order; frames are identified by Frame::GetFrameId().  Not thread-safe.                */
+
+typedef struct vio_window vio_window;
+
+/* a keyframe handed to vio_window_add_keyframe (copied; the caller keeps its buffers) */
+typedef struct {
+    int32_t frame_id;
+    int32_t num_features;
+    int32_t width;               /* Frame::GetWidth (pixel error scale of the triangulation check) */
+    int32_t _pad;
+    const float* T_wb;           /* 16, row-major: Frame::GetTwb() */
+    const float* T_bc;           /* 16, row-major: Frame::GetTBC() (camera-to-body) */
+    const int32_t* feature_id;   /* n: Feature::GetFeatureId() */
+    const float* uv;             /* 2n: GetPixelCoord() (carried for the BA map view) */
+    const float* bearing;        /* 3n: GetBearing() */
+    const uint8_t* valid;        /* n: IsValid() */
+    const int32_t* mappoint;     /* n: GetMapPoint() handle (-1: none), e.g. from vio_window_link_mappoints */
+    /* Feature::GetObservations() of each feature (its track): CSR, entries (frame id, feature index);
+       may be NULL (no track history) */
+    const int32_t* track_begin;  /* n + 1 */
+    const int32_t* track_frame;
+    const int32_t* track_feat;
+} vio_window_frame;
+
+typedef struct {
+    int32_t obs_added;           /* observations the new keyframe added (:679-690) */
+    int32_t transferred;         /* reference-keyframe transfers (marginalised MapPoints, :720-725) */
+    int32_t deleted;             /* referenced MapPoints no other keyframe observes, set bad (:726-729);
+                                    MapPoints left without observations (:747-749) also turn bad */
+    int32_t removed_frame;       /* frame id of the keyframe slid out (-1: none) */
+    int32_t num_keyframes;       /* window size after the call */
+    int32_t _pad;
+} vio_window_kf_stats;
+
+typedef struct {
+    float pos[3];
+    int32_t bad, marginalized, triangulated;
+    int32_t reference_frame;     /* reference keyframe id, -1 none */
+    int32_t num_observations;
+} vio_window_mappoint_info;
+
+int vio_window_create(int max_keyframes, vio_window** out);   /* max_keyframes: 10 (:693) */
+void vio_window_destroy(vio_window* win);
+/* new MapPoint at pos (e.g. Initializer::CreateMapPoints); reference_frame -1 for none */
+int vio_window_add_mappoint(vio_window* win, const float* pos, int32_t reference_frame, int32_t* handle);
+/* MapPoint::AddObservation(frame, feat) + Frame::SetMapPoint(feat, mp) for a keyframe of the store */
+int vio_window_add_observation(vio_window* win, int32_t mp, int32_t frame_id, int32_t feat);
+/* LinkMapPointsFromPreviousFrame: curr_mp[i] = the previous frame's (valid, last-by-id) feature's
+   MapPoint if it exists and is not bad, else -1 */
+int vio_window_link_mappoints(const vio_window* win, const int32_t* prev_id, const uint8_t* prev_valid,
+                              const int32_t* prev_mp, int n_prev, const int32_t* curr_id, int n_curr, int32_t* curr_mp);
+/* CreateKeyframe: append the keyframe, add its MapPoint observations, slide the window */
+int vio_window_add_keyframe(vio_window* win, const vio_window_frame* frame, vio_window_kf_stats* stats);
+/* TriangulateNewMapPoints(kf1, kf2) in two host halves around the device triangulation:
+   candidates: matched (kf1 index, kf2 index) pairs in kf2 order, their bearings (6 per pair) and the
+   two world-to-camera transforms GetTwc().inverse() (T_cw, 32 floats) -> vio_triangulate;
+   commit: creates a MapPoint per valid triangulation (reference kf1, observations kf1, kf2 and the
+   in-window keyframes of kf2's feature track) and returns the handles in new_mp (-1 where invalid).
+   vio_window_triangulate does both with the device in between; *n_new = new MapPoints. */
+int vio_window_triangulation_candidates(const vio_window* win, int32_t kf1_id, int32_t kf2_id, int32_t* pairs,
+                                        float* bearings, float* T_cw, int cap, int* n);
+int vio_window_commit_triangulation(vio_window* win, int32_t kf1_id, int32_t kf2_id, const int32_t* pairs,
+                                    const float* points, const uint8_t* valid, int n, int32_t* new_mp, int* n_new);
+int vio_window_triangulate(vio_window* win, vio_ctx* ctx, int32_t kf1_id, int32_t kf2_id, int* n_new);
+/* queries */
+int vio_window_keyframes(const vio_window* win, int32_t* frame_ids, int cap, int* n);   /* oldest first */
+int vio_window_num_mappoints(const vio_window* win);
+int vio_window_mappoint(const vio_window* win, int32_t mp, vio_window_mappoint_info* info);
+/* MapPoint::GetObservations() in order: (frame id, feature index) pairs */
+int vio_window_mappoint_observations(const vio_window* win, int32_t mp, int32_t* frame_ids, int32_t* feats, int cap,
+                                     int* n);
+int vio_window_frame_mappoints(const vio_window* win, int32_t frame_id, int32_t* mp, int cap, int* n);
+/* BA over the window: a vio_map_view of the window's keyframes (oldest first) and every MapPoint
+   (arrays owned by the window, valid until its next mutating call), for vio_ba_gather /
+   vio_ba_write_back; then the write-back applied to the window (frame poses, MapPoint positions,
+   SetBad) */
+int vio_window_map_view(vio_window* win, int height, int boundary_margin, vio_map_view* view);
+int vio_window_apply_update(vio_window* win, const vio_ba_map_update* upd);
 
 #ifdef __cplusplus
 }

@@ -59,6 +59,13 @@ STRUCTS = {
     "vio_mono_init_result": ("VioMonoInitResult", ["status", "best_hypothesis", "num_inliers", "pose_candidate",
                                                    "candidate_good", "num_triangulated", "num_valid",
                                                    "mean_reproj_error", "scale_factor", "E", "R", "t"]),
+    "vio_window_frame": ("VioWindowFrame", ["frame_id", "num_features", "width", "T_wb", "T_bc", "feature_id", "uv",
+                                            "bearing", "valid", "mappoint", "track_begin", "track_frame",
+                                            "track_feat"]),
+    "vio_window_kf_stats": ("VioWindowKfStats", ["obs_added", "transferred", "deleted", "removed_frame",
+                                                 "num_keyframes"]),
+    "vio_window_mappoint_info": ("VioWindowMappointInfo", ["pos", "bad", "marginalized", "triangulated",
+                                                           "reference_frame", "num_observations"]),
     "vio_ba_map_update": ("VioBaMapUpdate", ["frame_Twb", "frame_set", "frame_vel", "bias", "mp_pos", "mp_set",
                                              "mp_set_bad", "success", "num_inliers", "num_outliers",
                                              "num_poses_optimized", "num_points_optimized", "num_iterations",
