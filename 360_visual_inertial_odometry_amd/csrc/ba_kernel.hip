@@ -1263,6 +1263,123 @@ __device__ __forceinline__ bool cholesky_solve(BaShared& sh, int nf, Stamp stamp
     return true;
 }
 
+// Phase-route variant of cholesky_solve for nf % 16 != 0 (ph_solve): the right-hand side is carried
+// as row nf of S (columns < nf; S[nf][nf] = kRhsPivot, the padding rows below it identity), so the
+// factorisation itself produces y = L^-1 b as L[nf][0..nf) (the forward substitution runs in the
+// panels / trailing updates / diagonal tiles; the diagonal tiles are overwritten with their L).  One-step look-ahead: after the panel of column J,
+// wave 0 updates the next diagonal tile and factors it while the other waves apply the rest of
+// column J's trailing update (two workgroup barriers per tile column).  Then the backward solve as
+// in cholesky_solve.  Returns false (uniformly) when a pivot of rows < nf is not positive.
+constexpr double kRhsPivot = 1e300;
+template <typename Stamp = NoStamp>
+__device__ __forceinline__ bool cholesky_solve_rhs(BaShared& sh, int nf, Stamp stamp = Stamp()) {
+    double* S = sh.S;
+    double* LB = sh.stage;  // [nb][16 m][16 c] = Linv_J[c][m]
+    double* LT = sh.stage + 256 * ((BA_NF_MAX + 15) >> 4);
+    double* TB = LT + 256;
+    const int ls = s_ld(nf), nb = (nf + 15) >> 4;
+    constexpr int NW = BA_THREADS / 64;
+    const int wid = wave_id(), lane = threadIdx.x & 63;
+    const int r16 = lane & 15, kk = lane >> 4;
+    // trailing update of the lower tile (I, K) by column J
+    auto trail = [&](int I, int Kt, int J) {
+        const int c0 = 16 * J;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        const double* Ai = S + 16 * I * ls + c0;
+        const double* Bk = S + 16 * Kt * ls + c0;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const double a = Ai[r16 * ls + 4 * st + kk];
+            const double bb = Bk[r16 * ls + 4 * st + kk];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+        }
+        double* C = S + 16 * I * ls + 16 * Kt;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C[(kk + 4 * r) * ls + r16] -= acc[r];
+    };
+    if (wid == 0) {
+        const int bad = chol16_wave<true>(S, ls, LB, LT, lane, min(16, nf));
+        if (lane == 0) sh.chol_bad = bad;
+    }
+    __syncthreads();
+    stamp(8);
+    if (sh.chol_bad) return false;
+    for (int J = 0; J < nb; ++J) {
+        const int c0 = 16 * J;
+        // panel: L_IJ = S_IJ Linv_J^T
+        const double* lb = LB + 256 * J;
+        for (int I = J + 1 + wid; I < nb; I += NW) {
+            d4 acc = {0.0, 0.0, 0.0, 0.0};
+            double* A = S + 16 * I * ls + c0;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const double a = A[r16 * ls + 4 * st + kk];
+                const double bb = lb[(4 * st + kk) * 16 + r16];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[(kk + 4 * r) * ls + r16] = acc[r];
+        }
+        __syncthreads();
+        stamp(9);
+        if (J + 1 == nb) break;
+        if (wid == 0) {
+            // look-ahead: the next diagonal tile, updated by column J, then factored
+            trail(J + 1, J + 1, J);
+            wave_lds_sync();
+            const int bad = chol16_wave<true>(S + (c0 + 16) * ls + c0 + 16, ls, LB + 256 * (J + 1), LT, lane,
+                                               min(16, nf - c0 - 16));
+            if (lane == 0) sh.chol_bad = bad;
+        } else {
+            // the rest of column J's trailing update: lower tiles (I, K), J < K <= I < nb, except (J+1, J+1)
+            const int m = nb - J - 1, nt = m * (m + 1) / 2;
+            for (int t = wid; t < nt; t += NW - 1) {
+                int I = 0, tt = t;
+                while (tt > I) { tt -= I + 1; ++I; }
+                if (I == 0) continue;  // tile (J+1, J+1): wave 0
+                trail(I + J + 1, tt + J + 1, J);
+            }
+        }
+        __syncthreads();
+        stamp(10);
+        if (sh.chol_bad) return false;
+    }
+    // y = L^-1 b is row nf of L; the backward solve x_J = Linv_J^T (y_J - sum_{K>J} L_KJ^T x_K) by wave 0
+    if (wid == 0) {
+        double* y = sh.b;
+        for (int f = lane; f < 16 * nb; f += 64) y[f] = f < nf ? S[nf * ls + f] : 0.0;
+        wave_lds_sync();
+        stamp(11);
+        for (int J = nb - 1; J >= 0; --J) {
+            double p0 = 0.0, p1 = 0.0;
+            int cix = 16 * (J + 1) + kk;
+            const int cend = 16 * nb;
+            for (; cix + 4 < cend; cix += 8) {
+                p0 += S[cix * ls + 16 * J + r16] * y[cix];
+                p1 += S[(cix + 4) * ls + 16 * J + r16] * y[cix + 4];
+            }
+            if (cix < cend) p0 += S[cix * ls + 16 * J + r16] * y[cix];
+            double t = p0 + p1;
+            t += __shfl_xor(t, 16, 64);
+            t += __shfl_xor(t, 32, 64);
+            t = y[16 * J + r16] - t;
+            const double* lb = LB + 256 * J;
+            if (kk == 0) TB[r16] = t;
+            wave_lds_sync();
+            double v = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v += lb[16 * r16 + kk + 4 * q] * TB[kk + 4 * q];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            if (kk == 0) y[16 * J + r16] = v;
+            wave_lds_sync();
+        }
+        stamp(12);
+    }
+    __syncthreads();
+    return true;
+}
+
 // One LM step computation (ComputeTrustRegionStep): returns validity uniformly via sh.st.valid.
 __device__ __forceinline__ void compute_step(BaShared& sh, const WinCtx& c) {
     const BaWin& w = *c.w;

@@ -34,8 +34,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   lbt[16 m + c] = Linv[c][m]   (L^-1 transposed, the B operand of the panel MFMAs)
 //   A            <- L (lower, zeros above) when WRITE_L
 // using lt[256] as scratch.  Returns nonzero (the same on every lane) if a pivot is not positive.
+// Pivots of rows >= nvalid are not checked (a right-hand-side row carried through the factorisation).
 template <bool WRITE_L>
-__device__ __forceinline__ int chol16_wave(double* A, int ld, double* lbt, double* lt, int lane) {
+__device__ __forceinline__ int chol16_wave(double* A, int ld, double* lbt, double* lt, int lane, int nvalid = 16) {
     const int i = lane & 15, kk = lane >> 4;
     double d[16], il[16];
     const double* row = A + i * ld;
@@ -45,7 +46,7 @@ __device__ __forceinline__ int chol16_wave(double* A, int ld, double* lbt, doubl
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const double piv = readlane_d(d[j], j);
-        bad |= !(piv > 0.0);
+        bad |= j < nvalid && !(piv > 0.0);
         const double r = rsq_nr(piv);
         il[j] = r;
         const double cj = i == j ? piv * r : d[j] * r;
