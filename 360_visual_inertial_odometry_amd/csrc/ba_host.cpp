@@ -22,7 +22,7 @@ namespace vio360 {
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream);
 hipError_t launch_ba_pack(const BaPools& P, int n, uint8_t* dst, int64_t rec_bytes, hipStream_t stream);
 hipError_t launch_ba_phases(const BaPools& P, const BaWin* hw, int n, hipStream_t stream);
-size_t ba_phase_doubles(int K, int L, int N, int T);
+size_t ba_phase_doubles(int K, int L, int N, int T);  // sized for the smallest group (most partials)
 const char* ba_phases_failed_launch();
 hipError_t ba_phases_prepare(const BaWin* hw, int n);
 bool global_ba_applicable(const vio_ba_problem& p);
@@ -262,6 +262,11 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
 #define UP(vec, field, type)                                                  \
     if ((rc = up(vec.data(), bytes_of(vec), &ptr)) != VIO_OK) return rc;      \
     d.P.field = (type)ptr;
+    // landmark chunks per Schur split-k group (phase route): a full config-4 shard (>= 256 windows)
+    // fills the chip with 2 groups per window and halves ph_solve's partial sums; smaller batches keep
+    // more, shorter groups (latency)
+    const int gs = pk.win.size() >= 256 ? 10 : 5;
+    for (BaWin& w : pk.win) w.gs = gs;
     UP(pk.win, win, const BaWin*);
     UP(pk.pose_raw, pose_raw, const double*);
     UP(pk.kf_const, kf_const, const uint8_t*);

@@ -20,6 +20,7 @@ struct BaWin {
     int32_t K, L, N, variant;
     int32_t nf, np, npad, T;     // reduced size, pose rows (6*P), padded pose rows (16*T), tile
     int32_t ni;                  // imu-space size nf - np
+    int32_t gs;                  // phase route: landmark chunks per Schur group (set per batch at upload)
     int32_t max_iter, fixed_iter, rounds;
     int32_t is_vi, is_pnp, n_imu, tr_cap; // tr_cap: Summary::iterations entries kept (out_trace)
     int32_t pose_f[BA_KMAX];     // f-offset of pose k or -1 (constant / unused)

@@ -1036,11 +1036,16 @@ __global__ void __launch_bounds__(256) gftt_cand_kernel(GfArgs G) {
 // One workgroup.  Accepted corners live in a grid of cell = round(min_dist) with <= 3 per cell.
 constexpr int GS_THREADS = 256;
 constexpr int GS_SLOTS = 3;
-template <bool GLOBAL_GRID>
+// HASH: the batch's survivors are also chained per grid cell (head[cell] -> s_next[rank], dynamic LDS
+// after the grid), so a survivor compares only with the survivors of its 3x3 cells (every pair within
+// min_dist lies there, as for the grid test) and the insertion walks only its own cell: the same
+// conflict masks and slots as the all-pairs walks, in O(cell occupancy) instead of O(batch).
+template <bool GLOBAL_GRID, bool HASH>
 __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const unsigned long long* keys,
                                                                   const unsigned int* n_keys, unsigned int cap,
                                                                   int fast) {
     extern __shared__ uint32_t grid_lds[];
+    __shared__ int s_next[GS_THREADS];
     __shared__ int s_good[GS_THREADS];
     __shared__ unsigned int s_idx[GS_THREADS];  // the batch's candidate addresses
     __shared__ unsigned int s_sv[GS_THREADS];   // survivors of the pre-filter, batch order: y << 16 | x
@@ -1055,7 +1060,10 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
     __shared__ int s_stop;
     uint32_t* grid = GLOBAL_GRID ? G.grid_global : grid_lds;  // static address space (no flat access)
     const int ncell = G.gw * G.gh;
+    int* head = reinterpret_cast<int*>(grid_lds + (GLOBAL_GRID ? 0 : ncell * GS_SLOTS));
     for (int e = threadIdx.x; e < ncell * GS_SLOTS; e += GS_THREADS) grid[e] = 0xffffffffu;
+    if (HASH)
+        for (int e = threadIdx.x; e < ncell; e += GS_THREADS) head[e] = -1;
     if (threadIdx.x == 0) { s_acc = 0; s_stop = 0; }
     __syncthreads();
     const unsigned int total = min(*n_keys, cap);
@@ -1082,6 +1090,7 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
 #ifdef GFTT_DEBUG
     unsigned long long t_start = __builtin_amdgcn_s_memtime(), t_pre = 0, t_mask = 0, t_greedy = 0, tq;
     int nb_dbg = 0, nsv_dbg = 0;
+    unsigned long long dbgv[4][4] = {};
 #endif
     for (unsigned int c0 = 0; c0 < total; c0 += GS_THREADS) {
         // (1) parallel pre-filter against the corners accepted in earlier batches
@@ -1095,7 +1104,9 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
         s_good[threadIdx.x] = good;
         __syncthreads();
 #ifdef GFTT_DEBUG
-        tq = __builtin_amdgcn_s_memtime(); t_pre += tq - t_start; t_start = tq;
+        tq = __builtin_amdgcn_s_memtime(); t_pre += tq - t_start;
+        if (nb_dbg < 4) dbgv[nb_dbg][0] = tq - t_start;
+        t_start = tq;
 #endif
         // (2) in-order resolution inside the batch.  Survivors of (1) are compacted (batch order);
         // survivor r gets a bitmask of the earlier survivors within min_dist of it; thread 0 walks
@@ -1120,9 +1131,29 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
                 y = (int)(idx / G.W);
                 s_sv[rank] = ((unsigned int)y << 16) | (unsigned int)x;
                 s_cell[rank] = (y / cell) * G.gw + x / cell;
+                if (HASH) s_next[rank] = atomicExch(&head[s_cell[rank]], rank);
             }
             __syncthreads();
-            if (good) {
+            if (HASH && good) {
+                unsigned long long m[GS_THREADS / 64];
+#pragma unroll
+                for (int q = 0; q < GS_THREADS / 64; ++q) m[q] = 0ull;
+                const int xc = x / cell, yc = y / cell;
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        const int xx = xc + dx, yy = yc + dy;
+                        if (xx < 0 || yy < 0 || xx >= G.gw || yy >= G.gh) continue;
+                        for (int bq = head[yy * G.gw + xx]; bq >= 0; bq = s_next[bq]) {
+                            if (bq >= rank) continue;
+                            const unsigned int pj = s_sv[bq];
+                            const float ddx = (float)x - (float)(pj & 0xffff), ddy = (float)y - (float)(pj >> 16);
+                            if ((double)(ddx * ddx + ddy * ddy) < md2) m[bq >> 6] |= 1ull << (bq & 63);
+                        }
+                    }
+#pragma unroll
+                for (int q = 0; q < GS_THREADS / 64; ++q) s_conf[rank][q] = m[q];
+            }
+            if (!HASH && good) {
 #pragma unroll
                 for (int q = 0; q < GS_THREADS / 64; ++q) {  // word q of the mask stays in a register
                     unsigned long long m = 0ull;
@@ -1138,7 +1169,7 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
             }
             __syncthreads();
 #ifdef GFTT_DEBUG
-            tq = __builtin_amdgcn_s_memtime(); t_mask += tq - t_start; t_start = tq;
+            tq = __builtin_amdgcn_s_memtime(); t_mask += tq - t_start; if (nb_dbg < 5 && nb_dbg > 0) dbgv[nb_dbg - 1][1] = tq - t_start; t_start = tq;
 #endif
             // greedy in batch order, resolved in rounds: a survivor is accepted once none of its earlier
             // conflicting survivors can still be accepted (all decided rejected), rejected once one of
@@ -1170,6 +1201,11 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
                 }
                 __syncthreads();
             }
+#ifdef GFTT_DEBUG
+            tq = __builtin_amdgcn_s_memtime(); t_greedy += tq - t_start;
+            if (nb_dbg < 5 && nb_dbg > 0) dbgv[nb_dbg - 1][2] = tq - t_start;
+            t_start = tq;
+#endif
             // max_corners: keep the first (max_corners - s_acc) accepted in order
             if (threadIdx.x == 0 && G.max_corners > 0) {
                 int room = G.max_corners - s_acc;
@@ -1203,11 +1239,19 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
                 G.corners[2 * kk + 1] = (float)y;
                 const int mycell = s_cell[rank];
                 int i_cell = 0, m_cell = 0;
-                for (int r = 0; r < nsv; ++r) {
-                    if (!((s_am[r >> 6] >> (r & 63)) & 1ull)) continue;
-                    if (s_cell[r] == mycell) {
+                if (HASH) {
+                    for (int r = head[mycell]; r >= 0; r = s_next[r]) {
+                        if (!((s_am[r >> 6] >> (r & 63)) & 1ull)) continue;
                         if (r < rank) ++i_cell;
                         ++m_cell;
+                    }
+                } else {
+                    for (int r = 0; r < nsv; ++r) {
+                        if (!((s_am[r >> 6] >> (r & 63)) & 1ull)) continue;
+                        if (s_cell[r] == mycell) {
+                            if (r < rank) ++i_cell;
+                            ++m_cell;
+                        }
                     }
                 }
                 uint32_t* cellp = &grid[mycell * GS_SLOTS];
@@ -1220,7 +1264,14 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
             __syncthreads();
             if (good && ((s_am[rank >> 6] >> (rank & 63)) & 1ull) && s_slot_idx[rank] >= 0)
                 grid[s_slot_idx[rank]] = s_slot_val[rank];
+            if (HASH && good) head[s_cell[rank]] = -1;  // every chain of the batch emptied (read above)
             if (threadIdx.x == 0) s_acc = nacc_before + nacc;
+#ifdef GFTT_DEBUG
+            __syncthreads();
+            tq = __builtin_amdgcn_s_memtime();
+            if (nb_dbg < 5 && nb_dbg > 0) dbgv[nb_dbg - 1][3] = tq - t_start;
+            t_start = tq;
+#endif
         }
         __syncthreads();
         if (s_stop) break;
@@ -1229,6 +1280,9 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
     if (threadIdx.x == 0)
         printf("gftt_select: total %u batches %d survivors %d pre %llu mask %llu greedy %llu rest %llu\n", total, nb_dbg, nsv_dbg,
                t_pre, t_mask, t_greedy, __builtin_amdgcn_s_memtime() - t_start);
+    if (threadIdx.x == 0)
+        for (int q = 0; q < 2; ++q)
+            printf("gftt_select batch %d: pre %llu mask %llu rounds %llu insert %llu\n", q, dbgv[q][0], dbgv[q][1], dbgv[q][2], dbgv[q][3]);
 #endif
     if (threadIdx.x == 0) {
         *G.n_out = s_acc;
@@ -1778,26 +1832,40 @@ static hipError_t gftt_candidates(const GfArgs& g, hipStream_t st) {
     hipLaunchKernelGGL(gftt_cand_kernel, grd, dim3(256), 0, st, g);
     return hipGetLastError();
 }
-static size_t gftt_select_lds(const GfArgs& g) {
-    return g.grid_global ? 0 : (size_t)g.gw * g.gh * GS_SLOTS * sizeof(uint32_t);
+static size_t gftt_select_lds(const GfArgs& g, bool hash) {
+    const size_t ncell = (size_t)g.gw * g.gh;
+    return (g.grid_global ? 0 : ncell * GS_SLOTS * sizeof(uint32_t)) + (hash ? ncell * sizeof(int) : 0);
 }
-// fast path: candidates -> histogram -> top-K compaction -> sort of topk_cap keys -> greedy
+// greedy selection over n_keys sorted keys: the cell-chained variant when its chain heads fit next to
+// the grid in LDS, else the all-pairs walks
+static hipError_t launch_select(const GfArgs& g, const unsigned long long* keys, const unsigned int* n_keys,
+                                unsigned int cap, int fast, hipStream_t st) {
+    const bool hash = gftt_select_lds(g, true) <= GF_SELECT_LDS_MAX;
+    const size_t lds = gftt_select_lds(g, hash);
+    if (g.grid_global) {
+        if (hash) hipLaunchKernelGGL((gftt_select_kernel<true, true>), dim3(1), dim3(GS_THREADS), lds, st, g, keys, n_keys, cap, fast);
+        else hipLaunchKernelGGL((gftt_select_kernel<true, false>), dim3(1), dim3(GS_THREADS), lds, st, g, keys, n_keys, cap, fast);
+    } else {
+        if (hash) hipLaunchKernelGGL((gftt_select_kernel<false, true>), dim3(1), dim3(GS_THREADS), lds, st, g, keys, n_keys, cap, fast);
+        else hipLaunchKernelGGL((gftt_select_kernel<false, false>), dim3(1), dim3(GS_THREADS), lds, st, g, keys, n_keys, cap, fast);
+    }
+    return hipGetLastError();
+}
+// descending radix sort of the top-K buffer (topk_cap keys; unused slots hold 0 and sort to the end)
+static hipError_t gftt_sort_topk(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {
+    size_t tb = sort_tmp_bytes;
+    return hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.topk, g.topk_sorted, (int)g.topk_cap, 0, 64, st);
+}
+// fast path: candidates -> histogram -> top-K compaction -> sort of the top-K keys -> greedy
 hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {
     hipError_t e = gftt_candidates(g, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(gftt_hist_kernel, dim3(256), dim3(256), 0, st, g);
     hipLaunchKernelGGL(gftt_cut_kernel, dim3(1), dim3(GC_THREADS), 0, st, g);
     hipLaunchKernelGGL(gftt_topk_compact_kernel, dim3(256), dim3(256), 0, st, g);
-    size_t tb = sort_tmp_bytes;
-    e = hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.topk, g.topk_sorted, (int)g.topk_cap, 0, 64, st);
+    e = gftt_sort_topk(g, sort_tmp, sort_tmp_bytes, st);
     if (e != hipSuccess) return e;
-    if (g.grid_global)
-        hipLaunchKernelGGL(gftt_select_kernel<true>, dim3(1), dim3(GS_THREADS), 0, st, g,
-                           (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
-    else
-        hipLaunchKernelGGL(gftt_select_kernel<false>, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
-                           (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
-    return hipGetLastError();
+    return launch_select(g, (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1, st);
 }
 hipError_t launch_gftt_lmax(const GfArgs& g, hipStream_t st) {
     hipLaunchKernelGGL(gftt_lmax_kernel, dim3(g.tiles_x, g.tiles_y), dim3(256), 0, st, g);
@@ -1812,17 +1880,9 @@ hipError_t launch_gftt_after_lmax(const GfArgs& g, void* sort_tmp, size_t sort_t
     hipLaunchKernelGGL(gftt_lm_hist_kernel, dim3(256), dim3(256), 0, st, g);
     hipLaunchKernelGGL(gftt_cut_kernel, dim3(1), dim3(GC_THREADS), 0, st, g);
     hipLaunchKernelGGL(gftt_lm_topk_kernel, dim3(256), dim3(256), 0, st, g);
-    size_t tb = sort_tmp_bytes;
-    hipError_t e =
-        hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.topk, g.topk_sorted, (int)g.topk_cap, 0, 64, st);
+    hipError_t e = gftt_sort_topk(g, sort_tmp, sort_tmp_bytes, st);
     if (e != hipSuccess) return e;
-    if (g.grid_global)
-        hipLaunchKernelGGL(gftt_select_kernel<true>, dim3(1), dim3(GS_THREADS), 0, st, g,
-                           (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
-    else
-        hipLaunchKernelGGL(gftt_select_kernel<false>, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
-                           (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1);
-    return hipGetLastError();
+    return launch_select(g, (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1, st);
 }
 hipError_t launch_gftt_flatten(const GfArgs& g, hipStream_t st) {
     hipLaunchKernelGGL(gftt_lm_flatten_kernel, dim3(256), dim3(256), 0, st, g);
@@ -1837,13 +1897,7 @@ hipError_t launch_gftt_full(const GfArgs& g, unsigned int count, void* sort_tmp,
     hipError_t e = hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.cand, g.cand_sorted, (int)count, 0, 64,
                                                                st);
     if (e != hipSuccess) return e;
-    if (g.grid_global)
-        hipLaunchKernelGGL(gftt_select_kernel<true>, dim3(1), dim3(GS_THREADS), 0, st, g,
-                           (const unsigned long long*)g.cand_sorted, (const unsigned int*)g.n_cand, g.cand_cap, 0);
-    else
-        hipLaunchKernelGGL(gftt_select_kernel<false>, dim3(1), dim3(GS_THREADS), gftt_select_lds(g), st, g,
-                           (const unsigned long long*)g.cand_sorted, (const unsigned int*)g.n_cand, g.cand_cap, 0);
-    return hipGetLastError();
+    return launch_select(g, (const unsigned long long*)g.cand_sorted, (const unsigned int*)g.n_cand, g.cand_cap, 0, st);
 }
 size_t gftt_sort_tmp_bytes(unsigned int cap) {
     size_t tb = 0;
@@ -1852,7 +1906,13 @@ size_t gftt_sort_tmp_bytes(unsigned int cap) {
     return tb;
 }
 hipError_t gftt_select_set_lds(size_t bytes) {
-    return hipFuncSetAttribute((const void*)gftt_select_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    const void* fns[4] = {(const void*)gftt_select_kernel<false, false>, (const void*)gftt_select_kernel<false, true>,
+                          (const void*)gftt_select_kernel<true, false>, (const void*)gftt_select_kernel<true, true>};
+    for (const void* f : fns) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace vio360

@@ -134,7 +134,7 @@ int ensure_iters(erp_tracker* t, int iters) {
 
 // the GFTT selection grid (3 slots x 4 B per min-distance cell) lives in LDS up to this size, next
 // to the selection kernel's ~14 KB of static LDS (config 1: 128 x 64 cells = 96 KB)
-constexpr size_t kSelectGridLds = 140 * 1024;
+constexpr size_t kSelectGridLds = GF_SELECT_LDS_MAX;
 
 int ensure_gftt(erp_tracker* t, double min_dist) {
     int rc;
@@ -146,7 +146,7 @@ int ensure_gftt(erp_tracker* t, double min_dist) {
         if ((rc = dalloc(t, &t->d_cand_sorted, sizeof(unsigned long long) * t->cand_cap)) != VIO_OK) return rc;
         t->sort_tmp_bytes = gftt_sort_tmp_bytes(t->cand_cap);
         if ((rc = dalloc(t, (char**)&t->d_sort_tmp, t->sort_tmp_bytes)) != VIO_OK) return rc;
-        t->topk_cap = std::min<unsigned int>(65536u, t->cand_cap);
+        t->topk_cap = std::min<unsigned int>(GF_TOPK_CAP, t->cand_cap);
         if ((rc = dalloc(t, &t->d_hist, sizeof(unsigned int) * GF_BUCKETS)) != VIO_OK) return rc;
         if ((rc = dalloc(t, &t->d_topk, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
         if ((rc = dalloc(t, &t->d_topk_sorted, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
@@ -158,6 +158,11 @@ int ensure_gftt(erp_tracker* t, double min_dist) {
         if ((rc = dalloc(t, &t->d_tile_max, sizeof(uint32_t) * nt)) != VIO_OK) return rc;
         if ((rc = dalloc(t, &t->d_tile_dirty, nt)) != VIO_OK) return rc;
         if ((rc = dalloc(t, &t->d_tile_kmax, sizeof(uint32_t) * nt)) != VIO_OK) return rc;
+        // dynamic-LDS limit of the single-workgroup selection kernel, once per tracker (its device is
+        // current here): the selection grid and chain heads up to kSelectGridLds (larger grids live in
+        // d_grid)
+        hipError_t e = gftt_select_set_lds(kSelectGridLds);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "hipFuncSetAttribute(gftt_select)");
     }
     if (min_dist >= 1) {
         int cell = (int)std::lrint(min_dist);
@@ -331,10 +336,6 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     g.grid_global = lds > kSelectGridLds ? t->d_grid : nullptr;
     g.corners = t->d_corners;
     g.n_out = t->d_scal + 4;
-    if (!g.grid_global) {
-        hipError_t e = gftt_select_set_lds(std::max<size_t>(lds, 4));
-        if (e != hipSuccess) return hip_fail(t->ctx, e, "hipFuncSetAttribute(gftt_select)");
-    }
     g.hist = t->d_hist;
     g.topk = t->d_topk;
     g.topk_sorted = t->d_topk_sorted;

@@ -100,6 +100,12 @@ struct GfArgs {
 constexpr int LM_TX = 64, LM_TY = 32, LM_CAP = 1024;
 
 constexpr int GF_BUCKETS = 2048;    // float bits >> 20 of a positive response
+// top-K buffer: the strongest candidates (>= 16 x max_corners of them when the buckets allow) sorted
+// for the greedy selection; a selection that runs dry falls back to the full candidate sort
+constexpr unsigned int GF_TOPK_CAP = 16384;
+// dynamic LDS of the greedy selection (grid of 3 slots x 4 B per min-distance cell, + 4 B chain head per
+// cell), next to its ~15 KB of static LDS; larger grids live in global memory
+constexpr size_t GF_SELECT_LDS_MAX = 140 * 1024;
 
 struct DiscArgs {
     const float* pts;       // [n][2]
