@@ -713,6 +713,9 @@ __global__ void __launch_bounds__(256) ransac_hyp_kernel(RansacArgs R) {
     }
     float Rm[9];
     kabsch_rotation(Hm, Rm);
+#pragma unroll
+    for (int i = 0; i < 9; ++i)  // ransac_select reads the best one back
+        if (lane == i) R.rot[9 * it + i] = Rm[i];
     if (fabsf(det3f(Rm) - 1.0f) > 0.1f) {
         if (lane == 0) R.count[it] = -1;
         return;
@@ -751,16 +754,8 @@ __global__ void __launch_bounds__(256) ransac_select_kernel(RansacArgs R) {
     const int bit = sidx[0];
     if (threadIdx.x == 0) {
         *R.n_in = n < 3 ? n : sbest[0];
-        if (bit >= 0) {
-            float Hm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-            for (int s = 0; s < 3; ++s) {
-                int k = R.samples[3 * bit + s];
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c) Hm[3 * r + c] += R.b1[3 * k + r] * R.b0[3 * k + c];
-            }
-            kabsch_rotation(Hm, Rs);
-        }
     }
+    if (bit >= 0 && threadIdx.x < 9) Rs[threadIdx.x] = R.rot[9 * bit + threadIdx.x];  // ransac_hyp's rotation
     __syncthreads();
     for (int j = threadIdx.x; j < n; j += 256) {
         uint8_t m = 1;

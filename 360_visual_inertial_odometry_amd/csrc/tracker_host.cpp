@@ -56,6 +56,7 @@ struct erp_tracker {
     float *d_pts = nullptr, *d_next = nullptr, *d_err = nullptr, *d_b0 = nullptr, *d_b1 = nullptr;
     uint8_t *d_status = nullptr, *d_kept = nullptr;
     int *d_gidx = nullptr, *d_count = nullptr;
+    float* d_rot = nullptr;
     int32_t* d_samples = nullptr;
     int iters_cap = 0;
     int n_pts = 0;
@@ -128,6 +129,7 @@ int ensure_iters(erp_tracker* t, int iters) {
     int rc;
     if ((rc = dalloc(t, &t->d_samples, sizeof(int32_t) * 3 * cap)) != VIO_OK) return rc;
     if ((rc = dalloc(t, &t->d_count, sizeof(int) * cap)) != VIO_OK) return rc;
+    if ((rc = dalloc(t, &t->d_rot, sizeof(float) * 9 * cap)) != VIO_OK) return rc;
     t->iters_cap = cap;
     return VIO_OK;
 }
@@ -280,7 +282,7 @@ RansacArgs ransac_args(erp_tracker* t, int n, int mode, int iters, uint32_t seed
     r.b0 = t->d_b0; r.b1 = t->d_b1;
     r.samples = t->d_samples; r.iters = iters; r.seed = seed; r.thresh = thr;
     r.raw = t->d_raw;
-    r.count = t->d_count; r.kept = t->d_kept; r.n_in = t->d_scal + 1;
+    r.count = t->d_count; r.rot = t->d_rot; r.kept = t->d_kept; r.n_in = t->d_scal + 1;
     return r;
 }
 

@@ -49,6 +49,7 @@ struct RansacArgs {
     uint32_t seed;
     float thresh;
     int* count;            // [iters]
+    float* rot;            // [iters][9] each hypothesis' rotation (ransac_hyp), read back for the best
     uint8_t* kept;         // [n] output mask in input order
     int* n_in;             // device scalar
 };

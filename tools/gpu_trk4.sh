@@ -11,7 +11,3 @@ cat gpurun_out/trk_time.log
 rm -rf gpurun_out/trkprof
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/trkprof -o trk --output-format csv -- python3 tools/trk_time.py 5 > gpurun_out/trk_prof.log 2>&1 || exit 1
 echo prof ok
-for g in 3 10; do
-  VIO360_LIB=tools/probe/libvio360_gs$g.so timeout -k 10 200 python3 tools/ba_quick.py > gpurun_out/ba_quick_gs$g.log 2>&1 || exit 1
-  echo "PH_GS=$g"; grep -E "windows=" gpurun_out/ba_quick_gs$g.log
-done
