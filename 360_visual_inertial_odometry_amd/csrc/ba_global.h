@@ -60,7 +60,7 @@ struct GbaArgs {
     double* Linv;             // [nfp/64][64][64]
     hipStream_t side;         // look-ahead stream of the Cholesky (nullptr: plain schedule)
     hipEvent_t ev[2];
-    int* flags;               // [32 (2 nfp/64 + 1)] persistent triangular-solve flags, one per 128 B (+ timeout word)
+    int* flags;               // [32 (3 nfp/64 + 1)] triangular-solve flags, one per 128 B (+ timeout word), Cholesky step flags
 };
 
 hipError_t gba_launch_setup(const GbaArgs& A, hipStream_t s);
@@ -69,6 +69,7 @@ hipError_t gba_launch_eval(const GbaArgs& A, const double* xp, const double* xl,
                            double* out, hipStream_t s);
 hipError_t gba_launch_linearise(const GbaArgs& A, int first, double* partial, double* out_gmax, hipStream_t s);
 hipError_t gba_launch_step_prep(const GbaArgs& A, double radius, double* partial, double* out_bad, hipStream_t s);
+hipError_t gba_cholesky_attributes();
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s);
 hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s);
 hipError_t gba_launch_backsub(const GbaArgs& A, double* partial, double* out_nonfinite, hipStream_t s);

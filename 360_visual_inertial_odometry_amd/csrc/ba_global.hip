@@ -20,6 +20,8 @@
 #include <float.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "ba_factor_dev.h"
 #include "ba_global.h"
 #include "chol_dev.h"
@@ -376,45 +378,40 @@ using d4 = __attribute__((ext_vector_type(4))) double;
 // X_IJ = -Linv_II sum_{J<=K<I} L_IK X_KJ, again on MFMA.  Dynamic LDS: CHOL_DIAG_LDS bytes.
 constexpr int TLD = NB + 1;  // odd row stride: the column reads of the MFMA operands spread over banks
 constexpr size_t CHOL_DIAG_LDS = sizeof(double) * (2 * NB * TLD + 4 * 256 + 256 + 4 * 16 * 17);
-__global__ void __launch_bounds__(256) chol_diag_kernel(double* S, int n, int k, double* Linv, int* fail) {
-    extern __shared__ double dyn[];
-    double* T = dyn;             // [NB][TLD] S_kk, then L_kk
-    double* X = T + NB * TLD;    // [NB][TLD] L_kk^-1
-    double* LB = X + NB * TLD;   // [4][16 m][16 c] = Linv_J[c][m] of the diagonal tiles
-    double* LT = LB + 4 * 256;   // scratch of chol16_wave
-    double* P = LT + 256;        // [4 waves][16][17] product scratch of the inverse
-    __shared__ int bad_s;
-    double* blk = S + (size_t)k * NB * n + (size_t)k * NB;
-    {
-        constexpr int PER = NB * NB / 256;  // loads first, then the LDS stores
-        double v[PER];
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int e = threadIdx.x + 256 * u, r = e >> 6, c = e & 63;
-            v[u] = c <= r ? blk[(size_t)r * n + c] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int e = threadIdx.x + 256 * u, r = e >> 6, c = e & 63;
-            T[r * TLD + c] = v[u];
-            X[r * TLD + c] = 0.0;
-        }
-    }
-    __syncthreads();
+// factor the 64x64 block held in T (lower part, row stride TLD) in place into L and build X = L^-1
+// (X zeroed by the caller); LB / LT / P: scratch as laid out by diag_lds_layout.  Returns nonzero
+// (the same in every thread) when a pivot is not positive.
+__device__ int diag_block_lds(double* T, double* X, double* LB, double* LT, double* P, int& bad_s) {
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int r16 = lane & 15, kk = lane >> 4;
     constexpr int NT = NB / 16;
+    // trailing update of the lower tile (I, K) by tile column J
+    auto trail = [&](int I, int Kt, int J) {
+        const int c0 = 16 * J;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        const double* Ai = T + 16 * I * TLD + c0;
+        const double* Bk = T + 16 * Kt * TLD + c0;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const double a = Ai[r16 * TLD + 4 * st + kk];
+            const double bb = Bk[r16 * TLD + 4 * st + kk];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+        }
+        double* C = T + 16 * I * TLD + 16 * Kt;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C[(kk + 4 * r) * TLD + r16] -= acc[r];
+    };
+    // one-step look-ahead (as the window solver's cholesky_solve_rhs): after the panel of column J,
+    // wave 0 updates and factors the next diagonal tile while the other waves finish column J's
+    // trailing update; each tile still receives its updates in column order
+    if (wid == 0) {
+        const int bad = chol16_wave<true>(T, TLD, LB, LT, lane);
+        if (lane == 0) bad_s = bad;
+    }
+    __syncthreads();
     for (int J = 0; J < NT; ++J) {
         const int c0 = 16 * J;
-        if (wid == 0) {
-            const int bad = chol16_wave<true>(T + c0 * TLD + c0, TLD, LB + 256 * J, LT, lane);
-            if (lane == 0) bad_s = bad;
-        }
-        __syncthreads();
-        if (bad_s) {
-            if (threadIdx.x == 0) *fail = 1;
-            return;
-        }
+        if (bad_s) return 1;
         const double* lb = LB + 256 * J;
         for (int I = J + 1 + wid; I < NT; I += 4) {  // panel
             d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -429,27 +426,23 @@ __global__ void __launch_bounds__(256) chol_diag_kernel(double* S, int n, int k,
             for (int r = 0; r < 4; ++r) A[(kk + 4 * r) * TLD + r16] = acc[r];
         }
         __syncthreads();
-        const int m = NT - J - 1, nt = m * (m + 1) / 2;
-        for (int t = wid; t < nt; t += 4) {  // trailing lower tiles (I, K), J < K <= I
-            int I = 0, tt = t;
-            while (tt > I) { tt -= I + 1; ++I; }
-            const int Kt = tt + J + 1;
-            I += J + 1;
-            d4 acc = {0.0, 0.0, 0.0, 0.0};
-            const double* Ai = T + 16 * I * TLD + c0;
-            const double* Bk = T + 16 * Kt * TLD + c0;
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const double a = Ai[r16 * TLD + 4 * st + kk];
-                const double bb = Bk[r16 * TLD + 4 * st + kk];
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+        if (J + 1 == NT) break;
+        if (wid == 0) {
+            trail(J + 1, J + 1, J);
+            wave_lds_sync();
+            const int bad = chol16_wave<true>(T + (c0 + 16) * TLD + c0 + 16, TLD, LB + 256 * (J + 1), LT, lane);
+            if (lane == 0) bad_s = bad;
+        } else {
+            const int m = NT - J - 1, nt = m * (m + 1) / 2;
+            for (int t = wid; t < nt; t += 3) {  // trailing lower tiles (I, K), J < K <= I, except (J+1, J+1)
+                int I = 0, tt = t;
+                while (tt > I) { tt -= I + 1; ++I; }
+                trail(I + J + 1, tt + J + 1, J);
             }
-            double* C = T + 16 * I * TLD + 16 * Kt;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) C[(kk + 4 * r) * TLD + r16] -= acc[r];
         }
         __syncthreads();
     }
+    if (bad_s) return 1;
     for (int e = threadIdx.x; e < NT * 256; e += 256) {  // diagonal tiles of the inverse
         const int J = e >> 8, q = (e >> 4) & 15, i = e & 15;
         X[(16 * J + q) * TLD + 16 * J + i] = LB[256 * J + 16 * i + q];
@@ -481,6 +474,38 @@ __global__ void __launch_bounds__(256) chol_diag_kernel(double* S, int n, int k,
             for (int r = 0; r < 4; ++r) X[(16 * I + kk + 4 * r) * TLD + 16 * J + r16] = -acc2[r];
         }
         __syncthreads();
+    }
+    return 0;
+}
+
+__global__ void __launch_bounds__(256) chol_diag_kernel(double* S, int n, int k, double* Linv, int* fail) {
+    extern __shared__ double dyn[];
+    double* T = dyn;             // [NB][TLD] S_kk, then L_kk
+    double* X = T + NB * TLD;    // [NB][TLD] L_kk^-1
+    double* LB = X + NB * TLD;   // [4][16 m][16 c] = Linv_J[c][m] of the diagonal tiles
+    double* LT = LB + 4 * 256;   // scratch of chol16_wave
+    double* P = LT + 256;        // [4 waves][16][17] product scratch of the inverse
+    __shared__ int bad_s;
+    double* blk = S + (size_t)k * NB * n + (size_t)k * NB;
+    {
+        constexpr int PER = NB * NB / 256;  // loads first, then the LDS stores
+        double v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = threadIdx.x + 256 * u, r = e >> 6, c = e & 63;
+            v[u] = c <= r ? blk[(size_t)r * n + c] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = threadIdx.x + 256 * u, r = e >> 6, c = e & 63;
+            T[r * TLD + c] = v[u];
+            X[r * TLD + c] = 0.0;
+        }
+    }
+    __syncthreads();
+    if (diag_block_lds(T, X, LB, LT, P, bad_s)) {
+        if (threadIdx.x == 0) *fail = 1;
+        return;
     }
     double* Li = Linv + (size_t)k * NB * NB;
     for (int e = threadIdx.x; e < NB * NB; e += 256) {
@@ -700,6 +725,120 @@ __device__ __forceinline__ void flag_publish(int* f) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store((gint*)f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Fused Cholesky step for block column k (the critical chain of the look-ahead schedule in one
+// launch): workgroup 0 applies column k-1's update to the diagonal block (k, k) and factors it
+// (diag_block_lds), publishing L_kk^-1 through a flag (hand-off as above); workgroup i >= 1 applies
+// column k-1's update to the panel block (k+i, k) while the diagonal block is factored, waits for the
+// flag and multiplies by L_kk^-T.  The arithmetic is chol_syrk_kernel's (part 1), chol_diag_kernel's
+// and chol_trsm_kernel's, in the same order: bitwise the three-launch step.  k == 0: no update.
+// Dynamic LDS: CHOL_DIAG_LDS bytes.  flag: 0 pending, 1 L_kk^-1 final, 2 the block is not positive
+// definite.
+__global__ void __launch_bounds__(256) chol_step_kernel(double* S, int n, int k, double* Linv, int* fail, int* flag) {
+    extern __shared__ double dyn[];
+    double (*As)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(dyn);
+    double (*Bs)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(dyn + NB * TLD);
+    __shared__ int bad_s, ok_s;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r0 = 32 * (wid >> 1), c0 = 32 * (wid & 1);
+    const bool diag = blockIdx.x == 0;
+    const int i = k + (int)blockIdx.x;
+    double* C = S + (size_t)i * NB * n + (size_t)k * NB;
+    double cv[2][2][4];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                cv[ti][tj][q] = (!diag || c <= r) ? C[(size_t)r * n + c] : 0.0;
+            }
+    if (k > 0) {  // C -= A_{i,k-1} A_{k,k-1}^T
+        const double* Aik = S + (size_t)i * NB * n + (size_t)(k - 1) * NB;
+        const double* Ajk = S + (size_t)k * NB * n + (size_t)(k - 1) * NB;
+        stage_tiles(As, Bs, Aik, (size_t)n, Ajk, (size_t)n);
+        __syncthreads();
+        d4 acc[2][2];
+        for (int a = 0; a < 2; ++a)
+            for (int b = 0; b < 2; ++b) acc[a][b] = d4{0, 0, 0, 0};
+        mfma_tile_ABt(As, Bs, acc, wid, lane);
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                    if (!diag || c <= r) cv[ti][tj][q] = cv[ti][tj][q] - acc[ti][tj][q];
+                }
+        __syncthreads();  // every wave is done with As / Bs
+    }
+    // the updated block into As (for the diagonal block: the T area of chol_diag_kernel, upper part 0)
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                As[r][c] = cv[ti][tj][q];
+            }
+    if (diag) {
+        double* T = dyn;
+        double* X = T + NB * TLD;
+        double* LB = X + NB * TLD;
+        double* LT = LB + 4 * 256;
+        double* P = LT + 256;
+        for (int e = threadIdx.x; e < NB * NB; e += 256) X[(e >> 6) * TLD + (e & 63)] = 0.0;
+        __syncthreads();
+        const int bad = diag_block_lds(T, X, LB, LT, P, bad_s);
+        if (!bad) {
+            double* Li = Linv + (size_t)k * NB * NB;
+            for (int e = threadIdx.x; e < NB * NB; e += 256) {
+                const int r = e >> 6, c = e & 63;
+                if (c <= r) C[(size_t)r * n + c] = T[r * TLD + c];
+                st_sc1(Li + e, X[r * TLD + c]);
+            }
+        } else if (threadIdx.x == 0) {
+            *fail = 1;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store((gint*)flag, bad ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (threadIdx.x == 0) {
+        const bool arrived = flag_wait(flag);
+        ok_s = arrived && __hip_atomic_load((gint*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
+        if (!arrived) *fail = 1;
+    }
+    __syncthreads();
+    if (!ok_s) return;
+    {   // L_kk^-1 (published with sc1 stores) into Bs with sc1 loads, all in flight before the LDS stores
+        const double* Li = Linv + (size_t)k * NB * NB;
+        constexpr int PER = NB * NB / 256;
+        double v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) v[u] = ld_sc1(Li + threadIdx.x + 256 * u);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            Bs[e / NB][e % NB] = v[u];
+        }
+    }
+    __syncthreads();
+    d4 acc[2][2];
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0, 0, 0, 0};
+    mfma_tile_ABt(As, Bs, acc, wid, lane);
+    for (int ti = 0; ti < 2; ++ti)
+        for (int tj = 0; tj < 2; ++tj)
+            for (int q = 0; q < 4; ++q) {
+                const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                C[(size_t)r * n + c] = acc[ti][tj][q];
+            }
 }
 
 // Two 64-row blocks per workgroup (TG): a hand-off per pair instead of per block; the second
@@ -1050,12 +1189,18 @@ hipError_t gba_launch_step_prep(const GbaArgs& A, double radius, double* partial
 // factors block k+1 and its panel while the rest of step k's trailing update runs on a side stream;
 // the main stream joins it before the next first-column update.  Every tile sees the same updates
 // in the same k order as the plain schedule (bitwise the same factor).
+// > 64 KB of LDS: opt in, on the current device, before any launch or stream capture of the Cholesky
+hipError_t gba_cholesky_attributes() {
+    hipError_t e = hipFuncSetAttribute((const void*)chol_diag_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)CHOL_DIAG_LDS);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)chol_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)CHOL_DIAG_LDS);
+    return e;
+}
+constexpr int kGbaFuseM = 48;  // chol_step_kernel for steps with at most this many block rows
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
-    // > 64 KB of LDS: opt in (per call: the attribute is per device and the call is host-only)
-    const hipError_t ea = hipFuncSetAttribute((const void*)chol_diag_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)CHOL_DIAG_LDS);
-    if (ea != hipSuccess) return ea;
     hipStream_t r = A.side;
     hipEvent_t ev_panel = A.ev[0], ev_rest = A.ev[1];
     if (!r || !ev_panel || !ev_rest) {  // no side stream: the plain schedule
@@ -1071,26 +1216,39 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
         return hipGetLastError();
     }
     hipError_t e;
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, 0, A.Linv, fail);
-    if (nblk > 1) hipLaunchKernelGGL(chol_trsm_kernel, dim3(nblk - 1), dim3(256), 0, s, A.S, n, 0, (const double*)A.Linv);
-    bool rest_pending = false;
+    // fused steps (chol_step_kernel) once the chain, not the trailing update, bounds a step: panel
+    // workgroups wait for the diagonal block, so early steps (large trailing updates on the side
+    // stream) keep the separate launches
+    static const int fuse_m = [] {
+        const char* v = std::getenv("VIO_GBA_FUSE_M");
+        return v ? std::atoi(v) : kGbaFuseM;
+    }();
+    int* sflag = A.flags + FLAG_STRIDE * (2 * (size_t)nblk + 1);
+    if ((e = hipMemsetAsync(sflag, 0, sizeof(int) * FLAG_STRIDE * (size_t)nblk, s)) != hipSuccess) return e;
+    auto step = [&](int k) {  // column k-1's update of block column k (k > 0), diagonal block k, panel k
+        const int m = nblk - k - 1;
+        if (m + 1 <= fuse_m) {
+            hipLaunchKernelGGL(chol_step_kernel, dim3(m + 1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv, fail,
+                               sflag + FLAG_STRIDE * k);
+            return;
+        }
+        if (k > 0) hipLaunchKernelGGL(chol_syrk_kernel, dim3(m + 1), dim3(256), 0, s, A.S, n, k - 1, 1);
+        hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv, fail);
+        if (m > 0) hipLaunchKernelGGL(chol_trsm_kernel, dim3(m), dim3(256), 0, s, A.S, n, k, (const double*)A.Linv);
+    };
+    step(0);
     for (int k = 0; k + 1 < nblk; ++k) {
         const int m = nblk - k - 1;  // trailing block rows of step k
         if ((e = hipEventRecord(ev_panel, s)) != hipSuccess) return e;  // panel k final
-        hipLaunchKernelGGL(chol_syrk_kernel, dim3(m), dim3(256), 0, s, A.S, n, k, 1);
         if (m >= 2) {
             if ((e = hipStreamWaitEvent(r, ev_panel, 0)) != hipSuccess) return e;
             hipLaunchKernelGGL(chol_syrk_kernel, dim3((unsigned)((long long)(m - 1) * m / 2)), dim3(256), 0, r, A.S, n,
                                k, 2);
             if ((e = hipEventRecord(ev_rest, r)) != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k + 1, A.Linv, fail);
-        if (m - 1 > 0)
-            hipLaunchKernelGGL(chol_trsm_kernel, dim3(m - 1), dim3(256), 0, s, A.S, n, k + 1, (const double*)A.Linv);
-        rest_pending = m >= 2;
-        if (rest_pending && (e = hipStreamWaitEvent(s, ev_rest, 0)) != hipSuccess) return e;
+        step(k + 1);
+        if (m >= 2 && (e = hipStreamWaitEvent(s, ev_rest, 0)) != hipSuccess) return e;
     }
-    (void)rest_pending;
     return hipGetLastError();
 }
 hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -212,7 +213,7 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     uint8_t *d_outl, *d_bad;
     double* d_chi2;
     if ((rc = B.alloc(&partial, 3 * nblk_max + 3 * (size_t)K)) || (rc = B.alloc(&scal, 16)) ||
-        (rc = B.alloc(&dfail, 4)) || (rc = B.alloc(&A.flags, 32 * (2 * ((size_t)nfp / 64) + 1))) || (rc = B.alloc(&d_outl, Ns)) || (rc = B.alloc(&d_bad, Ls)) ||
+        (rc = B.alloc(&dfail, 4)) || (rc = B.alloc(&A.flags, 32 * (3 * ((size_t)nfp / 64) + 1))) || (rc = B.alloc(&d_outl, Ns)) || (rc = B.alloc(&d_bad, Ls)) ||
         (rc = B.alloc(&d_chi2, Ns)))
         return rc;
     // look-ahead stream + events of the Cholesky (released with the solve)
@@ -227,6 +228,38 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     if (hipStreamCreateWithFlags(&A.side, hipStreamNonBlocking) != hipSuccess) A.side = nullptr;
     for (hipEvent_t& e : A.ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    GBA_CHECK(gba_cholesky_attributes());
+    // the Cholesky + triangular solves of a step are the same launches every LM iteration: captured
+    // once (fork / join of the look-ahead stream included) and replayed as one graph
+    static const bool use_graph = [] {
+        const char* v = std::getenv("VIO_GBA_GRAPH");
+        return !(v && v[0] == '0');
+    }();
+    struct GraphGuard {
+        hipGraphExec_t g = nullptr;
+        ~GraphGuard() {
+            if (g) (void)hipGraphExecDestroy(g);
+        }
+    } chol_graph;
+    auto factor_and_solve = [&]() -> hipError_t {
+        if (!use_graph) {
+            hipError_t e = gba_launch_cholesky(A, dfail, st);
+            return e == hipSuccess ? gba_launch_solve(A, st) : e;
+        }
+        if (!chol_graph.g) {
+            hipGraph_t g = nullptr;
+            hipError_t e = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+            if (e != hipSuccess) return e;
+            hipError_t el = gba_launch_cholesky(A, dfail, st);
+            if (el == hipSuccess) el = gba_launch_solve(A, st);
+            e = hipStreamEndCapture(st, &g);
+            if (el != hipSuccess) e = el;
+            if (e == hipSuccess) e = hipGraphInstantiate(&chol_graph.g, g, nullptr, nullptr, 0);
+            if (g) (void)hipGraphDestroy(g);
+            if (e != hipSuccess) return e;
+        }
+        return hipGraphLaunch(chol_graph.g, st);
+    };
     GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));
     GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0.data(), sizeof(double) * 3 * L, hipMemcpyHostToDevice, st));
     GBA_CHECK(gba_launch_setup(A, st));
@@ -294,8 +327,7 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             // ComputeTrustRegionStep + candidate cost, one batch of kernels, one readback
             GBA_CHECK(hipMemsetAsync(dfail, 0, sizeof(int), st));
             GBA_CHECK(gba_launch_step_prep(A, radius, partial, scal + 2, st));
-            GBA_CHECK(gba_launch_cholesky(A, dfail, st));
-            GBA_CHECK(gba_launch_solve(A, st));
+            GBA_CHECK(factor_and_solve());
             GBA_CHECK(gba_launch_backsub(A, partial, scal + 3, st));
             GBA_CHECK(gba_launch_model(A, partial, scal + 4, st));
             GBA_CHECK(gba_launch_eval(A, A.c_pose, A.c_lm, 0, partial, scal + 7, st));
