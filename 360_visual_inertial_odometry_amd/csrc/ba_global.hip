@@ -1198,7 +1198,7 @@ hipError_t gba_cholesky_attributes() {
                                 (int)CHOL_DIAG_LDS);
     return e;
 }
-constexpr int kGbaFuseM = 48;  // chol_step_kernel for steps with at most this many block rows
+constexpr int kGbaFuseM = 96;  // chol_step_kernel for steps with at most this many block rows (config 5: every step)
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
     hipStream_t r = A.side;

@@ -28,11 +28,7 @@ sys.path.insert(0, ROOT)
 FP64_PEAK = 78.6e12  # MI355X FP64 vector (= FP64 matrix) peak, AMD spec
 
 
-TRACKER_KERNELS = ("pyr_down_kernel", "lk_kernel", "ransac_prep_kernel", "ransac_sample_kernel", "ransac_hyp_kernel",
-                   "ransac_select_kernel", "gftt_reset_kernel", "gftt_eig_kernel", "gftt_max_kernel", "gftt_hist_kernel",
-                   "gftt_cand_kernel", "gftt_cut_kernel", "ransac_raw_kernel",
-                   "gftt_topk_compact_kernel", "gftt_select_kernel<false>", "gftt_select_kernel<true>",
-                   "disc_mask_kernel")
+TRACKER_PREFIXES = ("pyr_down_kernel", "lk_kernel", "ransac_", "gftt_", "disc_mask_kernel", "rocprim")
 
 
 def pmc_traffic():
@@ -70,8 +66,10 @@ def klt_traffic():
     if not k or "lk_kernel" not in k:
         return None
     runs = k["lk_kernel"]["dispatches"]
+    # every kernel the pipeline launches once or more per run (rocprim: the top-K key sort); the one-off
+    # kernels of the standalone GFTT that picks the bench's start points run fewer times and are left out
     return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items()
-               if n in TRACKER_KERNELS or n.startswith("rocprim")) / runs  # rocprim: the top-K key sort
+               if n.startswith(TRACKER_PREFIXES) and v["dispatches"] >= runs) / runs
 
 
 def kernel_traffic(name):
@@ -352,12 +350,19 @@ def global_ba_bench(vio, synth, ctx, lm_iters):
     p = vio.BaProblem(w, variant=vio.VIO_BA_FULL, max_iterations=lm_iters, fixed_iterations=1)
     p2 = vio.BaProblem(w, variant=vio.VIO_BA_FULL, max_iterations=2 * lm_iters, fixed_iterations=1)
     ctx.ba_solve([p])  # warm-up (allocations, code objects)
-    t0 = time.perf_counter()
-    r = ctx.ba_solve([p])[0]
-    wall = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    ctx.ba_solve([p2])
-    wall2 = time.perf_counter() - t0
+
+    def best_of(prob, reps=3):  # the minimum of a few calls: the host-side part of a call is noisy
+        best, res = None, None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            out = ctx.ba_solve([prob])[0]
+            dt = time.perf_counter() - t0
+            if best is None or dt < best:
+                best, res = dt, out
+        return best, res
+
+    wall, r = best_of(p)
+    wall2, _ = best_of(p2)
     # per-iteration time with the problem resident: the difference of a 2L- and an L-iteration solve
     # (the host-side assembly, allocation and upload of vio_ba_solve cancel)
     per_iter = max(wall2 - wall, 1e-9) / lm_iters
@@ -370,8 +375,8 @@ def global_ba_bench(vio, synth, ctx, lm_iters):
         "ms_per_solve_call": wall * 1e3,
         "iterations_per_s_whole_call": lm_iters / wall,
         "note": "value: LM iterations per second with the problem resident (time of a 2L-iteration solve "
-                "minus an L-iteration solve, / L); whole_call: one vio_ba_solve incl. host assembly, "
-                "allocation, upload and the final chi2 pass; fixed iterations",
+                "minus an L-iteration solve, / L; each the fastest of 3 calls); whole_call: one vio_ba_solve "
+                "incl. host assembly, allocation, upload and the final chi2 pass; fixed iterations",
         "final_cost_ratio": r["final_cost"] / r["initial_cost"],
         "roofline": {"bound": "mfma", "achieved": flops / per_iter / 1e12, "peak": FP64_PEAK / 1e12,
                      "unit": "TFLOP/s", "frac": flops / per_iter / FP64_PEAK, "traffic": None,

@@ -1,4 +1,5 @@
-"""Diagnostic: config-5 global BA per-LM-iteration time (2L - L iteration solves, as bench.py)."""
+"""Diagnostic: config-5 global BA per-LM-iteration time (2L - L iteration solves, as bench.py; the
+minimum of R repetitions of each, which removes most of the per-call host noise)."""
 import importlib
 import os
 import sys
@@ -10,17 +11,26 @@ import torch  # noqa: E402,F401
 
 vio = importlib.import_module("360_visual_inertial_odometry_amd")
 synth = importlib.import_module("360_visual_inertial_odometry_amd.synth")
-L = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+L = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+R = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 ctx = vio.Context(0)
 w = synth.make_global()
 p = vio.BaProblem(w, variant=vio.VIO_BA_FULL, max_iterations=L, fixed_iterations=1)
 p2 = vio.BaProblem(w, variant=vio.VIO_BA_FULL, max_iterations=2 * L, fixed_iterations=1)
 ctx.ba_solve([p])
-t0 = time.perf_counter()
-ctx.ba_solve([p])
-a = time.perf_counter() - t0
-t0 = time.perf_counter()
-ctx.ba_solve([p2])
-b = time.perf_counter() - t0
-print(f"gba split={'off' if os.environ.get('VIO_GBA_NO_CU_SPLIT') else 'on'} ms_per_iteration={(b - a) / L * 1e3:.3f}", flush=True)
+
+
+def best(prob):
+    t = []
+    for _ in range(R):
+        t0 = time.perf_counter()
+        ctx.ba_solve([prob])
+        t.append(time.perf_counter() - t0)
+    return min(t)
+
+
+a = best(p)
+b = best(p2)
+print(f"gba fuse_m={os.environ.get('VIO_GBA_FUSE_M', 'default')} ms_per_iteration={(b - a) / L * 1e3:.3f} "
+      f"(L={L}: {a * 1e3:.1f} ms, 2L: {b * 1e3:.1f} ms)", flush=True)
 ctx.close()
