@@ -21,7 +21,8 @@ import ctypes as C
 out = (C.c_ulonglong * 24)()
 ctx.check(vio.lib().vio_ba_batch_phase_cycles(b.h, out), "phase_cycles")
 names = {0: "prep U partials", 1: "prep imu", 2: "prep cost partials", 3: "prep imu normal eq", 4: "prep gradient",
-         5: "prep finalize+diag", 8: "chol diag tiles", 9: "chol panels", 10: "chol trailing", 11: "chol forward",
+         5: "prep finalize+diag", 6: "schur g0 landmark blocks", 15: "schur g0 zero panel", 7: "schur g0 fills",
+         13: "schur g0 mfma phases", 14: "schur g0 combine+write", 8: "chol diag tiles", 9: "chol panels", 10: "chol trailing", 11: "chol forward",
          12: "chol backward",
          16: "solve assembly+partials", 17: "solve cholesky+solves", 18: "solve candidates+posecache",
          19: "solve imu model+cand", 20: "solve reductions", 21: "ctrl lane", 22: "ctrl copies"}
