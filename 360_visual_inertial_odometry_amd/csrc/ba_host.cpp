@@ -265,7 +265,8 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     // landmark chunks per Schur split-k group (phase route): a full config-4 shard (>= 256 windows)
     // fills the chip with 2 groups per window and halves ph_solve's partial sums; smaller batches keep
     // more, shorter groups (latency)
-    const int gs = pk.win.size() >= 256 ? 10 : 5;
+    const char* gse = std::getenv("VIO_BA_SCHUR_GS");  // experiment override
+    const int gs = gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : 5;
     for (BaWin& w : pk.win) w.gs = gs;
     UP(pk.win, win, const BaWin*);
     UP(pk.pose_raw, pose_raw, const double*);
