@@ -101,10 +101,11 @@ __global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLeve
 }
 
 // ------------------------------------------------------------------------------------------
-// LK.  One wavefront per point.
-constexpr int LK_WAVES = 4;
+// LK.  One workgroup per point.
+constexpr int LK_WAVES = 4;  // one point per workgroup of LK_WAVES waves
+constexpr int LK_THREADS = 64 * LK_WAVES;
 constexpr int LK_WIN_MAX = 21;
-constexpr int LK_NIT = (LK_WIN_MAX * LK_WIN_MAX + 63) / 64;  // patch pixels per lane
+constexpr int LK_NIT = (LK_WIN_MAX * LK_WIN_MAX + LK_THREADS - 1) / LK_THREADS;  // patch pixels per lane
 constexpr int LK_T = LK_WIN_MAX + 3;  // prev tile (patch + 1 bilinear + 1 Scharr each side)
 constexpr int LK_D = LK_WIN_MAX + 1;  // derivative / next tile
 
@@ -131,14 +132,6 @@ __device__ __forceinline__ double lane_d(double v, int l) {
     const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
     return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ long long wave_sum_i64(long long v) {
-    double d = (double)v;
-    d += dpp_d<0xB1>(d);   // quad_perm [1,0,3,2]
-    d += dpp_d<0x4E>(d);   // quad_perm [2,3,0,1]
-    d += dpp_d<0x141>(d);  // row_half_mirror
-    d += dpp_d<0x140>(d);  // row_mirror: every lane holds its row's sum
-    return (long long)(((lane_d(d, 0) + lane_d(d, 16)) + lane_d(d, 32)) + lane_d(d, 48));
-}
 
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 
@@ -149,42 +142,62 @@ __device__ __forceinline__ void lk_weights(float a, float b, int& w00, int& w01,
     w11 = 16384 - w00 - w01 - w10;
 }
 
+// workgroup sum of integer partials (exact: each wave's partials summed as doubles with DPP row
+// reductions and the four row totals read out, then the LK_WAVES wave totals
+// added in wave order through LDS); every thread gets the total.  red: LK_WAVES doubles of LDS.
+__device__ __forceinline__ long long wg_sum_i64(long long v, double* red) {
+    double d = (double)v;
+    d += dpp_d<0xB1>(d);
+    d += dpp_d<0x4E>(d);
+    d += dpp_d<0x141>(d);
+    d += dpp_d<0x140>(d);
+    const double ws = ((lane_d(d, 0) + lane_d(d, 16)) + lane_d(d, 32)) + lane_d(d, 48);
+    const int wid = threadIdx.x >> 6;
+    __syncthreads();  // red is free (the previous sum's readers are done)
+    if ((threadIdx.x & 63) == 0) red[wid] = ws;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < LK_WAVES; ++q) t += red[q];
+    return (long long)t;
+}
+
 // make the staged region cover the (win+1)^2 window at (ix, iy); restage around it when it does
 // not (one global round trip per level instead of one per iteration).  Values are the
-// REFLECT_101-padded pixels, exactly what a per-window load would read.
+// REFLECT_101-padded pixels, exactly what a per-window load would read.  Workgroup-uniform.
 __device__ __forceinline__ void lk_region(uint8_t* Jr, int& rx0, int& ry0, const uint8_t* J, int w, int h, int pitch,
-                                          int ix, int iy, int win, int lane) {
+                                          int ix, int iy, int win) {
     const int D = win + 1;
     if (ix >= rx0 && iy >= ry0 && ix + D <= rx0 + LK_R && iy + D <= ry0 + LK_R) return;
     rx0 = ix - LK_MARGIN;
     ry0 = iy - LK_MARGIN;
-    __builtin_amdgcn_wave_barrier();
-    // every global load of the region is issued before the first LDS store (one memory round trip
-    // instead of one per 64 pixels)
-    constexpr int NR = (LK_R * LK_R + 63) / 64;
+    __syncthreads();  // the previous region's readers are done
+    // every global load of the region is issued before the first LDS store
+    constexpr int NR = (LK_R * LK_R + LK_THREADS - 1) / LK_THREADS;
     uint32_t v[NR];
 #pragma unroll
     for (int it = 0; it < NR; ++it) {
-        const int e = lane + 64 * it;
+        const int e = threadIdx.x + LK_THREADS * it;
         const int ty = e / LK_R, tx = e - ty * LK_R;
         v[it] = e < LK_R * LK_R ? J[(size_t)reflect101(ry0 + ty, h) * pitch + reflect101(rx0 + tx, w)] : 0u;
     }
 #pragma unroll
     for (int it = 0; it < NR; ++it) {
-        const int e = lane + 64 * it;
+        const int e = threadIdx.x + LK_THREADS * it;
         if (e < LK_R * LK_R) Jr[e] = (uint8_t)v[it];
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __syncthreads();
 }
 
-// Σ |diff| or the b-vector over the window for the current J tile
-__global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
-    __shared__ LkShared shm[LK_WAVES];
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int pt = blockIdx.x * LK_WAVES + wid;
-    if (pt >= A.n) return;  // whole wave exits together (wave-uniform)
-    LkShared& S = shm[wid];
+// calcOpticalFlowPyrLK for one point per workgroup (LK_WAVES waves): the patch pixels are spread over
+// all lanes (<= LK_NIT each), the window sums are exact integer workgroup sums, so every order gives
+// the sequential values; the per-iteration update is computed by every thread from the same totals.
+__global__ void __launch_bounds__(LK_THREADS) lk_kernel(LkArgs A) {
+    __shared__ LkShared S;
+    __shared__ double red[LK_WAVES];
+    const int tid = threadIdx.x;
+    const int pt = blockIdx.x;
+    if (pt >= A.n) return;  // whole workgroup
     const int win = A.win;
     const float hw = (win - 1) * 0.5f;
     const float FLT_SCALE = 1.f / (1 << 20);
@@ -212,26 +225,26 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
         }
         // stage the prev tile: rows ipy-1 .. ipy+win+1, cols ipx-1 .. ipx+win+1
         const int T = win + 3;
+        __syncthreads();  // the previous level's readers of It / dx / dy are done
         {
-            constexpr int NT = (LK_T * LK_T + 63) / 64;  // loads first, then the LDS stores
+            constexpr int NT = (LK_T * LK_T + LK_THREADS - 1) / LK_THREADS;  // loads first, then the LDS stores
             uint32_t v[NT];
 #pragma unroll
             for (int it = 0; it < NT; ++it) {
-                const int e = lane + 64 * it;
+                const int e = tid + LK_THREADS * it;
                 const int ty = e / T, tx = e - (e / T) * T;
                 v[it] = e < T * T ? I[(size_t)reflect101(ipy - 1 + ty, h) * Lv.pitch + reflect101(ipx - 1 + tx, w)] : 0u;
             }
 #pragma unroll
             for (int it = 0; it < NT; ++it) {
-                const int e = lane + 64 * it;
+                const int e = tid + LK_THREADS * it;
                 if (e < T * T) S.It[e] = (uint8_t)v[it];
             }
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __syncthreads();
         // Scharr derivatives at (ipx+tx, ipy+ty), tx,ty in [0, win]; zero outside the image
         const int D = win + 1;
-        for (int e = lane; e < D * D; e += 64) {
+        for (int e = tid; e < D * D; e += LK_THREADS) {
             int ty = e / D, tx = e % D;
             int X = ipx + tx, Y = ipy + ty;
             int gx = 0, gy = 0;
@@ -247,18 +260,17 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
             S.dx[e] = (int16_t)gx;
             S.dy[e] = (int16_t)gy;
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __syncthreads();
         float a = px - ipx, b = py - ipy;
         int w00, w01, w10, w11;
         lk_weights(a, b, w00, w01, w10, w11);
-        // the lane's patch pixels e = lane + 64 it: interpolated I and derivatives stay in registers
+        // the lane's patch pixels e = tid + LK_THREADS it: interpolated I and derivatives stay in registers
         // for all iterations of the level; joff = offset of the pixel in the next-frame window (-1: none)
         int joff[LK_NIT], iwv[LK_NIT], ixr[LK_NIT], iyr[LK_NIT];
-        int sA11 = 0, sA12 = 0, sA22 = 0;  // per-lane partials fit int32 (<= 7 terms < 2^26 each)
+        int sA11 = 0, sA12 = 0, sA22 = 0;
 #pragma unroll
         for (int it = 0; it < LK_NIT; ++it) {
-            const int e = lane + 64 * it;
+            const int e = tid + LK_THREADS * it;
             joff[it] = -1;
             iwv[it] = ixr[it] = iyr[it] = 0;
             if (e < np) {
@@ -279,7 +291,7 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
                 sA22 += iyv * iyv;
             }
         }
-        const long long tA11 = wave_sum_i64(sA11), tA12 = wave_sum_i64(sA12), tA22 = wave_sum_i64(sA22);
+        const long long tA11 = wg_sum_i64(sA11, red), tA12 = wg_sum_i64(sA12, red), tA22 = wg_sum_i64(sA22, red);
         const float A11 = (float)tA11 * FLT_SCALE, A12 = (float)tA12 * FLT_SCALE, A22 = (float)tA22 * FLT_SCALE;
         float Dt = A11 * A22 - A12 * A12;
         const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win * win);
@@ -299,9 +311,9 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
             }
             a = nx - inx; b = ny - iny;
             lk_weights(a, b, w00, w01, w10, w11);
-            lk_region(S.Jr, rx0, ry0, J, w, h, Lv.pitch, inx, iny, win, lane);
+            lk_region(S.Jr, rx0, ry0, J, w, h, Lv.pitch, inx, iny, win);
             const uint8_t* Jw = S.Jr + (iny - ry0) * LK_R + (inx - rx0);
-            int ib1 = 0, ib2 = 0;  // per-lane partials fit int32 (<= 7 terms < 2^26 each)
+            int ib1 = 0, ib2 = 0;
 #pragma unroll
             for (int it = 0; it < LK_NIT; ++it) {
                 if (joff[it] >= 0) {
@@ -311,7 +323,7 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
                     ib2 += diff * iyr[it];
                 }
             }
-            const float b1 = (float)wave_sum_i64(ib1) * FLT_SCALE, b2 = (float)wave_sum_i64(ib2) * FLT_SCALE;
+            const float b1 = (float)wg_sum_i64(ib1, red) * FLT_SCALE, b2 = (float)wg_sum_i64(ib2, red) * FLT_SCALE;
             const float ddx = (A12 * b2 - A22 * b1) * Dt;
             const float ddy = (A12 * b1 - A11 * b2) * Dt;
             nx += ddx; ny += ddy;
@@ -331,7 +343,7 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
                 status = 0;
             } else {
                 lk_weights(fx - ix, fy - iy, w00, w01, w10, w11);
-                lk_region(S.Jr, rx0, ry0, J, w, h, Lv.pitch, ix, iy, win, lane);
+                lk_region(S.Jr, rx0, ry0, J, w, h, Lv.pitch, ix, iy, win);
                 const uint8_t* Jw = S.Jr + (iy - ry0) * LK_R + (ix - rx0);
                 long long es = 0;
 #pragma unroll
@@ -343,13 +355,12 @@ __global__ void __launch_bounds__(64 * LK_WAVES) lk_kernel(LkArgs A) {
                         es += diff < 0 ? -diff : diff;
                     }
                 }
-                es = wave_sum_i64(es);
+                es = wg_sum_i64(es, red);
                 err = (float)es * (1.f / (32 * win * win));
             }
         }
-        __builtin_amdgcn_wave_barrier();
     }
-    if (lane == 0) {
+    if (tid == 0) {
         A.next[2 * pt] = nxt_x;
         A.next[2 * pt + 1] = nxt_y;
         A.status[pt] = (uint8_t)status;
@@ -374,15 +385,17 @@ __device__ void pixel_to_bearing(float u, float v, int W, int H, float* b) {
     b[0] = x; b[1] = y; b[2] = z;
 }
 
-// order-preserving compaction of the RANSAC input (single workgroup of 1024 threads):
+// order-preserving compaction of the RANSAC input (single workgroup of RP_THREADS: four waves get a CU
+// sooner than sixteen while GFTT pass 1 occupies the chip from the side stream):
 //   mode 0: all n points (erp_rot_ransac); mode 1: status ∧ !polar ∧ !boundary (pipeline)
-__global__ void __launch_bounds__(1024) ransac_prep_kernel(RansacArgs R) {
-    __shared__ int wsum[16];
+constexpr int RP_THREADS = 256;
+__global__ void __launch_bounds__(RP_THREADS) ransac_prep_kernel(RansacArgs R) {
+    __shared__ int wsum[RP_THREADS / 64];
     __shared__ int base;
     if (threadIdx.x == 0) base = 0;
     __syncthreads();
     const int n = R.n;
-    for (int c0 = 0; c0 < n; c0 += 1024) {
+    for (int c0 = 0; c0 < n; c0 += RP_THREADS) {
         int i = c0 + threadIdx.x;
         int good = 0;
         if (i < n) {
@@ -413,7 +426,7 @@ __global__ void __launch_bounds__(1024) ransac_prep_kernel(RansacArgs R) {
         __syncthreads();
         if (threadIdx.x == 0) {
             int t = 0;
-            for (int k = 0; k < 16; ++k) t += wsum[k];
+            for (int k = 0; k < RP_THREADS / 64; ++k) t += wsum[k];
             base += t;
         }
         __syncthreads();
@@ -1795,7 +1808,7 @@ hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int fra
 }
 hipError_t launch_lk(const LkArgs& a, hipStream_t st) {
     if (a.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(lk_kernel, dim3((a.n + LK_WAVES - 1) / LK_WAVES), dim3(64 * LK_WAVES), 0, st, a);
+    hipLaunchKernelGGL(lk_kernel, dim3(a.n), dim3(LK_THREADS), 0, st, a);
     return hipGetLastError();
 }
 size_t ransac_raw_words() { return RS_RAW; }
@@ -1804,7 +1817,7 @@ hipError_t launch_ransac_raw(uint32_t seed, uint32_t* raw, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st) {
-    hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(1024), 0, st, r);
+    hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(RP_THREADS), 0, st, r);
     if (gen_samples) hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(RS_THREADS), 0, st, r);
     if (r.iters > 0) hipLaunchKernelGGL(ransac_hyp_kernel, dim3((r.iters + 3) / 4), dim3(256), 0, st, r);
     hipLaunchKernelGGL(ransac_select_kernel, dim3(1), dim3(256), 0, st, r);

@@ -92,7 +92,7 @@ struct erp_tracker {
     hipEvent_t ev[6] = {};
     // the GFTT eigenvalue map runs on a side stream, overlapped with pyramids / LK / RANSAC
     hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr, raw_done = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, raw_done = nullptr, disc_zero = nullptr;
     bool ran = false;
     std::vector<void*> allocs;
 };
@@ -120,6 +120,7 @@ void tracker_free(erp_tracker* t) {
     if (t->fork) (void)hipEventDestroy(t->fork);
     if (t->join) (void)hipEventDestroy(t->join);
     if (t->raw_done) (void)hipEventDestroy(t->raw_done);
+    if (t->disc_zero) (void)hipEventDestroy(t->disc_zero);
 }
 
 int ensure_iters(erp_tracker* t, int iters) {
@@ -208,10 +209,15 @@ int tracker_alloc(erp_tracker* t) {
     if ((rc = dalloc(t, &t->d_raw, sizeof(uint32_t) * ransac_raw_words()))) return rc;
     for (auto& e : t->ev)
         if (hipEventCreate(&e) != hipSuccess) return hip_fail(t->ctx, hipErrorUnknown, "hipEventCreate");
-    if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess ||
+    // the side stream (GFTT pass 1, the RANSAC raw draws) runs at the lowest priority: its 3600-workgroup
+    // pass yields CUs to the latency-bound LK / RANSAC kernels of the main stream, which it overlaps
+    int prio_least = 0, prio_greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_least = 0;
+    if (hipStreamCreateWithPriority(&t->side, hipStreamNonBlocking, prio_least) != hipSuccess ||
         hipEventCreateWithFlags(&t->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t->raw_done, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&t->raw_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&t->disc_zero, hipEventDisableTiming) != hipSuccess)
         return hip_fail(t->ctx, hipErrorUnknown, "side stream / events");
     return VIO_OK;
 }
@@ -312,7 +318,8 @@ GfArgs gf_lmax_args(erp_tracker* t, const uint8_t* img, int pitch, int margin, f
 
 // eig_ready: the map of `img` was already produced (launch_gftt_eig joined into the context stream)
 int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* mask, int mask_pitch, int max_corners,
-                 double quality, double min_dist, bool discs, int margin, float polar, bool eig_ready = false) {
+                 double quality, double min_dist, bool discs, int margin, float polar, bool eig_ready = false,
+                 bool reset_done = false) {
     int rc = ensure_gftt(t, min_dist);
     if (rc) return rc;
     GfArgs g;
@@ -348,7 +355,7 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     g.topk_target = (unsigned int)std::min<size_t>(t->topk_cap, std::max<size_t>(4096, 16 * (size_t)max_corners));
     // scalars [2] max_ord [3] n_cand [4] n_out [6] n_top [7..8] cut [9] incomplete
     t->last_gf = g;
-    hipError_t e = launch_gftt_reset(g, t->d_scal, t->ctx->stream);
+    hipError_t e = reset_done ? hipSuccess : launch_gftt_reset(g, t->d_scal, t->ctx->stream);
     if (g.lmax) {
         if (e == hipSuccess && !eig_ready) e = launch_gftt_lmax(g, t->ctx->stream);
         if (e == hipSuccess) e = launch_gftt_after_lmax(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
@@ -512,6 +519,17 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac_raw_kernel");
         VIO_HIP(t->ctx, hipEventRecord(t->raw_done, t->side));
     }
+    {  // off the main stream's path: the GFTT counters / histogram / top-K reset and the disc bitmap clear
+        GfArgs gr;
+        std::memset(&gr, 0, sizeof gr);
+        gr.hist = t->d_hist;
+        gr.topk = t->d_topk;
+        gr.topk_cap = t->topk_cap;
+        hipError_t e = launch_gftt_reset(gr, t->d_scal, t->side);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_reset_kernel");
+        VIO_HIP(t->ctx, hipMemsetAsync(t->d_disc, 0, sizeof(uint32_t) * t->disc_words * t->H, t->side));
+        VIO_HIP(t->ctx, hipEventRecord(t->disc_zero, t->side));
+    }
     if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK
     {  // GFTT pass 1 shares the chip with the latency-bound LK / RANSAC, not with the pyramids
         VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->ev[1], 0));
@@ -531,8 +549,8 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal, 0, 2 * sizeof(int), st));
     }
     VIO_HIP(t->ctx, hipEventRecord(t->ev[3], st));
-    // CreateFeatureMask: discs of radius (int)min_dist around every kept point
-    VIO_HIP(t->ctx, hipMemsetAsync(t->d_disc, 0, sizeof(uint32_t) * t->disc_words * t->H, st));
+    // CreateFeatureMask: discs of radius (int)min_dist around every kept point (bitmap cleared on the side stream)
+    VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->disc_zero, 0));
     const int radius = (int)p->min_dist;
     if (radius != t->halfw_r) {
         std::vector<int> hw = circle_half_widths(radius);
@@ -548,7 +566,7 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
     }
     VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->join, 0));
     if ((rc = enqueue_gftt(t, t->lvl[1][0], t->lp[0], nullptr, 0, p->max_corners, p->quality, p->min_dist, true,
-                           p->boundary_margin, p->polar_ratio, true)))
+                           p->boundary_margin, p->polar_ratio, true, true)))
         return rc;
     VIO_HIP(t->ctx, hipEventRecord(t->ev[4], st));
     t->ran = true;
