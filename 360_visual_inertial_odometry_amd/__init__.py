@@ -27,6 +27,7 @@ EXPORTS = [
     "erp_klt_track", "erp_gftt", "erp_rot_ransac", "erp_ransac_samples", "erp_tracker_create",
     "erp_tracker_upload", "erp_tracker_device_frame", "erp_tracker_swap", "erp_tracker_set_points",
     "erp_tracker_run", "erp_tracker_sync", "erp_tracker_download", "erp_tracker_stage_ms",
+    "erp_tracker_set_stage_timing",
     "erp_tracker_destroy", "erp_frontend_create", "erp_frontend_track", "erp_frontend_features",
     "erp_frontend_stats", "erp_frontend_destroy", "vio_imu_preintegrate", "vio_imu_preintegrate_kernel_ms", "vio_imu_preintegrate_device",
     "vio_ba_batch_set_preint",
@@ -87,6 +88,7 @@ def lib():
     L.erp_tracker_sync.argtypes = [vp]
     L.erp_tracker_download.argtypes = [vp, vp, vp, vp, vp, C.POINTER(C.c_int)]
     L.erp_tracker_stage_ms.argtypes = [vp] + [C.POINTER(C.c_double)] * 5
+    L.erp_tracker_set_stage_timing.argtypes = [vp, C.c_int]
     L.erp_tracker_destroy.argtypes = [vp]
     L.erp_frontend_create.argtypes = [vp, C.c_int, C.c_int, C.POINTER(abi.ErpFrontendParams), C.POINTER(C.c_void_p)]
     L.erp_frontend_track.argtypes = [vp, vp, C.c_int, C.POINTER(C.c_int)]
@@ -528,6 +530,10 @@ class Tracker:
         self.ctx.check(lib().erp_tracker_download(self.h, _p(nxt), _p(st), _p(kept), _p(cor), C.byref(nc)),
                        "erp_tracker_download")
         return {"next": nxt[:n], "status": st[:n], "kept": kept[:n], "corners": cor[: nc.value].copy()}
+
+    def set_stage_timing(self, on):
+        """Record the per-stage events on the next runs (on) or only the pipeline's start and end."""
+        self.ctx.check(lib().erp_tracker_set_stage_timing(self.h, 1 if on else 0), "erp_tracker_set_stage_timing")
 
     def stage_ms(self):
         v = [C.c_double() for _ in range(5)]

@@ -92,7 +92,9 @@ struct erp_tracker {
     hipEvent_t ev[6] = {};
     // the GFTT eigenvalue map runs on a side stream, overlapped with pyramids / LK / RANSAC
     hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr, raw_done = nullptr, disc_zero = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, raw_done = nullptr;
+    bool stage_timing = true;  // record the per-stage events (each marker costs the stream a few us)
+    bool timed_run = false;    // the last run recorded them
     bool ran = false;
     std::vector<void*> allocs;
 };
@@ -120,7 +122,6 @@ void tracker_free(erp_tracker* t) {
     if (t->fork) (void)hipEventDestroy(t->fork);
     if (t->join) (void)hipEventDestroy(t->join);
     if (t->raw_done) (void)hipEventDestroy(t->raw_done);
-    if (t->disc_zero) (void)hipEventDestroy(t->disc_zero);
 }
 
 int ensure_iters(erp_tracker* t, int iters) {
@@ -216,8 +217,7 @@ int tracker_alloc(erp_tracker* t) {
     if (hipStreamCreateWithPriority(&t->side, hipStreamNonBlocking, prio_least) != hipSuccess ||
         hipEventCreateWithFlags(&t->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t->raw_done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t->disc_zero, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&t->raw_done, hipEventDisableTiming) != hipSuccess)
         return hip_fail(t->ctx, hipErrorUnknown, "side stream / events");
     return VIO_OK;
 }
@@ -252,11 +252,11 @@ int check_klt(vio_ctx* ctx, const erp_klt_params* p) {
     return VIO_OK;
 }
 
-int enqueue_lk(erp_tracker* t, const erp_klt_params* p, int n) {
+int enqueue_lk(erp_tracker* t, const erp_klt_params* p, int n, bool pyr_built = false) {
     LkArgs a;
     std::memset(&a, 0, sizeof a);
     int top = lk_top_level(t, p->win, p->max_level);
-    int rc = build_pyramids(t, top);
+    int rc = pyr_built ? VIO_OK : build_pyramids(t, top);
     if (rc) return rc;
     for (int l = 0; l <= top; ++l) a.lv[l] = LkLevel{t->lvl[0][l], t->lvl[1][l], t->lw[l], t->lh[l], t->lp[l]};
     a.levels = top;
@@ -517,7 +517,6 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
     {  // the RANSAC draws' raw stream depends on the seed only
         hipError_t e = launch_ransac_raw(p->ransac_seed, t->d_raw, t->side);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac_raw_kernel");
-        VIO_HIP(t->ctx, hipEventRecord(t->raw_done, t->side));
     }
     {  // off the main stream's path: the GFTT counters / histogram / top-K reset and the disc bitmap clear
         GfArgs gr;
@@ -528,7 +527,7 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         hipError_t e = launch_gftt_reset(gr, t->d_scal, t->side);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_reset_kernel");
         VIO_HIP(t->ctx, hipMemsetAsync(t->d_disc, 0, sizeof(uint32_t) * t->disc_words * t->H, t->side));
-        VIO_HIP(t->ctx, hipEventRecord(t->disc_zero, t->side));
+        VIO_HIP(t->ctx, hipEventRecord(t->raw_done, t->side));  // raw draws, reset and cleared discs: one wait
     }
     if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK
     {  // GFTT pass 1 shares the chip with the latency-bound LK / RANSAC, not with the pyramids
@@ -538,7 +537,7 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_lmax_kernel");
     }
     VIO_HIP(t->ctx, hipEventRecord(t->join, t->side));
-    VIO_HIP(t->ctx, hipEventRecord(t->ev[2], st));
+    if (t->stage_timing) VIO_HIP(t->ctx, hipEventRecord(t->ev[2], st));
     RansacArgs r = ransac_args(t, n, 1, p->ransac_iters, p->ransac_seed, p->ransac_thresh_rad, p->polar_ratio,
                                p->boundary_margin, t->d_pts, t->d_next);
     if (n > 0) {
@@ -548,9 +547,10 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
     } else {
         VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal, 0, 2 * sizeof(int), st));
     }
-    VIO_HIP(t->ctx, hipEventRecord(t->ev[3], st));
-    // CreateFeatureMask: discs of radius (int)min_dist around every kept point (bitmap cleared on the side stream)
-    VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->disc_zero, 0));
+    if (t->stage_timing) VIO_HIP(t->ctx, hipEventRecord(t->ev[3], st));
+    // CreateFeatureMask: discs of radius (int)min_dist around every kept point (bitmap cleared on the side
+    // stream before raw_done, which the main stream waited for before RANSAC)
+    if (n <= 0) VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->raw_done, 0));
     const int radius = (int)p->min_dist;
     if (radius != t->halfw_r) {
         std::vector<int> hw = circle_half_widths(radius);
@@ -570,6 +570,7 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         return rc;
     VIO_HIP(t->ctx, hipEventRecord(t->ev[4], st));
     t->ran = true;
+    t->timed_run = t->stage_timing;
     return VIO_OK;
 }
 
@@ -595,15 +596,23 @@ int erp_tracker_download(erp_tracker* t, float* next, uint8_t* status, uint8_t* 
     return VIO_OK;
 }
 
+int erp_tracker_set_stage_timing(erp_tracker* t, int on) {
+    if (!t) return VIO_EINVAL;
+    t->stage_timing = on != 0;
+    return VIO_OK;
+}
+
 int erp_tracker_stage_ms(erp_tracker* t, double* pyr_ms, double* lk_ms, double* ransac_ms, double* gftt_ms,
                          double* total_ms) {
     if (!t || !t->ran) return VIO_EINVAL;
     VIO_HIP(t->ctx, hipEventSynchronize(t->ev[4]));
-    float a = 0, b = 0, c = 0, d = 0, e = 0;
-    VIO_HIP(t->ctx, hipEventElapsedTime(&a, t->ev[0], t->ev[1]));
-    VIO_HIP(t->ctx, hipEventElapsedTime(&b, t->ev[1], t->ev[2]));
-    VIO_HIP(t->ctx, hipEventElapsedTime(&c, t->ev[2], t->ev[3]));
-    VIO_HIP(t->ctx, hipEventElapsedTime(&d, t->ev[3], t->ev[4]));
+    float a = -1, b = -1, c = -1, d = -1, e = 0;
+    if (t->timed_run) {
+        VIO_HIP(t->ctx, hipEventElapsedTime(&a, t->ev[0], t->ev[1]));
+        VIO_HIP(t->ctx, hipEventElapsedTime(&b, t->ev[1], t->ev[2]));
+        VIO_HIP(t->ctx, hipEventElapsedTime(&c, t->ev[2], t->ev[3]));
+        VIO_HIP(t->ctx, hipEventElapsedTime(&d, t->ev[3], t->ev[4]));
+    }
     VIO_HIP(t->ctx, hipEventElapsedTime(&e, t->ev[0], t->ev[4]));
     if (pyr_ms) *pyr_ms = a;
     if (lk_ms) *lk_ms = b;

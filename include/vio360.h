@@ -417,9 +417,13 @@ int erp_tracker_sync(erp_tracker* t);
    (status ∧ !polar ∧ !boundary ∧ RANSAC inlier); the new corners (≤ max_corners float2) */
 int erp_tracker_download(erp_tracker* t, float* next, uint8_t* status, uint8_t* kept, float* corners,
                          int* n_corners);
-/* device time (ms) of the pipeline stages of the last run */
+/* device time (ms) of the pipeline stages of the last run (the stage values are -1 when the run did not
+   record its stage events, see erp_tracker_set_stage_timing; total_ms is always measured) */
 int erp_tracker_stage_ms(erp_tracker* t, double* pyr_ms, double* lk_ms, double* ransac_ms, double* gftt_ms,
                          double* total_ms);
+/* on (default): runs record the per-stage events; off: only the pipeline's start and end (each event
+   marker costs the stream a few microseconds) */
+int erp_tracker_set_stage_timing(erp_tracker* t, int on);
 void erp_tracker_destroy(erp_tracker* t);
 
 /* ------------------------------------------------------------------------------------------ */

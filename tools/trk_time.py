@@ -34,6 +34,13 @@ for _ in range(steps):
     t.sync()
     s = t.stage_ms()
     stage = {k: (stage or {}).get(k, 0.0) + v / steps for k, v in s.items()}
+t.set_stage_timing(False)
+tot = 0.0
+for _ in range(steps):
+    t.run(prm)
+    t.sync()
+    tot += t.stage_ms()["total"] / steps
+print("total_ms without stage markers", round(tot, 4), flush=True)
 res = t.download()
 print("stage_ms", {k: round(v, 4) for k, v in stage.items()}, flush=True)
 print("kept", int(np.sum(res["status"])) if "status" in res else None, "new corners",
