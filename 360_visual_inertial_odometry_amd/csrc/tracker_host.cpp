@@ -210,11 +210,7 @@ int tracker_alloc(erp_tracker* t) {
     if ((rc = dalloc(t, &t->d_raw, sizeof(uint32_t) * ransac_raw_words()))) return rc;
     for (auto& e : t->ev)
         if (hipEventCreate(&e) != hipSuccess) return hip_fail(t->ctx, hipErrorUnknown, "hipEventCreate");
-    // the side stream (GFTT pass 1, the RANSAC raw draws) runs at the lowest priority: its 3600-workgroup
-    // pass yields CUs to the latency-bound LK / RANSAC kernels of the main stream, which it overlaps
-    int prio_least = 0, prio_greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_least = 0;
-    if (hipStreamCreateWithPriority(&t->side, hipStreamNonBlocking, prio_least) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&t->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->raw_done, hipEventDisableTiming) != hipSuccess)
