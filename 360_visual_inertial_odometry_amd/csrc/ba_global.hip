@@ -637,12 +637,20 @@ __global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k,
 __global__ void __launch_bounds__(256) trsv_fwd_kernel(const double* S, int n, int k, const double* Linv, double* b,
                                                        double* y) {
     __shared__ double yk[NB];
+    __shared__ double pt[4][64];
     const double* Li = Linv + (size_t)k * NB * NB;
-    if (threadIdx.x < NB) {
+    {   // y_k[r] = Linv_kk[r][:] b_k as the four 16-column group sums ((p0 + p1) + (p2 + p3))
+        const int r = threadIdx.x & 63, g = threadIdx.x >> 6;
         double s = 0.0;
-        for (int q = 0; q <= (int)threadIdx.x; ++q) s += Li[threadIdx.x * NB + q] * b[k * NB + q];
-        yk[threadIdx.x] = s;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int q = 16 * g + u;
+            if (q <= r) s += Li[r * NB + q] * b[k * NB + q];
+        }
+        pt[g][r] = s;
     }
+    __syncthreads();
+    if (threadIdx.x < NB) yk[threadIdx.x] = (pt[0][threadIdx.x] + pt[1][threadIdx.x]) + (pt[2][threadIdx.x] + pt[3][threadIdx.x]);
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x < NB) y[k * NB + threadIdx.x] = yk[threadIdx.x];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -672,11 +680,18 @@ __global__ void __launch_bounds__(256) trsv_bwd_kernel(const double* S, int n, i
     __shared__ double xk[NB];
     __shared__ double part[4][64];
     const double* Li = Linv + (size_t)k * NB * NB;
-    if (threadIdx.x < NB) {
+    {   // x_k[c] = Linv_kk[:][c] . y_k as the four 16-row group sums ((p0 + p1) + (p2 + p3))
+        const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
         double s = 0.0;
-        for (int q = threadIdx.x; q < NB; ++q) s += Li[q * NB + threadIdx.x] * y[k * NB + q];
-        xk[threadIdx.x] = s;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int q = 16 * g + u;
+            if (q >= c) s += Li[q * NB + c] * y[k * NB + q];
+        }
+        part[g][c] = s;
     }
+    __syncthreads();
+    if (threadIdx.x < NB) xk[threadIdx.x] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x < NB) x[k * NB + threadIdx.x] = xk[threadIdx.x];
     const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -717,6 +732,22 @@ __device__ __forceinline__ bool flag_wait(int* f) {
     // bounded spin: a producer that never arrives ends the wait instead of hanging the GPU
     for (int it = 0; it < (1 << 24); ++it) {
         if (__hip_atomic_load((gint*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+// triangular-solve hand-off without a flag: the consumer polls the 64 values themselves (set to this
+// NaN pattern before the solve; each 8-B value is stored whole), one round trip instead of flag +
+// data.  Called by the 64 lanes of one wave; false on a timed-out wait.
+constexpr unsigned long long kUnsetBits = ~0ull;
+__device__ __forceinline__ bool poll_block(const double* p, double& v) {
+    bool pend = true;
+    for (int it = 0; it < (1 << 24); ++it) {
+        if (pend) {
+            v = ld_sc1(p);
+            pend = (unsigned long long)__double_as_longlong(v) == kUnsetBits;
+        }
+        if (__ballot(pend) == 0ull) return true;
         __builtin_amdgcn_s_sleep(1);
     }
     return false;
@@ -849,11 +880,11 @@ constexpr int TG = 2;
 constexpr int LIS = NB + 1;  // odd LDS row stride
 
 // forward: workgroup j owns row blocks r = TG j + rl: b_r -= L_rk y_k for k = 0 .. r-1 (k order,
-// each row dot as the four 16-column group sums ((p0 + p1) + (p2 + p3)), the backward layout),
-// y_r = Linv_rr b_r.  flags[FLAG_STRIDE k] != 0: y_k is final.  flags[FLAG_STRIDE 2 nblk]: set on a
-// timed-out wait.
+// each row dot as 32 two-term lane products reduced by a butterfly over the half-wave: the row
+// streams as one 512-B segment), y_r = Linv_rr b_r.  y_k is final once none of its 64 values is the unset pattern (poll_block);
+// flags[FLAG_STRIDE 2 nblk]: set on a timed-out wait.
 __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* S, int n, const double* Linv,
-                                                                  double* b, double* y, int* flags) {
+                                                                  double* b, double* y, double* x, int* flags) {
     __shared__ double bs[TG * NB];
     __shared__ double yk[NB];
     __shared__ double part[TG][4][64];
@@ -861,7 +892,10 @@ __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* 
     __shared__ int ok_s;
     const int nblk = n / NB, r0 = TG * blockIdx.x, nl = min(TG, nblk - r0);
     const int rw = threadIdx.x & 63, g = threadIdx.x >> 6;  // row in the block, 16-column group
-    for (int e = threadIdx.x; e < nl * NB; e += 256) bs[e] = b[r0 * NB + e];
+    for (int e = threadIdx.x; e < nl * NB; e += 256) {
+        bs[e] = b[r0 * NB + e];
+        x[r0 * NB + e] = __longlong_as_double((long long)kUnsetBits);  // polled by the backward solve
+    }
     for (int rl = 0; rl < nl; ++rl) {
         const double* Li = Linv + (size_t)(r0 + rl) * NB * NB;
         double v[16];
@@ -875,68 +909,89 @@ __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* 
     }
     if (threadIdx.x == 0) ok_s = 1;
     __syncthreads();
+    // the off-diagonal rows stream as 512-B segments: a wave load instruction covers two rows (16 B
+    // per lane), each row dot reduced over its 32 lanes
+    const int lane = threadIdx.x & 63, h = lane >> 5, q0 = 2 * (lane & 31);
+    constexpr int NI = TG * NB / 8;  // row pairs per wave and step
     for (int k = 0; k < r0; ++k) {
-        double v[TG][16];
+        double pv = 0.0;
+        if (threadIdx.x < NB) pv = ld_sc1(y + k * NB + lane);  // first poll, ahead of the row loads
+        double2 v[NI];
 #pragma unroll
-        for (int rl = 0; rl < TG; ++rl)
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-                v[rl][u] = rl < nl ? S[(size_t)((r0 + rl) * NB + rw) * n + (size_t)k * NB + g * 16 + u] : 0.0;
-        if (threadIdx.x == 0 && !flag_wait(flags + FLAG_STRIDE * k)) { ok_s = 0; flags[FLAG_STRIDE * 2 * nblk] = 1; }
-        __syncthreads();
-        if (!ok_s) return;
-        if (threadIdx.x < NB) yk[threadIdx.x] = ld_sc1(y + k * NB + threadIdx.x);
-        __syncthreads();
-#pragma unroll
-        for (int rl = 0; rl < TG; ++rl) {
-            double t = 0.0;
-#pragma unroll
-            for (int u = 0; u < 16; ++u) t += v[rl][u] * yk[g * 16 + u];
-            part[rl][g][rw] = t;
+        for (int i = 0; i < NI; ++i) {
+            const int row = 2 * (g * NI + i) + h;  // rl NB + row in the block
+            v[i] = (row >> 6) < nl ? *reinterpret_cast<const double2*>(S + (size_t)(r0 * NB + row) * n + (size_t)k * NB + q0)
+                                   : make_double2(0.0, 0.0);
+        }
+        if (threadIdx.x < NB) {
+            if (__ballot((unsigned long long)__double_as_longlong(pv) == kUnsetBits) != 0ull &&
+                !poll_block(y + k * NB + lane, pv) && lane == 0) {
+                ok_s = 0;
+                flags[FLAG_STRIDE * 2 * nblk] = 1;
+            }
+            yk[lane] = pv;
         }
         __syncthreads();
-        if (g < nl) bs[g * NB + rw] -= (part[g][0][rw] + part[g][1][rw]) + (part[g][2][rw] + part[g][3][rw]);
+        if (!ok_s) return;
+        const double y0 = yk[q0], y1 = yk[q0 + 1];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            double t = v[i].x * y0 + v[i].y * y1;
+#pragma unroll
+            for (int off = 16; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+            const int row = 2 * (g * NI + i) + h;
+            if ((lane & 31) == 0 && (row >> 6) < nl) bs[row] -= t;
+        }
         __syncthreads();
     }
     for (int rl = 0; rl < nl; ++rl) {
         const int r = r0 + rl;
         // the later local blocks' rows of L_.r (final): loaded now, applied after y_r
-        double v[TG - 1][16];
+        constexpr int NI2 = NB / 8;
+        double2 v[TG - 1][NI2];
 #pragma unroll
         for (int b2 = 0; b2 < TG - 1; ++b2)
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int rb = rl + 1 + b2;
-                v[b2][u] = rb < nl ? S[(size_t)((r0 + rb) * NB + rw) * n + (size_t)r * NB + g * 16 + u] : 0.0;
+            for (int i = 0; i < NI2; ++i) {
+                const int rb = rl + 1 + b2, row = 2 * (g * NI2 + i) + h;
+                v[b2][i] = rb < nl ? *reinterpret_cast<const double2*>(S + (size_t)((r0 + rb) * NB + row) * n + (size_t)r * NB + q0)
+                                   : make_double2(0.0, 0.0);
             }
-        if (threadIdx.x < NB) {
+        {   // y_r = Linv_rr b_r as the four 16-column group sums (trsv_fwd_kernel)
             double t = 0.0;
-            for (int q = 0; q <= (int)threadIdx.x; ++q) t += LiS[rl][threadIdx.x * LIS + q] * bs[rl * NB + q];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int q = 16 * g + u;
+                if (q <= rw) t += LiS[rl][rw * LIS + q] * bs[rl * NB + q];
+            }
+            part[0][g][rw] = t;
+        }
+        __syncthreads();
+        if (threadIdx.x < NB) {
+            const double t = (part[0][0][rw] + part[0][1][rw]) + (part[0][2][rw] + part[0][3][rw]);
             st_sc1(y + r * NB + threadIdx.x, t);
             yk[threadIdx.x] = t;
             b[r * NB + threadIdx.x] = bs[rl * NB + threadIdx.x];
         }
-        flag_publish(flags + FLAG_STRIDE * r);
+        __syncthreads();  // yk
+        const double y0 = yk[q0], y1 = yk[q0 + 1];
 #pragma unroll
-        for (int b2 = 0; b2 < TG - 1; ++b2) {
-            double t = 0.0;
+        for (int b2 = 0; b2 < TG - 1; ++b2)
 #pragma unroll
-            for (int u = 0; u < 16; ++u) t += v[b2][u] * yk[g * 16 + u];
-            part[b2][g][rw] = t;
-        }
-        __syncthreads();
-        for (int b2 = 0; b2 < TG - 1; ++b2) {
-            const int rb = rl + 1 + b2;
-            if (g == 0 && rb < nl)
-                bs[rb * NB + rw] -= (part[b2][0][rw] + part[b2][1][rw]) + (part[b2][2][rw] + part[b2][3][rw]);
-        }
+            for (int i = 0; i < NI2; ++i) {
+                double t = v[b2][i].x * y0 + v[b2][i].y * y1;
+#pragma unroll
+                for (int off = 16; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+                const int rb = rl + 1 + b2, row = 2 * (g * NI2 + i) + h;
+                if ((lane & 31) == 0 && rb < nl) bs[rb * NB + row] -= t;
+            }
         __syncthreads();
     }
 }
 
 // backward: workgroup j owns column blocks c = nblk - 1 - (TG j + cl) (the last ones first):
 // y_c -= L_kc^T x_k for k = nblk-1 .. c+1 (k order, each as the four 16-row group sums
-// ((p0 + p1) + (p2 + p3))), x_c = Linv_cc^T y_c.  flags[FLAG_STRIDE (nblk + k)] != 0: x_k is final.
+// ((p0 + p1) + (p2 + p3))), x_c = Linv_cc^T y_c.  x_k is final once none of its values is the unset pattern.
 __global__ void __launch_bounds__(256) trsv_bwd_persistent_kernel(const double* S, int n, const double* Linv,
                                                                   double* y, double* x, int* flags) {
     __shared__ double ys[TG * NB];  // ys[cl NB + i]: column block c_hi - cl
@@ -961,20 +1016,24 @@ __global__ void __launch_bounds__(256) trsv_bwd_persistent_kernel(const double* 
     if (threadIdx.x == 0) ok_s = 1;
     __syncthreads();
     for (int k = nblk - 1; k > c_hi; --k) {
+        double pv = 0.0;
+        if (threadIdx.x < NB) pv = ld_sc1(x + k * NB + cl);  // first poll, ahead of the column loads
         double v[TG][16];
 #pragma unroll
         for (int bl = 0; bl < TG; ++bl)
 #pragma unroll
             for (int u = 0; u < 16; ++u)
                 v[bl][u] = bl < nl ? S[(size_t)(k * NB + g * 16 + u) * n + (size_t)(c_hi - bl) * NB + cl] : 0.0;
-        if (threadIdx.x == 0 && !flag_wait(flags + FLAG_STRIDE * (nblk + k))) {
-            ok_s = 0;
-            flags[FLAG_STRIDE * 2 * nblk] = 1;
+        if (threadIdx.x < NB) {
+            if (__ballot((unsigned long long)__double_as_longlong(pv) == kUnsetBits) != 0ull &&
+                !poll_block(x + k * NB + cl, pv) && cl == 0) {
+                ok_s = 0;
+                flags[FLAG_STRIDE * 2 * nblk] = 1;
+            }
+            xk[cl] = pv;
         }
         __syncthreads();
         if (!ok_s) return;
-        if (threadIdx.x < NB) xk[threadIdx.x] = ld_sc1(x + k * NB + threadIdx.x);
-        __syncthreads();
 #pragma unroll
         for (int bl = 0; bl < TG; ++bl) {
             double t = 0.0;
@@ -997,14 +1056,23 @@ __global__ void __launch_bounds__(256) trsv_bwd_persistent_kernel(const double* 
                 const int cb = bl + 1 + b2;
                 v[b2][u] = cb < nl ? S[(size_t)(c * NB + g * 16 + u) * n + (size_t)(c_hi - cb) * NB + cl] : 0.0;
             }
-        if (threadIdx.x < NB) {
+        {   // x_c = Linv_cc^T y_c as the four 16-row group sums (trsv_bwd_kernel)
             double t = 0.0;
-            for (int q = threadIdx.x; q < NB; ++q) t += LiS[bl][q * LIS + threadIdx.x] * ys[bl * NB + q];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int q = 16 * g + u;
+                if (q >= cl) t += LiS[bl][q * LIS + cl] * ys[bl * NB + q];
+            }
+            part[0][g][cl] = t;
+        }
+        __syncthreads();
+        if (threadIdx.x < NB) {
+            const double t = (part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]);
             st_sc1(x + c * NB + threadIdx.x, t);
             xk[threadIdx.x] = t;
             y[c * NB + threadIdx.x] = ys[bl * NB + threadIdx.x];
         }
-        flag_publish(flags + FLAG_STRIDE * (nblk + c));
+        __syncthreads();  // xk
 #pragma unroll
         for (int b2 = 0; b2 < TG - 1; ++b2) {
             double t = 0.0;
@@ -1254,11 +1322,14 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
 hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
     if (A.flags && nblk >= 1 && nblk <= 256) {  // every block resident: the persistent solves
-        hipError_t e = hipMemsetAsync(A.flags, 0, sizeof(int) * FLAG_STRIDE * (2 * (size_t)nblk + 1), s);
+        // y: the unset pattern (polled by the forward solve; x is reset by the forward kernel); the
+        // timeout word cleared
+        hipError_t e = hipMemsetAsync(A.yv, 0xff, sizeof(double) * (size_t)n, s);
+        if (e == hipSuccess) e = hipMemsetAsync(A.flags + FLAG_STRIDE * 2 * (size_t)nblk, 0, sizeof(int), s);
         if (e != hipSuccess) return e;
         const unsigned g = (unsigned)((nblk + TG - 1) / TG);
         hipLaunchKernelGGL(trsv_fwd_persistent_kernel, dim3(g), dim3(256), 0, s, (const double*)A.S, n,
-                           (const double*)A.Linv, A.bf, A.yv, A.flags);
+                           (const double*)A.Linv, A.bf, A.yv, A.xf, A.flags);
         hipLaunchKernelGGL(trsv_bwd_persistent_kernel, dim3(g), dim3(256), 0, s, (const double*)A.S, n,
                            (const double*)A.Linv, A.yv, A.xf, A.flags);
         return hipGetLastError();
