@@ -913,6 +913,16 @@ __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* 
     // per lane), each row dot reduced over its 32 lanes
     const int lane = threadIdx.x & 63, h = lane >> 5, q0 = 2 * (lane & 31);
     constexpr int NI = TG * NB / 8;  // row pairs per wave and step
+    // L_(r0+1),r0 (final; needed between y_r0 and y_r0+1, on the hand-off chain): loaded up front
+    static_assert(TG == 2, "one later local block");
+    constexpr int NI2 = NB / 8;
+    double2 v21[NI2];
+#pragma unroll
+    for (int i = 0; i < NI2; ++i) {
+        const int row = 2 * (g * NI2 + i) + h;
+        v21[i] = nl == 2 ? *reinterpret_cast<const double2*>(S + (size_t)((r0 + 1) * NB + row) * n + (size_t)r0 * NB + q0)
+                         : make_double2(0.0, 0.0);
+    }
     for (int k = 0; k < r0; ++k) {
         double pv = 0.0;
         if (threadIdx.x < NB) pv = ld_sc1(y + k * NB + lane);  // first poll, ahead of the row loads
@@ -946,17 +956,7 @@ __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* 
     }
     for (int rl = 0; rl < nl; ++rl) {
         const int r = r0 + rl;
-        // the later local blocks' rows of L_.r (final): loaded now, applied after y_r
-        constexpr int NI2 = NB / 8;
-        double2 v[TG - 1][NI2];
-#pragma unroll
-        for (int b2 = 0; b2 < TG - 1; ++b2)
-#pragma unroll
-            for (int i = 0; i < NI2; ++i) {
-                const int rb = rl + 1 + b2, row = 2 * (g * NI2 + i) + h;
-                v[b2][i] = rb < nl ? *reinterpret_cast<const double2*>(S + (size_t)((r0 + rb) * NB + row) * n + (size_t)r * NB + q0)
-                                   : make_double2(0.0, 0.0);
-            }
+        // the later local block's rows of L_.r: L_(r0+1),r0 (v21, loaded at the start)
         {   // y_r = Linv_rr b_r as the four 16-column group sums (trsv_fwd_kernel)
             double t = 0.0;
 #pragma unroll
@@ -974,17 +974,17 @@ __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* 
             b[r * NB + threadIdx.x] = bs[rl * NB + threadIdx.x];
         }
         __syncthreads();  // yk
-        const double y0 = yk[q0], y1 = yk[q0 + 1];
-#pragma unroll
-        for (int b2 = 0; b2 < TG - 1; ++b2)
+        if (rl + 1 < nl) {
+            const double y0 = yk[q0], y1 = yk[q0 + 1];
 #pragma unroll
             for (int i = 0; i < NI2; ++i) {
-                double t = v[b2][i].x * y0 + v[b2][i].y * y1;
+                double t = v21[i].x * y0 + v21[i].y * y1;
 #pragma unroll
                 for (int off = 16; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-                const int rb = rl + 1 + b2, row = 2 * (g * NI2 + i) + h;
-                if ((lane & 31) == 0 && rb < nl) bs[rb * NB + row] -= t;
+                const int row = 2 * (g * NI2 + i) + h;
+                if ((lane & 31) == 0) bs[NB + row] -= t;
             }
+        }
         __syncthreads();
     }
 }
@@ -1001,6 +1001,11 @@ __global__ void __launch_bounds__(256) trsv_bwd_persistent_kernel(const double* 
     __shared__ int ok_s;
     const int nblk = n / NB, c_hi = nblk - 1 - TG * blockIdx.x, nl = min(TG, c_hi + 1);
     const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+    // L_c_hi,(c_hi-1) (needed between x_c_hi and x_c_hi-1, on the hand-off chain): loaded up front
+    double v12[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+        v12[u] = nl == 2 ? S[(size_t)(c_hi * NB + g * 16 + u) * n + (size_t)(c_hi - 1) * NB + cl] : 0.0;
     for (int e = threadIdx.x; e < nl * NB; e += 256) ys[e] = y[(c_hi - e / NB) * NB + (e % NB)];
     for (int bl = 0; bl < nl; ++bl) {
         const double* Li = Linv + (size_t)(c_hi - bl) * NB * NB;
@@ -1047,15 +1052,7 @@ __global__ void __launch_bounds__(256) trsv_bwd_persistent_kernel(const double* 
     }
     for (int bl = 0; bl < nl; ++bl) {
         const int c = c_hi - bl;
-        // the rows of block c against the later local column blocks (final): loaded now
-        double v[TG - 1][16];
-#pragma unroll
-        for (int b2 = 0; b2 < TG - 1; ++b2)
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int cb = bl + 1 + b2;
-                v[b2][u] = cb < nl ? S[(size_t)(c * NB + g * 16 + u) * n + (size_t)(c_hi - cb) * NB + cl] : 0.0;
-            }
+        // the rows of block c_hi against column block c_hi - 1: v12, loaded at the start
         {   // x_c = Linv_cc^T y_c as the four 16-row group sums (trsv_bwd_kernel)
             double t = 0.0;
 #pragma unroll
@@ -1073,18 +1070,13 @@ __global__ void __launch_bounds__(256) trsv_bwd_persistent_kernel(const double* 
             y[c * NB + threadIdx.x] = ys[bl * NB + threadIdx.x];
         }
         __syncthreads();  // xk
-#pragma unroll
-        for (int b2 = 0; b2 < TG - 1; ++b2) {
+        if (bl + 1 < nl) {
             double t = 0.0;
 #pragma unroll
-            for (int u = 0; u < 16; ++u) t += v[b2][u] * xk[g * 16 + u];
-            part[b2][g][cl] = t;
-        }
-        __syncthreads();
-        for (int b2 = 0; b2 < TG - 1; ++b2) {
-            const int cb = bl + 1 + b2;
-            if (g == 0 && cb < nl)
-                ys[cb * NB + cl] -= (part[b2][0][cl] + part[b2][1][cl]) + (part[b2][2][cl] + part[b2][3][cl]);
+            for (int u = 0; u < 16; ++u) t += v12[u] * xk[g * 16 + u];
+            part[0][g][cl] = t;
+            __syncthreads();
+            if (g == 0) ys[NB + cl] -= (part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]);
         }
         __syncthreads();
     }
