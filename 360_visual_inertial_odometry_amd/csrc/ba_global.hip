@@ -880,8 +880,7 @@ constexpr int TG = 2;
 constexpr int LIS = NB + 1;  // odd LDS row stride
 
 // forward: workgroup j owns row blocks r = TG j + rl: b_r -= L_rk y_k for k = 0 .. r-1 (k order,
-// each row dot as 32 two-term lane products reduced by a butterfly over the half-wave: the row
-// streams as one 512-B segment), y_r = Linv_rr b_r.  y_k is final once none of its 64 values is the unset pattern (poll_block);
+// each row dot reduced over 8 lanes, see below), y_r = Linv_rr b_r.  y_k is final once none of its 64 values is the unset pattern (poll_block);
 // flags[FLAG_STRIDE 2 nblk]: set on a timed-out wait.
 __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* S, int n, const double* Linv,
                                                                   double* b, double* y, double* x, int* flags) {
@@ -909,30 +908,35 @@ __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* 
     }
     if (threadIdx.x == 0) ok_s = 1;
     __syncthreads();
-    // the off-diagonal rows stream as 512-B segments: a wave load instruction covers two rows (16 B
-    // per lane), each row dot reduced over its 32 lanes
-    const int lane = threadIdx.x & 63, h = lane >> 5, q0 = 2 * (lane & 31);
-    constexpr int NI = TG * NB / 8;  // row pairs per wave and step
+    // the off-diagonal rows stream as 128-B row segments, 8 lanes per row: a row dot is 8 two-term
+    // products per lane reduced over its 8 lanes (3 exchange levels: a 32-lane butterfly per row was
+    // a serial chain of LDS permutes, 4.4 us per step against 2.4 us)
+    const int lane = threadIdx.x & 63;
     // L_(r0+1),r0 (final; needed between y_r0 and y_r0+1, on the hand-off chain): loaded up front
     static_assert(TG == 2, "one later local block");
-    constexpr int NI2 = NB / 8;
-    double2 v21[NI2];
+    double2 v21[2][4];  // the main loop's 8-lanes-per-row layout, 16 rows per wave
 #pragma unroll
-    for (int i = 0; i < NI2; ++i) {
-        const int row = 2 * (g * NI2 + i) + h;
-        v21[i] = nl == 2 ? *reinterpret_cast<const double2*>(S + (size_t)((r0 + 1) * NB + row) * n + (size_t)r0 * NB + q0)
-                         : make_double2(0.0, 0.0);
-    }
+    for (int gr = 0; gr < 2; ++gr)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 16 * g + 8 * gr + (lane >> 3);
+            v21[gr][j] = nl == 2 ? *reinterpret_cast<const double2*>(S + (size_t)((r0 + 1) * NB + row) * n + (size_t)r0 * NB + 16 * j + 2 * (lane & 7))
+                                 : make_double2(0.0, 0.0);
+        }
     for (int k = 0; k < r0; ++k) {
         double pv = 0.0;
         if (threadIdx.x < NB) pv = ld_sc1(y + k * NB + lane);  // first poll, ahead of the row loads
-        double2 v[NI];
+        // 8 lanes per row (lane = 8 rr + c8), 4 row groups per wave; instruction j of a group reads
+        // columns [16 j, 16 j + 16) of its 8 rows (128 B per row), lane c8 the pair 16 j + 2 c8
+        double2 v[4][4];
 #pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int row = 2 * (g * NI + i) + h;  // rl NB + row in the block
-            v[i] = (row >> 6) < nl ? *reinterpret_cast<const double2*>(S + (size_t)(r0 * NB + row) * n + (size_t)k * NB + q0)
-                                   : make_double2(0.0, 0.0);
-        }
+        for (int gr = 0; gr < 4; ++gr)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = 32 * g + 8 * gr + (lane >> 3);  // rl NB + row in the block
+                v[gr][j] = (row >> 6) < nl ? *reinterpret_cast<const double2*>(S + (size_t)(r0 * NB + row) * n + (size_t)k * NB + 16 * j + 2 * (lane & 7))
+                                           : make_double2(0.0, 0.0);
+            }
         if (threadIdx.x < NB) {
             if (__ballot((unsigned long long)__double_as_longlong(pv) == kUnsetBits) != 0ull &&
                 !poll_block(y + k * NB + lane, pv) && lane == 0) {
@@ -943,14 +947,21 @@ __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* 
         }
         __syncthreads();
         if (!ok_s) return;
-        const double y0 = yk[q0], y1 = yk[q0 + 1];
+        double yv[4][2];
 #pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            double t = v[i].x * y0 + v[i].y * y1;
+        for (int j = 0; j < 4; ++j) {
+            yv[j][0] = yk[16 * j + 2 * (lane & 7)];
+            yv[j][1] = yk[16 * j + 2 * (lane & 7) + 1];
+        }
 #pragma unroll
-            for (int off = 16; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-            const int row = 2 * (g * NI + i) + h;
-            if ((lane & 31) == 0 && (row >> 6) < nl) bs[row] -= t;
+        for (int gr = 0; gr < 4; ++gr) {
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) t += v[gr][j].x * yv[j][0] + v[gr][j].y * yv[j][1];
+#pragma unroll
+            for (int off = 4; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+            const int row = 32 * g + 8 * gr + (lane >> 3);
+            if ((lane & 7) == 0 && (row >> 6) < nl) bs[row] -= t;
         }
         __syncthreads();
     }
@@ -975,14 +986,15 @@ __global__ void __launch_bounds__(256) trsv_fwd_persistent_kernel(const double* 
         }
         __syncthreads();  // yk
         if (rl + 1 < nl) {
-            const double y0 = yk[q0], y1 = yk[q0 + 1];
 #pragma unroll
-            for (int i = 0; i < NI2; ++i) {
-                double t = v21[i].x * y0 + v21[i].y * y1;
+            for (int gr = 0; gr < 2; ++gr) {
+                double t = 0.0;
 #pragma unroll
-                for (int off = 16; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-                const int row = 2 * (g * NI2 + i) + h;
-                if ((lane & 31) == 0) bs[NB + row] -= t;
+                for (int j = 0; j < 4; ++j)
+                    t += v21[gr][j].x * yk[16 * j + 2 * (lane & 7)] + v21[gr][j].y * yk[16 * j + 2 * (lane & 7) + 1];
+#pragma unroll
+                for (int off = 4; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+                if ((lane & 7) == 0) bs[NB + 16 * g + 8 * gr + (lane >> 3)] -= t;
             }
         }
         __syncthreads();
