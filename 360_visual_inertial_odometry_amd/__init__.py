@@ -114,7 +114,7 @@ def lib():
     L.vio_ba_record_bytes.restype = C.c_size_t
     L.vio_ba_batch_record_bytes.argtypes = [vp, C.POINTER(C.c_size_t)]
     L.vio_ba_batch_pack.argtypes = [vp, vp, C.c_int]
-    L.vio_ba_record_unpack.argtypes = [vp, C.POINTER(abi.VioBaOutput)]
+    L.vio_ba_record_unpack.argtypes = [vp, C.c_size_t, C.POINTER(abi.VioBaOutput)]
     L.vio_ba_gather.argtypes = [C.POINTER(abi.VioMapView), C.c_int, C.c_int, C.c_int, C.POINTER(abi.VioBaGatherOut)]
     L.vio_ba_write_back.argtypes = [C.POINTER(abi.VioMapView), C.c_int, C.POINTER(abi.VioBaGatherOut),
                                     C.POINTER(abi.VioBaOutput), C.POINTER(abi.VioBaMapUpdate)]
@@ -395,9 +395,13 @@ def record_bytes(K, L, N):
 def unpack_record(rec):
     """vio_ba_record_unpack (host): one packed record (uint8 array) -> result dict (no chi2 / trace)."""
     rec = np.ascontiguousarray(rec, np.uint8)
+    if rec.size < 16:
+        raise VioError("vio_ba_record_unpack: record shorter than its header")
     K, L, N = (int(v) for v in rec[:12].view(np.int32))
+    if K <= 0 or L < 0 or N < 0 or record_bytes(K, L, N) > rec.size:
+        raise VioError(f"vio_ba_record_unpack: header K={K} L={L} N={N} does not fit a {rec.size}-byte record")
     o = BaOutput(K, L, N)
-    rc = lib().vio_ba_record_unpack(_p(rec), C.byref(o.c))
+    rc = lib().vio_ba_record_unpack(_p(rec), rec.size, C.byref(o.c))
     if rc != 0:
         raise VioError(f"vio_ba_record_unpack failed ({rc})")
     r = o.result()

@@ -63,6 +63,10 @@ struct GbaArgs {
     int* flags;               // [32 (3 nfp/64 + 1)] triangular-solve flags, one per 128 B (+ timeout word), Cholesky step flags
 };
 
+// the word a timed-out inter-workgroup wait of the Cholesky / triangular solves sets (cleared at the start
+// of every gba_launch_cholesky); nonzero after a step means a device fault, not a failed factorisation
+inline int* gba_timeout_word(const GbaArgs& A) { return A.flags ? A.flags + 32 * 2 * (size_t)(A.nfp / 64) : nullptr; }
+
 hipError_t gba_launch_setup(const GbaArgs& A, hipStream_t s);
 // mode 0 cost of active blocks, 1 + Jacobians, 2 cost of the constant blocks; out[0] = cost
 hipError_t gba_launch_eval(const GbaArgs& A, const double* xp, const double* xl, int mode, double* partial,

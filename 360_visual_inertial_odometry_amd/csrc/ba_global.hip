@@ -632,8 +632,9 @@ __global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k,
 }
 
 // forward substitution step k: y_k = Linv_kk b_k (every block recomputes it from the final b_k;
-// block 0 publishes it), then b_r -= L_rk y_k for the rows below: one wavefront per row, coalesced
-// 512-B row segment, shuffle reduction
+// block 0 publishes it), then b_r -= L_rk y_k for the 32 rows of the block below: 8 lanes per row,
+// each lane two-term products over 4 double2 column pairs, reduced over its 8 lanes — the row dot of
+// trsv_fwd_persistent_kernel in the same order, so both paths give the same bits
 __global__ void __launch_bounds__(256) trsv_fwd_kernel(const double* S, int n, int k, const double* Linv, double* b,
                                                        double* y) {
     __shared__ double yk[NB];
@@ -653,24 +654,25 @@ __global__ void __launch_bounds__(256) trsv_fwd_kernel(const double* S, int n, i
     if (threadIdx.x < NB) yk[threadIdx.x] = (pt[0][threadIdx.x] + pt[1][threadIdx.x]) + (pt[2][threadIdx.x] + pt[3][threadIdx.x]);
     __syncthreads();
     if (blockIdx.x == 0 && threadIdx.x < NB) y[k * NB + threadIdx.x] = yk[threadIdx.x];
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const double ylane = yk[lane];
-    // the wave's four rows: loads first, then the four reductions
-    const int rb = (k + 1) * NB + blockIdx.x * 16 + wid, rend = min(n, (k + 1) * NB + (blockIdx.x + 1) * 16);
-    double sv[4];
+    const int lane = threadIdx.x & 63, c8 = lane & 7;
+    const int r = (k + 1) * NB + blockIdx.x * 32 + (threadIdx.x >> 3);
+    double2 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int r = rb + 4 * u;
-        sv[u] = r < rend ? S[(size_t)r * n + (size_t)k * NB + lane] : 0.0;
+    for (int j = 0; j < 4; ++j)
+        v[j] = r < n ? *reinterpret_cast<const double2*>(S + (size_t)r * n + (size_t)k * NB + 16 * j + 2 * c8)
+                     : make_double2(0.0, 0.0);
+    double yv[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        yv[j][0] = yk[16 * j + 2 * c8];
+        yv[j][1] = yk[16 * j + 2 * c8 + 1];
     }
+    double t = 0.0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int r = rb + 4 * u;
-        double s = sv[u] * ylane;
+    for (int j = 0; j < 4; ++j) t += v[j].x * yv[j][0] + v[j].y * yv[j][1];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        if (lane == 0 && r < rend) b[r] -= s;
-    }
+    for (int off = 4; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+    if (c8 == 0 && r < n) b[r] -= t;
 }
 
 // backward substitution step k (k = nblk-1 .. 0): x_k = Linv_kk^T y_k, y_c -= sum_q L[kNB+q][c] x_k[q]
@@ -728,9 +730,13 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 __device__ __forceinline__ void st_sc1(double* p, double v) {
     __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// bounded spins: each poll is an sc1 load round trip (~1-2 us under load), so 2^19 polls give up after
+// about a second, orders of magnitude above any legitimate wait (a whole LM iteration is ~6 ms); a
+// timed-out wait sets the solve's timeout word, which the host reports as a device error
+constexpr int kSpinMax = 1 << 19;
 __device__ __forceinline__ bool flag_wait(int* f) {
     // bounded spin: a producer that never arrives ends the wait instead of hanging the GPU
-    for (int it = 0; it < (1 << 24); ++it) {
+    for (int it = 0; it < kSpinMax; ++it) {
         if (__hip_atomic_load((gint*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
         __builtin_amdgcn_s_sleep(1);
     }
@@ -742,7 +748,7 @@ __device__ __forceinline__ bool flag_wait(int* f) {
 constexpr unsigned long long kUnsetBits = ~0ull;
 __device__ __forceinline__ bool poll_block(const double* p, double& v) {
     bool pend = true;
-    for (int it = 0; it < (1 << 24); ++it) {
+    for (int it = 0; it < kSpinMax; ++it) {
         if (pend) {
             v = ld_sc1(p);
             pend = (unsigned long long)__double_as_longlong(v) == kUnsetBits;
@@ -766,7 +772,8 @@ __device__ __forceinline__ void flag_publish(int* f) {
 // and chol_trsm_kernel's, in the same order: bitwise the three-launch step.  k == 0: no update.
 // Dynamic LDS: CHOL_DIAG_LDS bytes.  flag: 0 pending, 1 L_kk^-1 final, 2 the block is not positive
 // definite.
-__global__ void __launch_bounds__(256) chol_step_kernel(double* S, int n, int k, double* Linv, int* fail, int* flag) {
+__global__ void __launch_bounds__(256) chol_step_kernel(double* S, int n, int k, double* Linv, int* fail, int* flag,
+                                                        int* tmo) {
     extern __shared__ double dyn[];
     double (*As)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(dyn);
     double (*Bs)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(dyn + NB * TLD);
@@ -843,7 +850,7 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* S, int n, int k,
     if (threadIdx.x == 0) {
         const bool arrived = flag_wait(flag);
         ok_s = arrived && __hip_atomic_load((gint*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
-        if (!arrived) *fail = 1;
+        if (!arrived) *tmo = 1;  // a device fault, not a failed factorisation
     }
     __syncthreads();
     if (!ok_s) return;
@@ -1273,6 +1280,11 @@ hipError_t gba_cholesky_attributes() {
 constexpr int kGbaFuseM = 96;  // chol_step_kernel for steps with at most this many block rows (config 5: every step)
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
+    int* tmo = A.flags ? A.flags + FLAG_STRIDE * 2 * (size_t)nblk : nullptr;  // timeout word of the Cholesky + solves
+    if (tmo) {
+        const hipError_t e0 = hipMemsetAsync(tmo, 0, sizeof(int), s);
+        if (e0 != hipSuccess) return e0;
+    }
     hipStream_t r = A.side;
     hipEvent_t ev_panel = A.ev[0], ev_rest = A.ev[1];
     if (!r || !ev_panel || !ev_rest) {  // no side stream: the plain schedule
@@ -1301,7 +1313,7 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
         const int m = nblk - k - 1;
         if (m + 1 <= fuse_m) {
             hipLaunchKernelGGL(chol_step_kernel, dim3(m + 1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv, fail,
-                               sflag + FLAG_STRIDE * k);
+                               sflag + FLAG_STRIDE * k, tmo);
             return;
         }
         if (k > 0) hipLaunchKernelGGL(chol_syrk_kernel, dim3(m + 1), dim3(256), 0, s, A.S, n, k - 1, 1);
@@ -1325,11 +1337,14 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
 }
 hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
-    if (A.flags && nblk >= 1 && nblk <= 256) {  // every block resident: the persistent solves
+    static const bool per_step = [] {  // VIO_GBA_PERSISTENT_SOLVE=0: the per-step kernels (A/B tests)
+        const char* v = std::getenv("VIO_GBA_PERSISTENT_SOLVE");
+        return v && v[0] == '0';
+    }();
+    if (A.flags && nblk >= 1 && nblk <= 256 && !per_step) {  // every block resident: the persistent solves
         // y: the unset pattern (polled by the forward solve; x is reset by the forward kernel); the
-        // timeout word cleared
+        // timeout word was cleared before the Cholesky (gba_launch_cholesky)
         hipError_t e = hipMemsetAsync(A.yv, 0xff, sizeof(double) * (size_t)n, s);
-        if (e == hipSuccess) e = hipMemsetAsync(A.flags + FLAG_STRIDE * 2 * (size_t)nblk, 0, sizeof(int), s);
         if (e != hipSuccess) return e;
         const unsigned g = (unsigned)((nblk + TG - 1) / TG);
         hipLaunchKernelGGL(trsv_fwd_persistent_kernel, dim3(g), dim3(256), 0, s, (const double*)A.S, n,
@@ -1340,7 +1355,7 @@ hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {
     }
     for (int k = 0; k < nblk; ++k) {
         int rows = n - (k + 1) * NB;
-        int nb = rows > 0 ? (rows + 15) / 16 : 1;
+        int nb = rows > 0 ? (rows + 31) / 32 : 1;
         hipLaunchKernelGGL(trsv_fwd_kernel, dim3(nb), dim3(256), 0, s, (const double*)A.S, n, k,
                            (const double*)A.Linv, A.bf, A.yv);
     }

@@ -80,7 +80,7 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
         for (int o = 1; o < N; ++o)
             if (key[o] == key[o - 1]) { set_error(ctx, "duplicate (keyframe, landmark) observation"); return VIO_EINVAL; }
     }
-    (void)hipSetDevice(ctx->device);
+    DeviceScope _vio_dev_scope(ctx->device);
     hipStream_t st = ctx->stream;
     // ---- reduced problem (Ceres RemoveFixedBlocks; points are the e-blocks) ----
     std::vector<uint8_t> pose_used(K, 0), lm_used(L, 0), active(N, 0);
@@ -331,9 +331,14 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             GBA_CHECK(gba_launch_backsub(A, partial, scal + 3, st));
             GBA_CHECK(gba_launch_model(A, partial, scal + 4, st));
             GBA_CHECK(gba_launch_eval(A, A.c_pose, A.c_lm, 0, partial, scal + 7, st));
-            int hfail = 0;
+            int hfail = 0, htmo = 0;
             GBA_CHECK(hipMemcpyAsync(&hfail, dfail, sizeof(int), hipMemcpyDeviceToHost, st));
+            if (int* tw = gba_timeout_word(A)) GBA_CHECK(hipMemcpyAsync(&htmo, tw, sizeof(int), hipMemcpyDeviceToHost, st));
             if ((rc = read(h, 0, 8))) return rc;
+            if (htmo) {  // an inter-workgroup wait timed out: report the fault instead of an invalid LM step
+                set_error(ctx, "global BA: a Cholesky / triangular-solve hand-off timed out on the device");
+                return VIO_EDEVICE;
+            }
             bool valid = h[2] == 0.0 && hfail == 0 && h[3] == 0.0;
             model_change = h[4];
             if (valid) it.model_cost_change = model_change;

@@ -38,7 +38,8 @@ int hip_fail(vio_ctx* ctx, hipError_t e, const char* what) {
 }
 void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes) {
     // the buffer must live on the context's device whatever device the calling thread has current
-    if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.err != hipSuccess) return nullptr;
     if ((int)ctx->bufs.size() <= slot) {
         ctx->bufs.resize(slot + 1, nullptr);
         ctx->caps.resize(slot + 1, 0);
@@ -413,7 +414,7 @@ static bool force_monolithic(const vio_ctx* ctx, const BaDevice& d) {
 }
 
 static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     if (timed) VIO_HIP(ctx, hipEventRecord(d.ev0, ctx->stream));
     bool any_pnp = false, any_other = false;
     for (const BaWin& w : d.pk.win) (w.is_pnp ? any_pnp : any_other) = true;
@@ -485,7 +486,8 @@ int vio_ctx_create(int device, vio_ctx** out) {
         g_create_error = "device index out of range";
         return VIO_EINVAL;
     }
-    if (hipSetDevice(device) != hipSuccess) {
+    DeviceScope dev_scope(device);
+    if (dev_scope.err != hipSuccess) {
         g_create_error = "hipSetDevice failed";
         return VIO_EDEVICE;
     }
@@ -502,7 +504,7 @@ int vio_ctx_create(int device, vio_ctx** out) {
 
 void vio_ctx_destroy(vio_ctx* ctx) {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
+    DeviceScope _vio_dev_scope(ctx->device);
     for (void* p : ctx->bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : ctx->imu_ev)
@@ -524,7 +526,7 @@ const char* vio_ctx_last_error(const vio_ctx* ctx) {
 int vio_ba_batch_create(vio_ctx* ctx, const vio_ba_problem* probs, int n, vio_ba_batch** out) {
     if (!ctx || !probs || n <= 0 || !out) return VIO_EINVAL;
     *out = nullptr;
-    (void)hipSetDevice(ctx->device);
+    DeviceScope _vio_dev_scope(ctx->device);
     vio_ba_batch* b = new vio_ba_batch();
     b->ctx = ctx;
     b->dev.n = n;
@@ -563,7 +565,7 @@ int vio_ba_batch_set_preint(vio_ba_batch* b, const vio_preint* src, int count, i
     }
     if (count == 0) return VIO_OK;
     const size_t bytes = sizeof(vio_preint) * (size_t)count;
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     if (on_device) {
         VIO_HIP(ctx, hipMemcpyAsync((void*)b->dev.P.preint, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
     } else {
@@ -631,7 +633,7 @@ int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out) {
 
 void vio_ba_batch_destroy(vio_ba_batch* b) {
     if (!b) return;
-    (void)hipSetDevice(b->ctx->device);
+    DeviceScope _vio_dev_scope(b->ctx->device);
     (void)hipStreamSynchronize(b->ctx->stream);
     free_batch(b->dev);
     delete b;
@@ -655,7 +657,7 @@ int vio_ba_batch_pack(vio_ba_batch* b, void* dst, int on_device) {
     vio_ctx* ctx = b->ctx;
     size_t rb = 0;
     vio_ba_batch_record_bytes(b, &rb);
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     uint8_t* d = static_cast<uint8_t*>(dst);
     if (!on_device) {
         d = static_cast<uint8_t*>(ctx_buffer(ctx, kSlotRecords, rb * b->dev.n));
@@ -670,14 +672,15 @@ int vio_ba_batch_pack(vio_ba_batch* b, void* dst, int on_device) {
     return VIO_OK;
 }
 
-int vio_ba_record_unpack(const void* record, vio_ba_output* out) {
-    if (!record || !out) return VIO_EINVAL;
+int vio_ba_record_unpack(const void* record, size_t record_bytes, vio_ba_output* out) {
+    if (!record || !out || record_bytes < 16) return VIO_EINVAL;
     const uint8_t* rec = static_cast<const uint8_t*>(record);
     int32_t hdr[4];
     std::memcpy(hdr, rec, sizeof hdr);
     const int K = hdr[0], L = hdr[1], N = hdr[2];
     if (K <= 0 || L < 0 || N < 0 || hdr[3] != VIO_BA_RECORD_VERSION) return VIO_EINVAL;
     const RecLayout R = rec_layout(K, L, N);
+    if ((uint64_t)R.total > (uint64_t)record_bytes) return VIO_EINVAL;  // the header's layout overruns the record
     if (out->T_wb)
         for (int k = 0; k < K; ++k) {
             std::memcpy(out->T_wb[k].R, rec + R.T + 96 * k, 9 * sizeof(double));

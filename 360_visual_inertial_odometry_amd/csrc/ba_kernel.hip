@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "ba_types.h"
 #include "ba_factor_dev.h"
@@ -2201,21 +2202,27 @@ size_t ba_shared_bytes() { return sizeof(BaShared); }
 size_t ba_ws_extra_doubles() { return ba_ws_extra(); }
 
 // kernel attributes are per device: one flag per device ordinal (the caller has selected the
-// context's device)
+// context's device).  Contexts on one device may live on different host threads (one vio_ctx per
+// thread): the flags are read and set under one lock, so no thread launches before the attribute
+// call that another thread started has returned.
 constexpr int kMaxDevices = 64;
 static int current_device() {
     int d = 0;
     return hipGetDevice(&d) == hipSuccess && d >= 0 && d < kMaxDevices ? d : 0;
 }
+static std::mutex g_attr_mutex;
 
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream) {
-    static bool attr_set[kMaxDevices] = {};
-    const int dev = current_device();
-    if (!attr_set[dev]) {
-        hipError_t e = hipFuncSetAttribute((const void*)ba_window_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)sizeof(BaShared));
-        if (e != hipSuccess) return e;
-        attr_set[dev] = true;
+    {
+        static bool attr_set[kMaxDevices] = {};
+        std::lock_guard<std::mutex> lock(g_attr_mutex);
+        const int dev = current_device();
+        if (!attr_set[dev]) {
+            hipError_t e = hipFuncSetAttribute((const void*)ba_window_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)sizeof(BaShared));
+            if (e != hipSuccess) return e;
+            attr_set[dev] = true;
+        }
     }
     hipLaunchKernelGGL(ba_window_kernel, dim3(n), dim3(BA_THREADS), sizeof(BaShared), stream, P);
     return hipGetLastError();

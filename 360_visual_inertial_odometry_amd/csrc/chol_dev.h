@@ -85,4 +85,70 @@ __device__ __forceinline__ int chol16_wave(double* A, int ld, double* lbt, doubl
     return bad;
 }
 
+// One wave solves the n x n SPD system A x = b (n <= NMAX - 1) by an unblocked right-looking
+// Cholesky in registers, with no workgroup barrier: lane i holds row i of A (lower part; entries
+// above the diagonal are zero), lane n holds b, so the factorisation itself runs the forward
+// substitution (lane n ends with y = L^-1 b).  Pivot j: the pivot is broadcast by v_readlane, the
+// column c_i = L[i][j] is published to LDS (col, two buffers of NMAX doubles) and every lane updates
+// its row d[k] -= c_i L[k][j] (k > j) from broadcast LDS reads; L[i][j] is the textbook
+// (A[i][j] - sum_{m<j} L[i][m] L[j][m]) / L[j][j] with the sum in ascending m.  Then L is written back
+// over A (full rows, zeros above the diagonal), read column-wise (odd row stride: conflict-free), and
+// the backward substitution x_m = (y_m - sum_{k>m} L[k][m] x_k) / L[m][m] runs column-oriented with
+// one broadcast per step.  x (LDS, n) may alias b.  Returns nonzero (the same on every lane) if a pivot
+// is not positive.  Used for the diagonal blocks of the window's reduced system: with the reference's
+// zero IMU pose Jacobians (Factors.cpp:1415-1419, 1471-1475) the pose block and the velocity/bias
+// block of S are uncoupled and each is factored by its own wave.
+template <int NMAX>
+__device__ __forceinline__ int chol_wave_solve(double* A, int lda, const double* b, int n, double* x, double* col,
+                                               int lane) {
+    double d[NMAX];
+    const double* arow = A + lane * lda;
+#pragma unroll
+    for (int k = 0; k < NMAX; ++k) d[k] = lane < n ? (k <= lane ? arow[k] : 0.0) : (lane == n && k < n ? b[k] : 0.0);
+    int bad = 0;
+    double dinv = 0.0;  // 1 / L[lane][lane]
+#pragma unroll
+    for (int j = 0; j < NMAX - 1; ++j) {
+        if (j < n) {
+            const double piv = readlane_d(d[j], j);
+            bad |= !(piv > 0.0);
+            const double r = rsq_nr(piv);
+            const double c = lane == j ? piv * r : d[j] * r;
+            d[j] = c;
+            if (lane == j) dinv = r;
+            double* cb = col + (j & 1) * NMAX;
+            cb[lane] = c;
+            wave_lds_sync();
+#pragma unroll
+            for (int k = j + 1; k < NMAX; ++k) d[k] -= c * cb[k];
+        }
+    }
+    // lane n publishes y; L (rows) over A
+    if (lane == n) {
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k) col[k] = d[k];
+    }
+    if (lane < n) {
+        double* w = A + lane * lda;
+#pragma unroll
+        for (int k = 0; k < NMAX; ++k)
+            if (k < n) w[k] = k <= lane ? d[k] : 0.0;
+    }
+    wave_lds_sync();
+    double e[NMAX];  // column `lane` of L: e[m] = L[m][lane] (zero for m < lane)
+#pragma unroll
+    for (int m = 0; m < NMAX; ++m) e[m] = (m < n && lane < n) ? A[m * lda + lane] : 0.0;
+    double t = lane < n ? col[lane] : 0.0;
+#pragma unroll
+    for (int m = NMAX - 2; m >= 0; --m) {
+        if (m < n) {
+            const double xm = readlane_d(t * dinv, m);
+            t = lane == m ? xm : t - e[m] * xm;
+        }
+    }
+    if (lane < n) x[lane] = t;
+    wave_lds_sync();
+    return bad;
+}
+
 }  // namespace vio360

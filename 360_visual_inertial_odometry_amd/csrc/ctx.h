@@ -46,6 +46,27 @@ enum { kSlotImuInit = 16 };
 // vio_mono_init_solve inputs, outputs and scratch
 enum { kSlotMonoInit = 17 };
 
+// Selects a device for the rest of the enclosing scope and restores the calling thread's current
+// device on exit, so a C-ABI call never leaves the caller's thread on the context's device (a process
+// that also drives other GPUs, e.g. through torch, keeps its own current device).
+struct DeviceScope {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceScope(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) err = hipSetDevice(dev);
+        else prev = -1;  // nothing to restore
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+#define VIO_DEVICE(ctx)                     \
+    DeviceScope _vio_dev_scope((ctx)->device); \
+    VIO_HIP(ctx, _vio_dev_scope.err)
+
 #define VIO_HIP(ctx, expr)                                  \
     do {                                                    \
         hipError_t _e = (expr);                             \

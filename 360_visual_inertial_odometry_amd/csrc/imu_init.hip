@@ -733,7 +733,7 @@ extern "C" int vio_imu_init_solve(vio_ctx* ctx, const vio_imu_init_problem* prob
     const size_t b_v = ((sizeof(double) * hv.size()) + 255) & ~size_t(255);
     const size_t b_o = ((sizeof(IiOut) * hp.size()) + 255) & ~size_t(255);
     const size_t b_s = sizeof(double) * scratch;
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     auto* d = static_cast<char*>(ctx_buffer(ctx, kSlotImuInit, b_p + b_f + 2 * b_v + b_o + b_s));
     if (!d) {
         set_error(ctx, "vio_imu_init_solve: device allocation failed");

@@ -292,7 +292,7 @@ static size_t align_up(size_t v, size_t al) { return (v + al - 1) / al * al; }
 using namespace vio360;
 
 static int launch_preint(vio_ctx* ctx, const ImuArgs& a) {
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     for (hipEvent_t& ev : ctx->imu_ev)
         if (!ev) VIO_HIP(ctx, hipEventCreate(&ev));
     VIO_HIP(ctx, hipEventRecord(ctx->imu_ev[0], ctx->stream));
@@ -349,7 +349,7 @@ extern "C" int vio_imu_preintegrate(vio_ctx* ctx, const vio_imu_data* imu, int n
         return VIO_ENOMEM;
     }
     hipStream_t st = ctx->stream;
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     VIO_HIP(ctx, hipMemcpyAsync(d_imu, imu, sizeof(vio_imu_data) * (size_t)n_imu, hipMemcpyHostToDevice, st));
     ImuArgs a;
     a.imu = d_imu;

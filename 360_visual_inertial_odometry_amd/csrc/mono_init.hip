@@ -385,7 +385,7 @@ extern "C" int vio_mono_init_solve(vio_ctx* ctx, const float* bearings1, const f
                  bR = sizeof(vio_mono_init_result), bM = (size_t)n, bP = sizeof(float) * 3 * (size_t)n,
                  bErr = sizeof(float) * (size_t)n;
     const size_t total = 2 * al(bB) + al(bS) + al(bE) + al(bC) + al(bR) + al(bM) + al(bP) + al(bErr);
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     char* d = static_cast<char*>(ctx_buffer(ctx, kSlotMonoInit, total));
     if (!d) {
         set_error(ctx, "vio_mono_init_solve: device allocation failed");

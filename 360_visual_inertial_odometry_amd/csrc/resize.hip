@@ -123,7 +123,7 @@ extern "C" int erp_resize_area_device(vio_ctx* ctx, const uint8_t* src, int W, i
     a.fx = W / dW;
     a.fy = H / dH;
     a.scale = 1.f / (float)(a.fx * a.fy);
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     for (hipEvent_t& ev : ctx->rsz_ev)
         if (!ev) VIO_HIP(ctx, hipEventCreate(&ev));
     VIO_HIP(ctx, hipEventRecord(ctx->rsz_ev[0], ctx->stream));
@@ -158,7 +158,7 @@ extern "C" int erp_resize_area(vio_ctx* ctx, const uint8_t* src, int W, int H, i
         set_error(ctx, "erp_resize_area: device allocation failed");
         return VIO_ENOMEM;
     }
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     VIO_HIP(ctx, hipMemcpy2DAsync(d_src, sp, src, stride, W, H, hipMemcpyHostToDevice, ctx->stream));
     if ((rc = erp_resize_area_device(ctx, d_src, W, H, sp, 1, d_dst, dW, dH, dp))) return rc;
     VIO_HIP(ctx, hipMemcpy2DAsync(dst, dst_stride, d_dst, dp, dW, dH, hipMemcpyDeviceToHost, ctx->stream));

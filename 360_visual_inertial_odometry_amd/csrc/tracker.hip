@@ -21,6 +21,8 @@
 // -ffp-contract=off, so results are bitwise those of the oracle.
 #include <float.h>
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <hipcub/hipcub.hpp>
 
 #include "tracker_types.h"
@@ -1913,13 +1915,22 @@ size_t gftt_sort_tmp_bytes(unsigned int cap) {
                                                 (unsigned long long*)nullptr, (int)cap, 0, 64, (hipStream_t)0);
     return tb;
 }
+// the dynamic-LDS limit only grows (per device, under a lock): trackers of different sizes on one
+// device, on one or several host threads, never lower the limit another one launches with
 hipError_t gftt_select_set_lds(size_t bytes) {
+    static std::mutex mu;
+    static size_t cur[64] = {};
+    std::lock_guard<std::mutex> lock(mu);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (bytes <= cur[dev]) return hipSuccess;
     const void* fns[4] = {(const void*)gftt_select_kernel<false, false>, (const void*)gftt_select_kernel<false, true>,
                           (const void*)gftt_select_kernel<true, false>, (const void*)gftt_select_kernel<true, true>};
     for (const void* f : fns) {
         const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         if (e != hipSuccess) return e;
     }
+    cur[dev] = bytes;
     return hipSuccess;
 }
 

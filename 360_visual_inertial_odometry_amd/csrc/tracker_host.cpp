@@ -365,7 +365,7 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
 
 int upload_frame(erp_tracker* t, int slot, const uint8_t* img, int stride) {
     if (!img || stride < t->W) { set_error(t->ctx, "bad frame"); return VIO_EINVAL; }
-    VIO_HIP(t->ctx, hipSetDevice(t->ctx->device));
+    VIO_DEVICE(t->ctx);
     VIO_HIP(t->ctx, hipMemcpy2DAsync(t->lvl[slot][0], t->lp[0], img, stride, t->W, t->H, hipMemcpyHostToDevice,
                                      t->ctx->stream));
     return VIO_OK;
@@ -432,7 +432,7 @@ int erp_tracker_create(vio_ctx* ctx, int W, int H, int max_points, int max_corne
     if (!ctx || !out || W < 8 || H < 8 || W > 65535 || H > 65535 || max_points < 0 || max_corners < 0)
         return VIO_EINVAL;
     *out = nullptr;
-    (void)hipSetDevice(ctx->device);
+    DeviceScope _vio_dev_scope(ctx->device);
     erp_tracker* t = new erp_tracker();
     t->ctx = ctx; t->W = W; t->H = H; t->max_points = max_points; t->max_corners = max_corners;
     int rc = tracker_alloc(t);
@@ -443,7 +443,7 @@ int erp_tracker_create(vio_ctx* ctx, int W, int H, int max_points, int max_corne
 
 void erp_tracker_destroy(erp_tracker* t) {
     if (!t) return;
-    (void)hipSetDevice(t->ctx->device);
+    DeviceScope _vio_dev_scope(t->ctx->device);
     (void)hipStreamSynchronize(t->ctx->stream);
     tracker_free(t);
     delete t;
@@ -458,7 +458,7 @@ int erp_tracker_upload_resized(erp_tracker* t, int slot, const uint8_t* img, int
     if (!t || slot < 0 || slot > 1 || !img || W <= 0 || H <= 0 || stride < W) return VIO_EINVAL;
     if (W == t->W && H == t->H) return upload_frame(t, slot, img, stride);
     vio_ctx* ctx = t->ctx;
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     const int sp = (W + 15) & ~15;  // 16-byte rows: the resize fast path
     uint8_t* d_src = static_cast<uint8_t*>(ctx_buffer(ctx, kSlotResizeSrc, (size_t)sp * H));
     if (!d_src) {
@@ -501,7 +501,7 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         set_error(t->ctx, "bad erp_tracker_params");
         return VIO_EINVAL;
     }
-    VIO_HIP(t->ctx, hipSetDevice(t->ctx->device));
+    VIO_DEVICE(t->ctx);
     if ((rc = ensure_iters(t, std::max(p->ransac_iters, 1)))) return rc;
     if ((rc = ensure_gftt(t, p->min_dist))) return rc;
     hipStream_t st = t->ctx->stream;

@@ -150,7 +150,7 @@ extern "C" int vio_triangulate_device(vio_ctx* ctx, const float* T_cw, int n_pos
         return VIO_EINVAL;
     if (n == 0) return VIO_OK;
     TriArgs a{T_cw, n_poses, pose_pair, bearings, n, (float)width, points, valid, pixel_err};
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     for (hipEvent_t& ev : ctx->tri_ev)
         if (!ev) VIO_HIP(ctx, hipEventCreate(&ev));
     VIO_HIP(ctx, hipEventRecord(ctx->tri_ev[0], ctx->stream));
@@ -188,7 +188,7 @@ extern "C" int vio_triangulate(vio_ctx* ctx, const float* T_cw, int n_poses, con
     float* dE = reinterpret_cast<float*>(d_out + al(bX));
     uint8_t* dV = reinterpret_cast<uint8_t*>(d_out + al(bX) + al(bE));
     hipStream_t st = ctx->stream;
-    VIO_HIP(ctx, hipSetDevice(ctx->device));
+    VIO_DEVICE(ctx);
     VIO_HIP(ctx, hipMemcpyAsync(dT, T_cw, bT, hipMemcpyHostToDevice, st));
     VIO_HIP(ctx, hipMemcpyAsync(dP, pose_pair, bP, hipMemcpyHostToDevice, st));
     VIO_HIP(ctx, hipMemcpyAsync(dB, bearings, bB, hipMemcpyHostToDevice, st));

@@ -177,7 +177,9 @@ int vio_window_add_keyframe(vio_window* win, const vio_window_frame* fr, vio_win
     if (fr->track_begin && n > 0) {
         f.tbeg.assign(fr->track_begin, fr->track_begin + n + 1);
         const int nt = f.tbeg[n] - f.tbeg[0];
-        if (nt < 0 || !fr->track_frame || !fr->track_feat) return VIO_EINVAL;
+        if (nt < 0 || f.tbeg[0] < 0 || !fr->track_frame || !fr->track_feat) return VIO_EINVAL;
+        for (int i = 0; i < n; ++i)  // CSR offsets: monotonic, so every feature's range lies in [0, nt)
+            if (f.tbeg[i] > f.tbeg[i + 1]) return VIO_EINVAL;
         for (int i = 0; i <= n; ++i) f.tbeg[i] -= fr->track_begin[0];
         f.tframe.assign(fr->track_frame + fr->track_begin[0], fr->track_frame + fr->track_begin[0] + nt);
         f.tfeat.assign(fr->track_feat + fr->track_begin[0], fr->track_feat + fr->track_begin[0] + nt);

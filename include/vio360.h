@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VIO360_ABI_VERSION 2
+#define VIO360_ABI_VERSION 3
 
 /* ----------------------------------------------------------------------------------------- */
 /* error codes                                                                                */
@@ -240,9 +240,10 @@ int vio_ba_batch_record_bytes(vio_ba_batch* b, size_t* bytes);
 /* the batch's n records back to back into dst (on_device != 0: a device buffer of this context's
    device, written asynchronously on the context stream by a pack kernel; else host memory, blocking) */
 int vio_ba_batch_pack(vio_ba_batch* b, void* dst, int on_device);
-/* decode one record (host memory) into caller-owned outputs (NULL fields skipped; obs_chi2 and
-   trace are not carried: left untouched) */
-int vio_ba_record_unpack(const void* record, vio_ba_output* out);
+/* decode one record (host memory, record_bytes readable bytes) into caller-owned outputs (NULL fields
+   skipped; obs_chi2 and trace are not carried: left untouched).  Records arrive from other ranks:
+   VIO_EINVAL when the header is malformed or its K/L/N layout does not fit in record_bytes. */
+int vio_ba_record_unpack(const void* record, size_t record_bytes, vio_ba_output* out);
 
 /*
  * Problem assembly and write-back of the Optimizer entry points (SURVEY §8 a3 host half / a4) on a

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol(vio):
 
 
 def test_abi_version(vio):
-    assert vio.lib().vio_abi_version() == 2
+    assert vio.lib().vio_abi_version() == 3
 
 
 STRUCTS = {
@@ -119,3 +119,43 @@ def test_frontend_params_layout(vio, tmp_path):
     cls = vio.abi.ErpFrontendParams
     assert out[0] == C.sizeof(cls)
     assert out[1:] == [getattr(cls, f).offset for f in fields]
+
+
+def _record(K=3, L=5, N=7):
+    import numpy as np
+    import records
+    rng = np.random.default_rng(4)
+    T = np.tile(np.eye(4), (K, 1, 1))
+    T[:, :3, 3] = rng.normal(size=(K, 3))
+    r = {"success": 1, "termination": 0, "iterations": 4, "num_successful_steps": 3, "num_unsuccessful_steps": 1,
+         "num_inliers": N - 1, "num_outliers": 1, "num_bad_lm": 0, "initial_cost": 2.0, "final_cost": 1.0,
+         "fixed_cost": 0.0, "T_wb": T, "lm_xyz": rng.normal(size=(L, 3)), "vel": rng.normal(size=(K, 3)),
+         "bg": rng.normal(size=3), "ba": rng.normal(size=3), "obs_outlier": (np.arange(N) == 2).astype(np.uint8),
+         "lm_bad": np.zeros(L, np.uint8)}
+    return r, records.pack(r, K, L, N)
+
+
+def test_record_unpack_round_trip_and_rejects_malformed(vio):
+    """vio_ba_record_unpack (host decoder of the all-gathered records) takes the record's length and
+    rejects a header whose K/L/N layout overruns it, a short record and a bad version (records come
+    from other ranks)."""
+    import numpy as np
+    r, rec = _record()
+    out = vio.unpack_record(rec)
+    assert np.array_equal(out["lm_xyz"], r["lm_xyz"]) and out["iterations"] == 4
+    assert np.array_equal(out["obs_outlier"], r["obs_outlier"])
+    lib = vio.lib()
+    o = vio.BaOutput(3, 5, 7)
+    buf = np.ascontiguousarray(rec)
+    p = buf.ctypes.data
+    assert lib.vio_ba_record_unpack(p, buf.size, C.byref(o.c)) == 0
+    assert lib.vio_ba_record_unpack(p, buf.size - 1, C.byref(o.c)) == -22  # layout overruns the length
+    assert lib.vio_ba_record_unpack(p, 15, C.byref(o.c)) == -22            # shorter than the header
+    bad = buf.copy()
+    bad[:4] = np.array([1 << 24], np.int32).view(np.uint8)                 # corrupt K
+    assert lib.vio_ba_record_unpack(bad.ctypes.data, bad.size, C.byref(o.c)) == -22
+    bad = buf.copy()
+    bad[12:16] = np.array([99], np.int32).view(np.uint8)                   # unknown version
+    assert lib.vio_ba_record_unpack(bad.ctypes.data, bad.size, C.byref(o.c)) == -22
+    with pytest.raises(vio.VioError):
+        vio.unpack_record(rec[:-16])

@@ -226,3 +226,28 @@ def test_map_view_feeds_gather_and_write_back(vio):
     assert np.array_equal(W.mappoint(good[0])["pos"], [3.0, 3.0, 3.0])
     assert W.mappoint(good[1])["bad"]
     assert W.map_view().frame_Twb[3] == 7.0
+
+
+def test_add_keyframe_rejects_malformed_track_offsets(vio):
+    """vio_window_add_keyframe checks the caller's CSR feature-track offsets (track_begin monotonic)
+    before any later triangulation walks them."""
+    import ctypes as C
+    abi = vio.abi
+    n = 3
+    keep = [np.eye(4, dtype=np.float32).reshape(16), np.eye(4, dtype=np.float32).reshape(16),
+            np.arange(n, dtype=np.int32), np.tile(np.array([0, 0, 1], np.float32), n), np.ones(n, np.uint8),
+            np.full(n, -1, np.int32), np.zeros(2 * n, np.float32),
+            np.array([0, 2, 1, 3], np.int32), np.zeros(3, np.int32), np.zeros(3, np.int32)]
+    f = abi.VioWindowFrame()
+    f.frame_id, f.num_features, f.width = 5, n, 960
+    f.T_wb, f.T_bc = abi._ptr(keep[0], C.c_float), abi._ptr(keep[1], C.c_float)
+    f.feature_id, f.bearing = abi._ptr(keep[2], C.c_int32), abi._ptr(keep[3], C.c_float)
+    f.valid, f.mappoint, f.uv = abi._ptr(keep[4], C.c_uint8), abi._ptr(keep[5], C.c_int32), abi._ptr(keep[6], C.c_float)
+    f.track_begin, f.track_frame, f.track_feat = (abi._ptr(keep[7], C.c_int32), abi._ptr(keep[8], C.c_int32),
+                                                  abi._ptr(keep[9], C.c_int32))
+    w = vio.Window(10)
+    st = abi.VioWindowKfStats()
+    assert vio.lib().vio_window_add_keyframe(w.h, C.byref(f), C.byref(st)) == -22  # 2 > 1: not monotonic
+    keep[7][:] = [0, 1, 2, 3]
+    assert vio.lib().vio_window_add_keyframe(w.h, C.byref(f), C.byref(st)) == 0
+    w.close()
