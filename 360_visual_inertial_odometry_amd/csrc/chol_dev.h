@@ -151,4 +151,193 @@ __device__ __forceinline__ int chol_wave_solve(double* A, int lda, const double*
     return bad;
 }
 
+// Blocked right-looking LLT with 6x6 blocks (one block per pose) of up to two independent SPD systems
+// by all NT threads of the workgroup, the two systems sharing the barriers: system s is the n_s x n_s
+// matrix (n_s a multiple of 6) at A_s in LDS (row stride lda, lower part read), its right-hand side
+// stored as row n_s (columns < n_s), which the factorisation turns into y = L^-1 b (the forward
+// substitution rides along as an extra row).  Per block column j:
+//   (b) one thread per row below the diagonal block forms the panel L[i][6j+c] = (A[i][6j+c] -
+//       sum_m L[i][6j+m] L[6j+c][6j+m]) / L[6j+c][6j+c] (L_jj and 1/L[c][c] held in registers);
+//   (c) the trailing update A[i][k] -= L[i][6j+m] L[k][6j+m] (m ascending) as (row, 6-column strip)
+//       tasks; with a one-step look-ahead: lanes 0-5 of wave s first update the next diagonal block of
+//       system s (lane u = its row u) and factor it in registers (pivots and column entries by
+//       v_readlane, 1/L[c][c] into inv_s), while the other waves take the remaining tasks.
+// Each L[i][k] is the textbook (A[i][k] - sum_{m<k} L[i][m] L[k][m]) / L[k][k] with the sum in
+// ascending m.  Then the block backward substitution x_j = L_jj^-T (y_j - sum_{i>j} L_ij^T x_i) leaves
+// x in x_s.  The critical chain is n/6 six-pivot factors and panels; the O(n^3) work is spread over
+// the other waves.  Returns false (uniformly) when a pivot is not positive.  flag: one LDS int.
+// 6x6 diagonal factor by lanes 0..5 of one wave: d = row `lane` of the block (lower part), in place
+__device__ __forceinline__ int chol6_diag(double (&d)[6], int lane, double& my_inv) {
+    int bad = 0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        const double piv = readlane_d(d[c], c);
+        bad |= !(piv > 0.0);
+        const double r = rsq_nr(piv);
+        const double v = lane == c ? piv * r : d[c] * r;
+        d[c] = v;
+        if (lane == c) my_inv = r;
+#pragma unroll
+        for (int k = c + 1; k < 6; ++k) d[k] -= v * readlane_d(v, k);
+    }
+    return bad;
+}
+template <int NT>
+__device__ bool chol6_solve2(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1, double* inv0,
+                             double* inv1, int* flag) {
+    const int t = (int)threadIdx.x, wid = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
+    const int nb0 = n0 / 6, nb1 = n1 / 6, nb = nb0 > nb1 ? nb0 : nb1;
+    // waves not factoring a diagonal block take the trailing-update tasks
+    const int wfirst = nb1 > 0 ? 2 : 1, nworker = NT - 64 * wfirst, tw = t - 64 * wfirst;
+    if (t == 0) *flag = 0;
+    // diagonal block 0 of each system
+    if (wid < 2 && lane < 6 && (wid == 0 ? nb0 : nb1) > 0) {
+        double* A = wid == 0 ? A0 : A1;
+        double* inv = wid == 0 ? inv0 : inv1;
+        double d[6];
+        const double* row = A + lane * lda;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) d[m] = m <= lane ? row[m] : 0.0;
+        double my_inv = 0.0;
+        const int bad = chol6_diag(d, lane, my_inv);
+        double* w = A + lane * lda;
+#pragma unroll
+        for (int m = 0; m < 6; ++m)
+            if (m <= lane) w[m] = d[m];
+        inv[lane] = my_inv;
+        if (bad) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    if (*flag) return false;
+    for (int j = 0; j < nb; ++j) {
+        const int c0 = 6 * j, r0 = c0 + 6;
+        const int np0 = j < nb0 ? n0 + 1 - r0 : 0, np1 = j < nb1 ? n1 + 1 - r0 : 0;
+        // (b) panel rows (the right-hand-side row included)
+        for (int e = t; e < np0 + np1; e += NT) {
+            const bool s1 = e >= np0;
+            double* A = s1 ? A1 : A0;
+            const double* inv = s1 ? inv1 : inv0;
+            const int i = r0 + (s1 ? e - np0 : e);
+            double l[21], iv[6];  // L_jj (lower, row-major packed) and 1 / diagonal, loaded together
+#pragma unroll
+            for (int c = 0, q = 0; c < 6; ++c)
+#pragma unroll
+                for (int m = 0; m <= c; ++m, ++q) l[q] = A[(c0 + c) * lda + c0 + m];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) iv[c] = inv[c0 + c];
+            double* row = A + i * lda + c0;
+            double a[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) a[c] = row[c];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                double v = a[c];
+#pragma unroll
+                for (int m = 0; m < c; ++m) v -= a[m] * l[c * (c + 1) / 2 + m];
+                a[c] = v * iv[c];
+            }
+#pragma unroll
+            for (int c = 0; c < 6; ++c) row[c] = a[c];
+        }
+        __syncthreads();
+        // (c) trailing update: tasks (row u, strip q) over a rows x strips grid per system
+        const int R0 = np0, R1 = np1;  // rows incl. the rhs row
+        if (wid < wfirst) {
+            // look-ahead: this wave's system's next diagonal block, updated and factored by lanes 0..5
+            const bool s1 = wid == 1;
+            const int R = s1 ? R1 : R0;
+            if (lane < 6 && R >= 7) {  // a next diagonal block exists (6 matrix rows + the rhs row)
+                double* A = s1 ? A1 : A0;
+                double* inv = s1 ? inv1 : inv0;
+                const double* li = A + (r0 + lane) * lda + c0;
+                double l[6], d[6];
+#pragma unroll
+                for (int m = 0; m < 6; ++m) l[m] = li[m];
+#pragma unroll
+                for (int kk = 0; kk < 6; ++kk) {
+                    const double* lk = A + (r0 + kk) * lda + c0;
+                    double a = kk <= lane ? A[(r0 + lane) * lda + r0 + kk] : 0.0;
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) a -= l[m] * lk[m];
+                    d[kk] = kk <= lane ? a : 0.0;
+                }
+                double my_inv = 0.0;
+                const int bad = chol6_diag(d, lane, my_inv);
+                double* w = A + (r0 + lane) * lda + r0;
+#pragma unroll
+                for (int m = 0; m < 6; ++m)
+                    if (m <= lane) w[m] = d[m];
+                inv[r0 + lane] = my_inv;
+                if (bad) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else {
+            const int S0 = R0 > 1 ? (R0 - 2) / 6 + 1 : 0, S1 = R1 > 1 ? (R1 - 2) / 6 + 1 : 0;
+            const int T0 = R0 * S0, T1 = R1 * S1;
+            for (int e = tw; e < T0 + T1; e += nworker) {
+                const bool s1 = e >= T0;
+                const int ee = s1 ? e - T0 : e, S = s1 ? S1 : S0, R = s1 ? R1 : R0;
+                const int u = ee / S, q = ee - u * S;
+                const int kmax = u <= R - 2 ? u : R - 2;  // last column index (local) of row u
+                if (6 * q > kmax) continue;
+                if (q == 0 && u < 6 && (s1 ? wfirst > 1 : true)) continue;  // the next diagonal block: look-ahead
+                double* A = s1 ? A1 : A0;
+                const int i = r0 + u;
+                const double* li = A + i * lda + c0;
+                double l[6];
+#pragma unroll
+                for (int m = 0; m < 6; ++m) l[m] = li[m];
+#pragma unroll
+                for (int kk = 0; kk < 6; ++kk) {
+                    const int k = 6 * q + kk;
+                    if (k > kmax) break;
+                    const double* lk = A + (r0 + k) * lda + c0;
+                    double a = A[i * lda + r0 + k];
+#pragma unroll
+                    for (int m = 0; m < 6; ++m) a -= l[m] * lk[m];
+                    A[i * lda + r0 + k] = a;
+                }
+            }
+        }
+        __syncthreads();
+        if (*flag) return false;
+    }
+    // backward substitution, block by block from the last: y (row n_s) in place, x_s out
+    for (int j = nb - 1; j >= 0; --j) {
+        const int c0 = 6 * j;
+        if (t < 2 && j < (t == 0 ? nb0 : nb1)) {  // x_j = L_jj^-T y_j: one thread per system
+            double* A = t == 0 ? A0 : A1;
+            const double* inv = t == 0 ? inv0 : inv1;
+            double* x = t == 0 ? x0 : x1;
+            const double* y = A + (t == 0 ? n0 : n1) * lda;
+            double xv[6];
+#pragma unroll
+            for (int c = 5; c >= 0; --c) {
+                double v = y[c0 + c];
+#pragma unroll
+                for (int m = c + 1; m < 6; ++m) v -= A[(c0 + m) * lda + c0 + c] * xv[m];
+                xv[c] = v * inv[c0 + c];
+            }
+#pragma unroll
+            for (int c = 0; c < 6; ++c) x[c0 + c] = xv[c];
+        }
+        __syncthreads();
+        if (j == 0) break;
+        // y_k -= sum_m L[6j+m][k] x[6j+m] for k < 6j, both systems
+        const int m0 = j < nb0 ? c0 : 0, m1 = j < nb1 ? c0 : 0;
+        for (int e = t; e < m0 + m1; e += NT) {
+            const bool s1 = e >= m0;
+            double* A = s1 ? A1 : A0;
+            const double* x = s1 ? x1 : x0;
+            const int k = s1 ? e - m0 : e;
+            double* y = A + (s1 ? n1 : n0) * lda;
+            double v = y[k];
+#pragma unroll
+            for (int m = 0; m < 6; ++m) v -= A[(c0 + m) * lda + k] * x[c0 + m];
+            y[k] = v;
+        }
+        __syncthreads();
+    }
+    return true;
+}
+
 }  // namespace vio360

@@ -260,6 +260,115 @@ def cpu_baseline(vio, synth, lm_iters, seconds):
                       f"windows over 1/4/{nthr} threads (~{seconds / 6:.0f} s each)"}
 
 
+def time_batch(batch, reps, warmup=3):
+    """Wall time per run of a resident BaBatch (inputs already in HBM) and the HIP-event kernel time."""
+    for _ in range(warmup):
+        batch.run()
+    batch.sync()
+    batch.kernel_ms()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        batch.run()
+    batch.sync()
+    wall = (time.perf_counter() - t0) / reps
+    kms, _ = batch.kernel_ms()
+    return wall, kms
+
+
+def config2_bench(vio, synth, ctx, lm_iters, cpu_seconds, want_cpu, windows=256):
+    """Config 2 (BASELINE.json configs[1]): visual-only sliding-window BA, 10 KF x 200 landmarks, 2,000
+    ERP observations, RunLocalBA semantics (Optimizer.cpp:726-966; first keyframe constant).  Single
+    window resident (value) and per vio_ba_solve call (host problem in, results out), a batch of
+    `windows` independent windows for throughput, the oracle at 1 / 4 threads on the same window."""
+    probs = [vio.BaProblem(synth.config2(synth.SEED + i), variant=vio.VIO_BA_LOCAL, max_iterations=lm_iters,
+                           fixed_iterations=1) for i in range(windows)]
+    flops = ba_flops_per_iter(probs[0])
+    one = vio.BaBatch(ctx, probs[:1])
+    wall1, kms1 = time_batch(one, 20)
+    res = one.download()[0]
+    one.close()
+    ctx.ba_solve(probs[:1])
+    t0 = time.perf_counter()
+    for _ in range(20):
+        ctx.ba_solve(probs[:1])
+    xfer = (time.perf_counter() - t0) / 20
+    many = vio.BaBatch(ctx, probs)
+    wallm, kmsm = time_batch(many, 10)
+    many.close()
+    out = {
+        "metric": "config 2: visual-only sliding-window BA LM iterations/s (10 KF x 200 landmarks, one window)",
+        "value": lm_iters / wall1,
+        "unit": "LM-iterations/s",
+        "ms_per_solve_resident": wall1 * 1e3,
+        "kernel_ms": kms1,
+        "iters_per_s_with_transfer": lm_iters / xfer,
+        "batched": {"windows": windows, "window_iters_per_s": windows * lm_iters / wallm, "ms_per_step": wallm * 1e3},
+        "iterations": res["iterations"],
+        "roofline": {"bound": "mfma", "achieved": flops * lm_iters / (kms1 * 1e-3) / 1e12, "peak": FP64_PEAK / 1e12,
+                     "unit": "TFLOP/s", "frac": flops * lm_iters / (kms1 * 1e-3) / FP64_PEAK, "traffic": None,
+                     "flops_per_iteration": flops,
+                     "note": "one window: latency-bound (phase-route launch chain); SURVEY §8d flop convention"},
+        "cpu_baseline": None,
+    }
+    if want_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        L = oracle_lib.load()
+        by_t = {}
+        for T in (1, 4):
+            L.oracle_set_threads(T)
+            n, t0 = 0, time.perf_counter()
+            while n < 3 or time.perf_counter() - t0 < cpu_seconds / 4:
+                oracle_lib.ba_solve(vio, probs[n % len(probs)])
+                n += 1
+            by_t[str(T)] = n * lm_iters / (time.perf_counter() - t0)
+        L.oracle_set_threads(1)
+        out["cpu_baseline"] = {"value": by_t["4"], "unit": "LM-iterations/s", "cores": 4, "kind": "port",
+                               **cpu_host_info(), "by_threads": by_t,
+                               "sample": f"config-2 windows x {lm_iters} LM iterations through oracle/ba_oracle.c at "
+                                         f"1 / 4 threads inside the solve (~{cpu_seconds / 4:.0f} s each; Ceres "
+                                         f"num_threads = 4, Optimizer.cpp:79)"}
+        out["vs_cpu_4t"] = out["value"] / by_t["4"]
+    return out
+
+
+def shard_bench(vio, synth, ctx, lm_iters, windows=32):
+    """The per-rank shard of config 4 at 8 GPUs (256 windows / 8 = 32 windows) timed on
+    this GPU: the step time that bounds the 8-GPU strong-scaling run (its all-gather is ~30 us)."""
+    probs = [vio.BaProblem(synth.config3(synth.SEED + w), variant=vio.VIO_BA_VI, max_iterations=lm_iters,
+                           fixed_iterations=1) for w in range(windows)]
+    b = vio.BaBatch(ctx, probs)
+    wall, kms = time_batch(b, 20)
+    b.close()
+    return {"windows": windows, "ms_per_step": wall * 1e3, "kernel_ms": kms,
+            "window_iters_per_s": windows * lm_iters / wall}
+
+
+def global_cpu_baseline(vio, synth, w, threads=4):
+    """Config 5 on the CPU: the oracle runs ONE LM iteration of the full problem (1000 KF x 50k
+    landmarks; dense 5994^2 reduced system) at `threads` threads (Ceres num_threads = 4); the value is
+    that iteration's wall time (oracle_iter_seconds: ComputeTrustRegionStep through the step's
+    acceptance), without the solve's set-up and IterationZero.  The reduced-system LLT is single-
+    threaded, as Eigen's SimplicialLDLT under SPARSE_SCHUR is (schur_complement_solver.cc:319-356)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    L = oracle_lib.load()
+    L.oracle_iter_seconds.argtypes = [C.c_void_p, C.c_int]
+    p = vio.BaProblem(w, variant=vio.VIO_BA_FULL, max_iterations=1, fixed_iterations=1)
+    L.oracle_set_threads(threads)
+    t0 = time.perf_counter()
+    oracle_lib.ba_solve(vio, p)
+    total = time.perf_counter() - t0
+    L.oracle_set_threads(1)
+    sec = (C.c_double * 4)()
+    n = L.oracle_iter_seconds(sec, 4)
+    it = sec[0] if n >= 1 else total
+    return {"value": 1.0 / it, "unit": "LM-iterations/s", "cores": threads, "kind": "port", **cpu_host_info(),
+            "seconds_per_iteration": it, "solve_seconds": total,
+            "sample": f"one LM iteration of config 5 through oracle/ba_oracle.c at {threads} threads "
+                      f"(whole 1-iteration solve incl. set-up: {total:.1f} s)"}
+
+
 def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
     """Config 1: two-frame ERP KLT pair at 3840x1920, 300 corners.  One step = the
     device pipeline erp_tracker_run on frames resident in HBM: pyramids of both frames, LK of the
@@ -353,7 +462,19 @@ def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
     return out
 
 
-def global_ba_bench(vio, synth, ctx, lm_iters):
+def gba_traffic():
+    """PMC HBM bytes of one config-5 LM iteration from the committed summary (tools/gpu_pmc_gba.sh ->
+    profiles/r*_pmc_traffic_gba.json): every kernel's bytes per launch x launches per iteration."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_gba.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_iteration")
+
+
+def global_ba_bench(vio, synth, ctx, lm_iters, want_cpu=False):
     """Config 5: global BA, 1000 KF x 50k landmarks, 500k observations, dense 5994^2 reduced camera
     system (RunBA semantics, fix first).  Timed: one solve of exactly lm_iters LM iterations with
     inputs uploaded once; value = LM iterations per second of that solve."""
@@ -390,8 +511,9 @@ def global_ba_bench(vio, synth, ctx, lm_iters):
                 "incl. host assembly, allocation, upload and the final chi2 pass; fixed iterations",
         "final_cost_ratio": r["final_cost"] / r["initial_cost"],
         "roofline": {"bound": "mfma", "achieved": flops / per_iter / 1e12, "peak": FP64_PEAK / 1e12,
-                     "unit": "TFLOP/s", "frac": flops / per_iter / FP64_PEAK, "traffic": None,
+                     "unit": "TFLOP/s", "frac": flops / per_iter / FP64_PEAK, "traffic": gba_traffic(),
                      "flops_per_iteration": flops},
+        "cpu_baseline": global_cpu_baseline(vio, synth, w) if want_cpu else None,
     }
 
 
@@ -558,6 +680,7 @@ def main():
     ap.add_argument("--no-tri", action="store_true")
     ap.add_argument("--no-resize", action="store_true")
     ap.add_argument("--no-config4", action="store_true")
+    ap.add_argument("--no-config2", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -630,7 +753,11 @@ def main():
             ctx.ba_solve(probs[:1])
         single_xfer_wall = (time.perf_counter() - t1) / n1
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(vio, synth, args.lm_iters, args.cpu_seconds)
-        gba = None if args.no_global else global_ba_bench(vio, synth, ctx, args.lm_iters)
+        gba = None if args.no_global else global_ba_bench(vio, synth, ctx, args.lm_iters,
+                                                           not args.no_cpu_baseline and world == 1)
+        c2 = None if args.no_config2 else config2_bench(vio, synth, ctx, args.lm_iters, args.cpu_seconds,
+                                                        not args.no_cpu_baseline and world == 1)
+        shard = shard_bench(vio, synth, ctx, args.lm_iters)
         klt = None if args.no_klt else klt_bench(vio, synth, ctx, args.klt_steps, 3, args.cpu_seconds,
                                                  not args.no_cpu_baseline and world == 1)
         imu = None if args.no_imu else imu_bench(vio, ctx, 20, min(args.cpu_seconds, 3.0),
@@ -665,8 +792,8 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK,
                 "traffic": ba_traffic(args),
-                "kernel": "phase-route step graph (ph_setup, ph_lin, 11 x [ph_prep, ph_schur, ph_solve, "
-                          "ph_back, ph_ctrl], ph_post)",
+                "kernel": "phase-route step graph (ph_setup, ph_lin, 10 x [ph_prep, ph_schur, ph_solve, "
+                          "ph_back], ph_prep, ph_post)",
                 "kernel_avg_ms": kms,
                 "kernel_launches": kcount,
                 "flops_per_launch": flops_iter * args.lm_iters,
@@ -689,6 +816,11 @@ def main():
             },
             "cpu_baseline": cpu,
             "config4_strong": c4,
+            "config4_shard32": dict(shard, projected_8gpu_speedup=(elapsed / args.steps * 1e3) / shard["ms_per_step"]
+                                    if args.windows == 256 else None,
+                                    note="the 8-GPU strong-scaling shard (256 / 8 windows) on this GPU; projection = "
+                                         "this run's 256-window step / the 32-window step (the all-gather is ~30 us)"),
+            "config2": c2,
             "erp_klt": klt,
             "global_ba": gba,
             "imu_preint": imu,

@@ -30,6 +30,7 @@
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
+#include <time.h>
 #endif
 
 #include "../include/vio360.h"
@@ -1105,6 +1106,22 @@ void oracle_lm_diagonal(int n, const double* colsq, const double* s, double radi
 }
 
 /* x in/out: on return holds the solution Ceres would copy back to the user */
+/* wall time of each LM iteration of the calling thread's last minimisation (ComputeTrustRegionStep
+   through the step's acceptance / re-linearisation): the CPU baseline of a single iteration without the
+   set-up and IterationZero of the solve (bench.py, config 5) */
+static __thread double g_iter_sec[64];
+static __thread int g_iter_n;
+static double now_sec(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+int oracle_iter_seconds(double* out, int cap) {
+    const int n = g_iter_n < cap ? g_iter_n : cap;
+    for (int i = 0; i < n; ++i) out[i] = g_iter_sec[i];
+    return g_iter_n;
+}
+
 int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_user, lm_summary* sum) {
     const int n = P->n;
     memset(sum, 0, sizeof *sum);
@@ -1149,7 +1166,10 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
     double final_cost = sum->initial_cost;
     double model_change = 0, cand_cost = 0;
 
+    g_iter_n = 0;
+    double t_iter = -1.0;
     for (;;) {
+        if (t_iter >= 0.0 && g_iter_n < 64) g_iter_sec[g_iter_n++] = now_sec() - t_iter;
         /* FinalizeIterationAndCheckIfMinimizerCanContinue */
         if (step_successful) {
             sum->successful++;
@@ -1168,6 +1188,7 @@ int oracle_lm_minimize(const lm_problem* P, const lm_options* opt, double* x_use
         if (!fixed && rad.radius <= opt->min_radius) { sum->termination = VIO_TERM_CONVERGENCE; break; }
 
         iteration++;
+        t_iter = now_sec();
         memset(&it, 0, sizeof it);
         it.iteration = iteration;
         /* ComputeTrustRegionStep */

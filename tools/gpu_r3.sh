@@ -11,4 +11,5 @@ rc2=$?; echo "ba_quick rc=$rc2"; grep -E "windows=|parity|cfg|pnp|local" gpurun_
 if [ $rc2 -ne 0 ]; then exit $rc2; fi
 for W in 1 32 256; do timeout -k 10 120 python -u tools/ph_solve_stamps.py $W > gpurun_out/stamps_${tag}_$W.log 2>&1 || exit $?; done
 grep -E "chol|solve|prep|schur" gpurun_out/stamps_${tag}_1.log
+bash tools/gpu_prof_ba.sh $tag || exit $?
 exit $rc

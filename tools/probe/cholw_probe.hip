@@ -244,7 +244,15 @@ __global__ void __launch_bounds__(256, 1) probe(const double* gA, const double* 
         for (int e = threadIdx.x; e < 64 * LD; e += 256) S[e] = gA[e];
         if (threadIdx.x < 64) bb[threadIdx.x] = gb[threadIdx.x];
         __syncthreads();
-        if (threadIdx.x < 64) {
+        if (V == 7) {  // all threads: 6x6-blocked LLT (rhs as row n)
+            __shared__ int flag;
+            for (int f = threadIdx.x; f < n; f += 256) S[n * LD + f] = bb[f];
+            __syncthreads();
+            const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+            chol6_solve2<256>(S, n, S, 0, LD, bb, bb, Lscr, Lscr + 64, &flag);
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+            tot += t1 - t0;
+        } else if (threadIdx.x < 64) {
             const unsigned long long t0 = __builtin_amdgcn_s_memtime();
             if (V < 4) chol_var<64, V>(S, LD, bb, n, bb, col, lane);
             else if (V < 6) chol_pad<64, V>(S, LD, bb, n, bb, col, lane);
@@ -281,8 +289,8 @@ int main() {
     hipMalloc(&dc, 8);
     hipMemcpy(dA, A, sizeof(A), hipMemcpyHostToDevice);
     hipMemcpy(db, b, sizeof(b), hipMemcpyHostToDevice);
-    void (*fns[7])(const double*, const double*, int, int, double*, unsigned long long*) = {probe<0>, probe<1>, probe<2>, probe<3>, probe<4>, probe<5>, probe<6>};
-    for (int v = 0; v < 7; ++v) {
+    void (*fns[8])(const double*, const double*, int, int, double*, unsigned long long*) = {probe<0>, probe<1>, probe<2>, probe<3>, probe<4>, probe<5>, probe<6>, probe<7>};
+    for (int v = 0; v < 8; ++v) {
         hipLaunchKernelGGL(fns[v], dim3(1), dim3(256), 0, 0, dA, db, n, reps, dx, dc);
         unsigned long long cyc;
         double x[64];
