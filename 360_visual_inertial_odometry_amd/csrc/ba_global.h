@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "vio360.h"
+
 namespace vio360 {
 
 struct GbaArgs {
@@ -61,6 +63,26 @@ struct GbaArgs {
     hipStream_t side;         // look-ahead stream of the Cholesky (nullptr: plain schedule)
     hipEvent_t ev[2];
     int* flags;               // [32 (3 nfp/64 + 1)] triangular-solve flags, one per 128 B (+ timeout word), Cholesky step flags
+    // RunVIBA beyond one window (Optimizer.cpp:493-724): the velocities and the shared biases follow the
+    // pose blocks in the reduced system (f = np + imu index, the oracle's order); the IMU factors'
+    // pose Jacobians are zero in the reference (Factors.cpp:1326-1485), so the reduced system is
+    // blockdiag(pose Schur complement, IMU normal equations) and the landmarks never couple to it
+    int is_vi;
+    int np, ni;               // 6P pose rows, nf - np IMU rows
+    double gravity[3];
+    const vio_preint* preint;       // [K]
+    const uint8_t* preint_valid;    // [K]
+    const int* vel_f;         // [K] f-offset of velocity k or -1
+    int bg_f, ba_f;           // f-offsets of the biases (-1: no IMU factor)
+    double* sqi;              // [K][81] sqrt-information of each factor
+    double* x_vel;            // [K][3]
+    double* c_vel;
+    double* x_bias;           // [6] bg, ba
+    double* c_bias;
+    double* imuJ;             // [K][108] Jacobian 9x12 [vi | bg | ba | vj] at the linearisation point
+    double* imur;             // [K][9] residual there
+    double* imu_cost;         // [K] per-factor cost (scratch of the fixed-order sum)
+    double* Himu;             // [ni][ni] J^T J of the IMU factors (imu-space)
 };
 
 // the word a timed-out inter-workgroup wait of the Cholesky / triangular solves sets (cleared at the start
@@ -78,6 +100,18 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s);
 hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s);
 hipError_t gba_launch_backsub(const GbaArgs& A, double* partial, double* out_nonfinite, hipStream_t s);
 hipError_t gba_launch_model(const GbaArgs& A, double* partial, double* out3, hipStream_t s);
+// VIBA terms (ba_kernel.hip, next to the window solver's IMU factor code)
+hipError_t gba_imu_launch_setup(const GbaArgs& A, hipStream_t s);
+// IMU cost at (A.pc, xv, xb) into out[0]; with want_jac the Jacobians / residuals into imuJ / imur
+hipError_t gba_imu_launch_eval(const GbaArgs& A, const double* xv, const double* xb, int want_jac, double* out,
+                               hipStream_t s);
+// IMU normal equations, f-space gradient / column norms (/ Jacobi scale when first) and out[0] = the
+// gradient max-norm over the IMU parameters
+hipError_t gba_imu_launch_linearise(const GbaArgs& A, int first, double* out_gmax, hipStream_t s);
+// rows [np, nf) of the reduced system: sHs + D^2 on the IMU block, zero against the poses
+hipError_t gba_imu_launch_system(const GbaArgs& A, hipStream_t s);
+// IMU model change, velocity / bias candidates and their step / parameter norms into out3[0..2]
+hipError_t gba_imu_launch_model(const GbaArgs& A, double* out3, hipStream_t s);
 hipError_t gba_launch_post(const GbaArgs& A, double* chi2, uint8_t* outl, uint8_t* bad, double* partial, double* out3,
                            hipStream_t s);
 

@@ -57,8 +57,10 @@ struct DevBufs {
 
 }  // namespace
 
+// LocalBA / FullBA beyond 16 keyframes, VIBA beyond 10 (the windowed path's reduced-system bound)
 bool global_ba_applicable(const vio_ba_problem& p) {
-    return (p.variant == VIO_BA_LOCAL || p.variant == VIO_BA_FULL) && p.num_kf > BA_KMAX;
+    return ((p.variant == VIO_BA_LOCAL || p.variant == VIO_BA_FULL) && p.num_kf > BA_KMAX) ||
+           (p.variant == VIO_BA_VI && p.num_kf > VI_KMAX);
 }
 
 int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
@@ -68,6 +70,8 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
         set_error(ctx, "invalid global BA problem");
         return VIO_EINVAL;
     }
+    const bool vi = p.variant == VIO_BA_VI;
+    if (vi && (!p.preint || !p.preint_valid || !p.vel)) { set_error(ctx, "VIBA needs preint/preint_valid/vel"); return VIO_EINVAL; }
     for (int o = 0; o < N; ++o)
         if (p.obs_kf[o] < 0 || p.obs_kf[o] >= K || p.obs_lm[o] < 0 || p.obs_lm[o] >= L) {
             set_error(ctx, "observation index out of range");
@@ -91,11 +95,30 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
         if (lv) lm_used[l] = 1;
         active[o] = kv || lv;
     }
-    std::vector<int> pose_f(K, -1), pose_of_block;
+    // VIBA: an IMU factor k (preint_valid[k]) brings velocities k-1, k, the biases and its two poses in
+    // (RunVIBA: velocities and biases are never constant; Optimizer.cpp:493-636)
+    std::vector<uint8_t> vel_used(K, 0);
+    bool bias_used = false;
+    if (vi)
+        for (int k = 1; k < K; ++k) {
+            if (!p.preint_valid[k]) continue;
+            vel_used[k - 1] = vel_used[k] = 1;
+            bias_used = true;
+            if (!p.kf_const[k - 1]) pose_used[k - 1] = 1;
+            if (!p.kf_const[k]) pose_used[k] = 1;
+        }
+    std::vector<int> pose_f(K, -1), pose_of_block, vel_f(K, -1);
     for (int k = 0; k < K; ++k)
         if (pose_used[k]) { pose_f[k] = 6 * (int)pose_of_block.size(); pose_of_block.push_back(k); }
     const int P = (int)pose_of_block.size();
-    const int nf = 6 * P;
+    int nf = 6 * P;
+    for (int k = 0; k < K; ++k)
+        if (vel_used[k]) { vel_f[k] = nf; nf += 3; }
+    const int bg_f = bias_used ? nf : -1;
+    if (bias_used) nf += 3;
+    const int ba_f = bias_used ? nf : -1;
+    if (bias_used) nf += 3;
+    const int np = 6 * P, ni = nf - np;
     const int nfp = std::max(64, (nf + 63) / 64 * 64);
     int n_free = nf;
     for (int l = 0; l < L; ++l) n_free += 3 * lm_used[l];
@@ -171,6 +194,8 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     GbaArgs A;
     std::memset(&A, 0, sizeof A);
     A.K = K; A.L = L; A.N = N; A.P = P; A.nf = nf; A.nfp = nfp;
+    A.is_vi = vi; A.np = np; A.ni = ni; A.bg_f = bg_f; A.ba_f = ba_f;
+    if (vi) for (int i = 0; i < 3; ++i) A.gravity[i] = p.gravity[i];
     A.cols = p.cols; A.rows = p.rows; A.huber = p.huber_delta; A.chi2_thr = p.chi2_threshold;
     for (int i = 0; i < 4; ++i) A.info[i] = p.info[i];
     A.Lw[0] = 1; A.Lw[1] = 0; A.Lw[2] = 0; A.Lw[3] = 1;
@@ -212,7 +237,21 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     int* dfail;
     uint8_t *d_outl, *d_bad;
     double* d_chi2;
-    if ((rc = B.alloc(&partial, 3 * nblk_max + 3 * (size_t)K)) || (rc = B.alloc(&scal, 16)) ||
+    if (vi) {
+        const vio_preint* c_pre; const uint8_t* c_pv; const int* c_vf;
+        std::vector<vio_preint> pre(p.preint, p.preint + K);
+        std::vector<uint8_t> pv(p.preint_valid, p.preint_valid + K);
+        std::vector<double> v0(p.vel, p.vel + 3 * (size_t)K), b0(6);
+        for (int i = 0; i < 3; ++i) { b0[i] = p.bg[i]; b0[3 + i] = p.ba[i]; }
+        if ((rc = B.upload((vio_preint**)&c_pre, pre)) || (rc = B.upload((uint8_t**)&c_pv, pv)) ||
+            (rc = B.upload((int**)&c_vf, vel_f)) || (rc = B.upload(&A.x_vel, v0)) || (rc = B.upload(&A.x_bias, b0)) ||
+            (rc = B.alloc(&A.c_vel, 3 * (size_t)K)) || (rc = B.alloc(&A.c_bias, 6)) || (rc = B.alloc(&A.sqi, 81 * (size_t)K)) ||
+            (rc = B.alloc(&A.imuJ, 108 * (size_t)K)) || (rc = B.alloc(&A.imur, 9 * (size_t)K)) ||
+            (rc = B.alloc(&A.imu_cost, (size_t)K)) || (rc = B.alloc(&A.Himu, (size_t)ni * ni + ni)))
+            return rc;
+        A.preint = c_pre; A.preint_valid = c_pv; A.vel_f = c_vf;
+    }
+    if ((rc = B.alloc(&partial, 3 * nblk_max + 3 * (size_t)K)) || (rc = B.alloc(&scal, 32)) ||
         (rc = B.alloc(&dfail, 4)) || (rc = B.alloc(&A.flags, 32 * (3 * ((size_t)nfp / 64) + 1))) || (rc = B.alloc(&d_outl, Ns)) || (rc = B.alloc(&d_bad, Ls)) ||
         (rc = B.alloc(&d_chi2, Ns)))
         return rc;
@@ -263,14 +302,25 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));
     GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0.data(), sizeof(double) * 3 * L, hipMemcpyHostToDevice, st));
     GBA_CHECK(gba_launch_setup(A, st));
-
+    if (vi) GBA_CHECK(gba_imu_launch_setup(A, st));
+    // scal slots of the VIBA terms: [11] IMU cost at x, [12] IMU gradient max-norm, [13..15] IMU model change /
+    // step norm^2 / candidate norm^2, [16] IMU cost at the candidate (all 0 without IMU factors)
+    GBA_CHECK(hipMemsetAsync(scal, 0, sizeof(double) * 32, st));
+    // cost + Jacobians at the current point, then the normal-equation terms (visual and IMU)
+    auto linearise = [&](int first) -> hipError_t {
+        hipError_t e = gba_launch_eval(A, A.x_pose, A.x_lm, 1, partial, scal + 0, st);
+        if (e == hipSuccess && vi) e = gba_imu_launch_eval(A, A.x_vel, A.x_bias, 1, scal + 11, st);
+        if (e == hipSuccess) e = gba_launch_linearise(A, first, partial, scal + 1, st);
+        if (e == hipSuccess && vi) e = gba_imu_launch_linearise(A, first, scal + 12, st);
+        return e;
+    };
     auto read = [&](double* h, int off, int n) -> int {
         GBA_CHECK(hipMemcpyAsync(h, scal + off, sizeof(double) * n, hipMemcpyDeviceToHost, st));
         GBA_CHECK(hipStreamSynchronize(st));
         return VIO_OK;
     };
     // ---- fixed cost (program.cc:305-390) ----
-    double h[16];
+    double h[32];
     GBA_CHECK(gba_launch_eval(A, A.x_pose, A.x_lm, 2, partial, scal + 0, st));
     if ((rc = read(h, 0, 1))) return rc;
     const double fixed_cost = h[0];
@@ -295,10 +345,9 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     } else {
         double radius = 1e4, decrease = 2.0, x_norm = -1.0, min_cost = DBL_MAX;
         int consecutive_invalid = 0;
-        GBA_CHECK(gba_launch_eval(A, A.x_pose, A.x_lm, 1, partial, scal + 0, st));
-        GBA_CHECK(gba_launch_linearise(A, 1, partial, scal + 1, st));
-        if ((rc = read(h, 0, 2))) return rc;
-        double x_cost = h[0], gmax = h[1];
+        GBA_CHECK(linearise(1));
+        if ((rc = read(h, 0, 17))) return rc;
+        double x_cost = h[0] + h[11], gmax = std::max(h[1], h[12]);
         initial_cost = x_cost + fixed_cost;
         double step_eval_current = x_cost, iter_cost = x_cost + fixed_cost;
         final_cost = initial_cost;
@@ -327,14 +376,21 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             // ComputeTrustRegionStep + candidate cost, one batch of kernels, one readback
             GBA_CHECK(hipMemsetAsync(dfail, 0, sizeof(int), st));
             GBA_CHECK(gba_launch_step_prep(A, radius, partial, scal + 2, st));
+            if (vi) GBA_CHECK(gba_imu_launch_system(A, st));
             GBA_CHECK(factor_and_solve());
             GBA_CHECK(gba_launch_backsub(A, partial, scal + 3, st));
             GBA_CHECK(gba_launch_model(A, partial, scal + 4, st));
+            if (vi) GBA_CHECK(gba_imu_launch_model(A, scal + 13, st));
             GBA_CHECK(gba_launch_eval(A, A.c_pose, A.c_lm, 0, partial, scal + 7, st));
+            if (vi) GBA_CHECK(gba_imu_launch_eval(A, A.c_vel, A.c_bias, 0, scal + 16, st));
             int hfail = 0, htmo = 0;
             GBA_CHECK(hipMemcpyAsync(&hfail, dfail, sizeof(int), hipMemcpyDeviceToHost, st));
             if (int* tw = gba_timeout_word(A)) GBA_CHECK(hipMemcpyAsync(&htmo, tw, sizeof(int), hipMemcpyDeviceToHost, st));
-            if ((rc = read(h, 0, 8))) return rc;
+            if ((rc = read(h, 0, 17))) return rc;
+            h[4] += h[13];  // model change, |x - cand|^2, |cand|^2, candidate cost: visual + IMU terms
+            h[5] += h[14];
+            h[6] += h[15];
+            h[7] += h[16];
             if (htmo) {  // an inter-workgroup wait timed out: report the fault instead of an invalid LM step
                 set_error(ctx, "global BA: a Cholesky / triangular-solve hand-off timed out on the device");
                 return VIO_EDEVICE;
@@ -366,12 +422,15 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             if (rel > 1e-3) {
                 GBA_CHECK(hipMemcpyAsync(A.x_pose, A.c_pose, sizeof(double) * 6 * K, hipMemcpyDeviceToDevice, st));
                 GBA_CHECK(hipMemcpyAsync(A.x_lm, A.c_lm, sizeof(double) * 3 * L, hipMemcpyDeviceToDevice, st));
+                if (vi) {
+                    GBA_CHECK(hipMemcpyAsync(A.x_vel, A.c_vel, sizeof(double) * 3 * K, hipMemcpyDeviceToDevice, st));
+                    GBA_CHECK(hipMemcpyAsync(A.x_bias, A.c_bias, sizeof(double) * 6, hipMemcpyDeviceToDevice, st));
+                }
                 x_norm = std::sqrt(h[6]);
-                GBA_CHECK(gba_launch_eval(A, A.x_pose, A.x_lm, 1, partial, scal + 0, st));
-                GBA_CHECK(gba_launch_linearise(A, 0, partial, scal + 1, st));
-                if ((rc = read(h, 0, 2))) return rc;
-                x_cost = h[0];
-                gmax = h[1];
+                GBA_CHECK(linearise(0));
+                if ((rc = read(h, 0, 17))) return rc;
+                x_cost = h[0] + h[11];
+                gmax = std::max(h[1], h[12]);
                 step_ok = true;
                 radius = std::min(1e16, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3)));
                 decrease = 2.0;
@@ -390,6 +449,12 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
         if (termination == VIO_TERM_FAILURE) {  // Ceres leaves the user's parameters untouched
             GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));
             GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0.data(), sizeof(double) * 3 * L, hipMemcpyHostToDevice, st));
+            if (vi) {
+                std::vector<double> b0(6);
+                for (int i = 0; i < 3; ++i) { b0[i] = p.bg[i]; b0[3 + i] = p.ba[i]; }
+                GBA_CHECK(hipMemcpy(A.x_vel, p.vel, sizeof(double) * 3 * K, hipMemcpyHostToDevice));
+                GBA_CHECK(hipMemcpy(A.x_bias, b0.data(), sizeof(double) * 6, hipMemcpyHostToDevice));
+            }
         }
     }
     // ---- chi^2 / outliers / bad landmarks, outputs ----
@@ -413,6 +478,13 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
         if (out->obs_outlier) out->obs_outlier[perm[q]] = outl[q];
     }
     if (out->lm_bad) std::memcpy(out->lm_bad, bad.data(), L);
+    if (vi) {
+        double xb[6];
+        if (out->vel) GBA_CHECK(hipMemcpy(out->vel, A.x_vel, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
+        GBA_CHECK(hipMemcpy(xb, A.x_bias, sizeof xb, hipMemcpyDeviceToHost));
+        if (out->bg) std::memcpy(out->bg, xb, 3 * sizeof(double));
+        if (out->ba) std::memcpy(out->ba, xb + 3, 3 * sizeof(double));
+    }
     if (out->summary) {
         vio_ba_summary& s = *out->summary;
         std::memset(&s, 0, sizeof s);

@@ -26,7 +26,6 @@
 
 namespace vio360 {
 
-constexpr int VI_KMAX = 10;  // VIBA windows on this path: K <= 10 (ni = 3K+6 <= 36)
 constexpr int NI_MAX = 3 * VI_KMAX + 6;
 // per-window workspace after ba_ws_layout(): IMU sqrt-information, imu-space H and g
 __host__ __device__ constexpr int64_t ba_ws_extra() { return 81 * BA_KMAX + NI_MAX * NI_MAX + NI_MAX + 32; }
@@ -2231,3 +2230,4 @@ hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream) {
 }  // namespace vio360
 
 #include "ba_phases.inc"
+#include "gba_imu.inc"

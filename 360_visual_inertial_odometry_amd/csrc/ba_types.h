@@ -11,6 +11,7 @@ namespace vio360 {
 
 constexpr int BA_THREADS = 256;  // one workgroup (4 waves) per window
 constexpr int BA_KMAX = 16;      // keyframes per window on the single-workgroup path
+constexpr int VI_KMAX = 10;     // VIBA windows on the windowed path: K <= 10 (ni = 3K+6 <= 36); larger: global path
 constexpr int BA_NF_MAX = 96;    // reduced (Schur) system size bound: 6*15 poses or 54+30+6 (VIBA K=10)
 constexpr int BA_STAGE = 3392;   // doubles of LDS for the Schur k-panels (chunk depth derived per tile count)
 constexpr int BA_GCOL = 256;     // max k rows per Schur chunk

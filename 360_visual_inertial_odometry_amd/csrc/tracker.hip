@@ -391,13 +391,12 @@ __device__ void pixel_to_bearing(float u, float v, int W, int H, float* b) {
 // sooner than sixteen while GFTT pass 1 occupies the chip from the side stream):
 //   mode 0: all n points (erp_rot_ransac); mode 1: status ∧ !polar ∧ !boundary (pipeline)
 constexpr int RP_THREADS = 256;
-__global__ void __launch_bounds__(RP_THREADS) ransac_prep_kernel(RansacArgs R) {
-    __shared__ int wsum[RP_THREADS / 64];
-    __shared__ int base;
+template <int NT>
+__device__ int ransac_prep_body(const RansacArgs& R, int* wsum, int& base) {
     if (threadIdx.x == 0) base = 0;
     __syncthreads();
     const int n = R.n;
-    for (int c0 = 0; c0 < n; c0 += RP_THREADS) {
+    for (int c0 = 0; c0 < n; c0 += NT) {
         int i = c0 + threadIdx.x;
         int good = 0;
         if (i < n) {
@@ -428,12 +427,18 @@ __global__ void __launch_bounds__(RP_THREADS) ransac_prep_kernel(RansacArgs R) {
         __syncthreads();
         if (threadIdx.x == 0) {
             int t = 0;
-            for (int k = 0; k < RP_THREADS / 64; ++k) t += wsum[k];
+            for (int k = 0; k < NT / 64; ++k) t += wsum[k];
             base += t;
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) *R.n_good = base;
+    return base;
+}
+__global__ void __launch_bounds__(RP_THREADS) ransac_prep_kernel(RansacArgs R) {
+    __shared__ int wsum[RP_THREADS / 64];
+    __shared__ int base;
+    ransac_prep_body<RP_THREADS>(R, wsum, base);
 }
 
 // mt19937 + libstdc++-11 uniform_int_distribution (Lemire) — the reference's sampler
@@ -542,12 +547,16 @@ __global__ void __launch_bounds__(RS_THREADS) ransac_raw_kernel(uint32_t seed, u
     }
 }
 
+// PREP: the input compaction (ransac_prep_body) first, in the same workgroup (one launch fewer on the
+// tracker's critical path); the sampler then reads the count from LDS
+template <bool PREP>
 __global__ void __launch_bounds__(RS_THREADS) ransac_sample_kernel(RansacArgs R) {
     __shared__ uint32_t acc[RS_RAW];    // accepted draws (compacted), in stream order
     __shared__ uint8_t len3[RS_RAW];    // 1: a hypothesis starting at draw p consumes exactly 3 draws
     __shared__ int wsum[RS_THREADS / 64];
-    __shared__ int s_m, s_fallback;
-    const int n = *R.n_good;
+    __shared__ int s_m, s_fallback, s_base;
+    const int n = PREP ? ransac_prep_body<RS_THREADS>(R, wsum, s_base) : *R.n_good;
+    if (PREP) __syncthreads();  // wsum is reused below
     if (n < 3 || R.iters <= 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (tid == 0) {
@@ -1819,8 +1828,8 @@ hipError_t launch_ransac_raw(uint32_t seed, uint32_t* raw, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st) {
-    hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(RP_THREADS), 0, st, r);
-    if (gen_samples) hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(RS_THREADS), 0, st, r);
+    if (gen_samples) hipLaunchKernelGGL(ransac_sample_kernel<true>, dim3(1), dim3(RS_THREADS), 0, st, r);
+    else hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(RP_THREADS), 0, st, r);
     if (r.iters > 0) hipLaunchKernelGGL(ransac_hyp_kernel, dim3((r.iters + 3) / 4), dim3(256), 0, st, r);
     hipLaunchKernelGGL(ransac_select_kernel, dim3(1), dim3(256), 0, st, r);
     return hipGetLastError();
@@ -1861,10 +1870,48 @@ static hipError_t launch_select(const GfArgs& g, const unsigned long long* keys,
     }
     return hipGetLastError();
 }
-// descending radix sort of the top-K buffer (topk_cap keys; unused slots hold 0 and sort to the end)
-static hipError_t gftt_sort_topk(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {
-    size_t tb = sort_tmp_bytes;
-    return hipcub::DeviceRadixSort::SortKeysDescending(sort_tmp, tb, g.topk, g.topk_sorted, (int)g.topk_cap, 0, 64, st);
+// Descending sort of the top-K buffer (n = min(n_top, topk_cap) keys) by rank: the keys are unique
+// (response bits << 32 | pixel address), so key i belongs at position #{keys > key i} -- the order
+// a descending radix sort of the buffer gives.  64 keys per workgroup (one per lane); each of the 8
+// waves counts over one eighth of the list, its comparand reads wave-uniform (scalar loads, 8 keys
+// per batch), the partial counts are summed in LDS and the key is written to its position.  The
+// post-cut buffer holds ~16 x max_corners keys: O(n^2 / 512) compares per lane-slot, no passes over
+// digits and no temporary storage.
+constexpr int TS_WAVES = 8;
+__global__ void __launch_bounds__(64 * TS_WAVES) gftt_topk_sort_kernel(GfArgs G) {
+    __shared__ unsigned int part[TS_WAVES][64];
+    const unsigned int n = min(*G.n_top, G.topk_cap);
+    const unsigned int i0 = blockIdx.x * 64;
+    if (i0 >= n) return;
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const unsigned int i = i0 + lane;
+    const unsigned long long k = i < n ? G.topk[i] : ~0ull;
+    const unsigned int per = ((n + TS_WAVES - 1) / TS_WAVES + 7) & ~7u;
+    const unsigned int j0 = min(n, wid * per), j1 = min(n, j0 + per);
+    const unsigned long long* src = G.topk;
+    unsigned int cnt = 0;
+    const unsigned long long* q = src + j0;
+    const unsigned long long* q1 = src + j1;
+    for (; q + 8 <= q1; q += 8) {
+        unsigned long long c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = q[u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cnt += c[u] > k;
+    }
+    for (; q < q1; ++q) cnt += *q > k;
+    part[wid][lane] = cnt;
+    __syncthreads();
+    if (wid == 0 && i < n) {
+        unsigned int r = 0;
+#pragma unroll
+        for (int q = 0; q < TS_WAVES; ++q) r += part[q][lane];
+        G.topk_sorted[r] = k;
+    }
+}
+static hipError_t gftt_sort_topk(const GfArgs& g, void*, size_t, hipStream_t st) {
+    hipLaunchKernelGGL(gftt_topk_sort_kernel, dim3((g.topk_cap + 63) / 64), dim3(64 * TS_WAVES), 0, st, g);
+    return hipGetLastError();
 }
 // fast path: candidates -> histogram -> top-K compaction -> sort of the top-K keys -> greedy
 hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st) {

@@ -185,6 +185,24 @@ def assert_parity_vi_converged(vio, w, o, g, **kw):
     assert g["success"] == o["success"] == 1
 
 
+def assert_parity_survey_bar(o, g):
+    """SURVEY §8c's bar, asserted directly (no perturbation cloud): converged config 3 at the
+    reference's options (RunVIBA, Optimizer.cpp:493-724; Ceres tolerances trust_region_minimizer.cc:
+    740-760): positions <= 1e-4 m, rotations <= 1e-5 rad, landmarks <= 1e-3 m, velocities / biases
+    <= 1e-4, final cost rel 1e-6, iterations +-1."""
+    dt = np.abs(o["T_wb"][:, :3, 3] - g["T_wb"][:, :3, 3]).max()
+    dr = max(rot_angle(o["T_wb"][k, :3, :3], g["T_wb"][k, :3, :3]) for k in range(len(o["T_wb"])))
+    dl = np.abs(o["lm_xyz"] - g["lm_xyz"]).max()
+    print(f"config-3 converged parity: dt {dt:.3e} m  angle {dr:.3e} rad  landmarks {dl:.3e} m  "
+          f"iterations gpu {g['iterations']} oracle {o['iterations']}")
+    assert g["success"] == o["success"] == 1
+    assert dt <= 1e-4 and dr <= 1e-5 and dl <= 1e-3, (dt, dr, dl)
+    for key in ("vel", "bg", "ba"):
+        assert np.abs(o[key] - g[key]).max() <= 1e-4, key
+    assert abs(o["final_cost"] - g["final_cost"]) <= 1e-6 * o["final_cost"]
+    assert abs(o["iterations"] - g["iterations"]) <= 1, (o["iterations"], g["iterations"])
+
+
 @pytest.mark.parametrize("idx", range(8))
 def test_ba_parity_reference_options(vio, gpu_ctx, all_cases, idx):
     """Reference solver options (50 iterations, Ceres tolerances), every Optimizer variant."""
@@ -192,7 +210,9 @@ def test_ba_parity_reference_options(vio, gpu_ctx, all_cases, idx):
     p = vio.BaProblem(w, variant=var)
     o = oracle_lib.ba_solve(vio, p)
     g = gpu_ctx.ba_solve([p])[0]
-    if var == vio.VIO_BA_VI:
+    if name == "cfg3-vi":
+        assert_parity_survey_bar(o, g)
+    elif var == vio.VIO_BA_VI:
         assert_parity_vi_converged(vio, w, o, g)
     else:
         assert_parity(o, g, p.c.chi2_threshold)
@@ -297,8 +317,10 @@ def test_edge_cases(vio, synth, gpu_ctx):
     bad["obs_lm"] = bad["obs_lm"].copy(); bad["obs_lm"][0] = 999
     with pytest.raises(vio.VioError):
         gpu_ctx.ba_solve([vio.BaProblem(bad)])
+    # (5) VI windows beyond 10 keyframes: the resident-batch API (windowed path only) refuses them;
+    # vio_ba_solve routes them to the global path (test_global_vi_parity)
     with pytest.raises(vio.VioError):
-        gpu_ctx.ba_solve([vio.BaProblem(synth.make_window(K=12, L=10, seed=1, imu=True), variant=vio.VIO_BA_VI)])
+        vio.BaBatch(gpu_ctx, [vio.BaProblem(synth.make_window(K=12, L=10, seed=1, imu=True), variant=vio.VIO_BA_VI)])
 
 
 def test_config4_full_size_properties(vio, synth, gpu_ctx):
@@ -331,16 +353,51 @@ def test_config4_full_size_properties(vio, synth, gpu_ctx):
         e1 = np.abs(g["T_wb"][:, :3, 3] - w["T_wb_true"][:, :3, 3]).mean()
         ratio_g.append(e1 / e0)
         ratio_o.append(r["pose_err_final"] / r["pose_err_init"])
+    print(f"config 4 at reference options: windows outside the final-cost band {[o[0] for o in off_cost]}, "
+          f"outside the iteration band {[o[0] for o in off_it]}")
     assert len(off_cost) <= 2 and len(off_it) <= 2, (off_cost, off_it)
     ratio_g, ratio_o = np.array(ratio_g), np.array(ratio_o)
     assert abs(ratio_g.mean() - ratio_o.mean()) <= 0.01 and ratio_g.mean() < 0.2
     # converged answers of sampled windows at the VI parity bar (oracle perturbation cloud)
     for i in (0, 255):
         assert_parity_vi_converged(vio, ws[i], oracle_lib.ba_solve(vio, probs[i]), res[i])
-    fixed = [vio.BaProblem(ws[i], variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1) for i in (0, 97, 255)]
+    # fixed iterations (the timed configuration): every one of the 256 windows at the tight bar, none
+    # allowed outside it (oracle solves over a host thread pool; the ctypes call releases the GIL)
+    from concurrent.futures import ThreadPoolExecutor
+    fixed = [vio.BaProblem(w, variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1) for w in ws]
     fres = gpu_ctx.ba_solve(fixed)
-    for p, g in zip(fixed, fres):
-        assert_parity(oracle_lib.ba_solve(vio, p), g, p.c.chi2_threshold, iters_tol=0)
+    with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        fora = list(ex.map(lambda p: oracle_lib.ba_solve(vio, p), fixed))
+    off = []
+    for i, (p, g, o) in enumerate(zip(fixed, fres, fora)):
+        try:
+            assert_parity(o, g, p.c.chi2_threshold, iters_tol=0)
+        except AssertionError as e:
+            off.append((i, str(e)[:200]))
+    assert not off, off
+
+
+@pytest.mark.parametrize("K,L", [(16, 200), (40, 300)])
+def test_global_vi_parity(vio, synth, gpu_ctx, K, L):
+    """RunVIBA beyond the windowed path's 10 keyframes (Optimizer.cpp:493-724: any frames.size() >= 2)
+    on the global path (velocities and biases after the poses in the dense reduced system): 10 fixed LM
+    iterations at the tight bar with the iteration count and step outcomes exact, velocities / biases
+    to 1e-6; the converged solve at the reference's options at the VI bar."""
+    w = synth.make_window(K=K, L=L, seed=40 + K, imu=True, all_visible=False)
+    p = vio.BaProblem(w, variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1)
+    o = oracle_lib.ba_solve(vio, p)
+    g = gpu_ctx.ba_solve([p])[0]
+    assert o["iterations"] == g["iterations"] == 11
+    assert (o["num_successful_steps"], o["num_unsuccessful_steps"]) == \
+        (g["num_successful_steps"], g["num_unsuccessful_steps"])
+    assert_parity(o, g, p.c.chi2_threshold, iters_tol=0)
+    for key in ("vel", "bg", "ba"):
+        assert np.abs(o[key] - g[key]).max() <= 1e-6, key
+    p2 = vio.BaProblem(w, variant=vio.VIO_BA_VI)
+    o2 = oracle_lib.ba_solve(vio, p2)
+    g2 = gpu_ctx.ba_solve([p2])[0]
+    assert g2["final_cost"] < g2["initial_cost"]
+    assert_parity_vi_converged(vio, w, o2, g2)
 
 
 @pytest.mark.parametrize("variant", ["full", "local"])
