@@ -336,12 +336,13 @@ __device__ __noinline__ void imu_eval_wave(const vio_preint& p, const double* sq
         r_out = s;
     }
     if (lane >= 12) return;
+    // column `col` of J written row by row (the rows of the sqrt-information read as they are used: the
+    // function stays within the 128 registers of its callers' 4-waves-per-SIMD bound, no scratch)
     const int col = lane;
-    double Jcol[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) Jcol[i] = 0.0;
     if (col < 3 || col >= 9) {  // vi (col 0..2) / vj (col 9..11): diagonal sqrt-information blocks only
         const int j = col < 3 ? col : col - 9;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) J[12 * i + col] = 0.0;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             double a = 0, b = 0;
@@ -350,12 +351,8 @@ __device__ __noinline__ void imu_eval_wave(const vio_preint& p, const double* sq
                 a += sqi[9 * (3 + i) + 3 + k] * Rbwi[3 * k + j];
                 b += sqi[9 * (6 + i) + 6 + k] * Rbwi[3 * k + j];
             }
-            if (col < 3) {
-                Jcol[3 + i] = -a;
-                Jcol[6 + i] = -b * dt;
-            } else {
-                Jcol[3 + i] = a;
-            }
+            J[12 * (3 + i) + col] = col < 3 ? -a : a;
+            J[12 * (6 + i) + col] = col < 3 ? -b * dt : 0.0;
         }
     } else {  // bg (col 3..5) / ba (col 6..8)
         const int j = col < 6 ? col - 3 : col - 6;
@@ -391,16 +388,14 @@ __device__ __noinline__ void imu_eval_wave(const vio_preint& p, const double* sq
                 Tc[6 + i] = -(double)p.J_Pa[3 * i + j];
             }
         }
-#pragma unroll
+#pragma unroll 1
         for (int i = 0; i < 9; ++i) {
             double s = 0;
 #pragma unroll
             for (int k = 0; k < 9; ++k) s += sqi[9 * i + k] * Tc[k];
-            Jcol[i] = s;
+            J[12 * i + col] = s;
         }
     }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) J[12 * i + col] = Jcol[i];
 }
 
 // InertialFactorFixedGravity ctor (Factors.cpp:1310-1323): sqrt-information = chol((cov + 1e-8 I)^-1)^T,
