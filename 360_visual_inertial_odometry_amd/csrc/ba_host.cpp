@@ -21,7 +21,9 @@ namespace vio360 {
 
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream);
 hipError_t launch_ba_pack(const BaPools& P, int n, uint8_t* dst, int64_t rec_bytes, hipStream_t stream);
-hipError_t launch_ba_phases(const BaPools& P, const BaWin* hw, int n, hipStream_t stream);
+constexpr int kPhLanesMax = 4;  // sub-batches of the phase route, each on its own stream
+hipError_t launch_ba_phases(const BaPools& P, const BaWin* hw, int n, hipStream_t stream, int lanes,
+                            hipStream_t* side, hipEvent_t* ev);
 size_t ba_phase_doubles(int K, int L, int N, int T);  // sized for the smallest group (most partials)
 const char* ba_phases_failed_launch();
 hipError_t ba_phases_prepare(const BaWin* hw, int n);
@@ -240,6 +242,8 @@ struct BaDevice {
     void* prof_buf = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipGraphExec_t phase_graph = nullptr;  // the captured phase-kernel sequence of this batch
+    hipStream_t lane_st[kPhLanesMax - 1] = {};  // side streams of the phase route's sub-batches
+    hipEvent_t lane_ev[kPhLanesMax] = {};       // their fork / join events
     bool reusable = false;                 // vio_ba_batch: replayed many times (graph); one-shot solves launch directly
     double ms_sum = 0.0;
     int ms_count = 0;
@@ -330,6 +334,10 @@ static void free_batch(BaDevice& d) {
     d.ev0 = d.ev1 = nullptr;
     if (d.phase_graph) (void)hipGraphExecDestroy(d.phase_graph);
     d.phase_graph = nullptr;
+    for (hipStream_t& st : d.lane_st)
+        if (st) (void)hipStreamDestroy(st), st = nullptr;
+    for (hipEvent_t& ev : d.lane_ev)
+        if (ev) (void)hipEventDestroy(ev), ev = nullptr;
 }
 
 static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
@@ -421,6 +429,34 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     for (const BaWin& w : d.pk.win) (w.is_pnp ? any_pnp : any_other) = true;
     const bool phases = any_other && !force_monolithic(ctx, d);
     d.P.route = phases ? 1 : 0;
+    // IMU candidate terms beside the back-substitution walk for small batches (a single window's serial
+    // path is then shorter); in ph_solve for larger ones (ph_back keeps 4 waves per SIMD, no scratch)
+    static const int imu_back_max = [] {
+        const char* v = std::getenv("VIO_BA_IMU_BACK_MAX");  // experiment override
+        return v ? std::atoi(v) : 8;
+    }();
+    d.P.imu_in_back = d.n <= imu_back_max ? 1 : 0;
+    d.P.win_base = 0;
+    // sub-batches of the phase route on their own streams (launch_ba_phases): large batches only
+    static const int lanes_env = [] {
+        const char* v = std::getenv("VIO_BA_LANES");  // experiment override
+        return v ? std::max(1, std::min(kPhLanesMax, std::atoi(v))) : 0;
+    }();
+    // (measured at 256 windows: 2 lanes 0.99x, 3 lanes 0.71x, 4 lanes 0.93x of one stream; 32 windows,
+    // 2 lanes 0.88x -- not on by default)
+    int lanes = lanes_env ? lanes_env : 1;
+    for (int l = 0; l < lanes; ++l) {
+        if (l > 0 && !d.lane_st[l - 1] && hipStreamCreateWithFlags(&d.lane_st[l - 1], hipStreamNonBlocking) != hipSuccess) {
+            d.lane_st[l - 1] = nullptr;
+            lanes = l;
+            break;
+        }
+        if (!d.lane_ev[l] && hipEventCreateWithFlags(&d.lane_ev[l], hipEventDisableTiming) != hipSuccess) {
+            d.lane_ev[l] = nullptr;
+            lanes = std::max(1, l);
+            break;
+        }
+    }
     hipError_t e = hipSuccess;
     const char* what = "ba_window_kernel launch";
     if (phases) {
@@ -429,13 +465,13 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
         e = ba_phases_prepare(d.pk.win.data(), d.n);
         if (e != hipSuccess) what = "hipFuncSetAttribute(phase kernels)";
         if (e == hipSuccess && !d.reusable) {
-            e = launch_ba_phases(d.P, d.pk.win.data(), d.n, ctx->stream);
+            e = launch_ba_phases(d.P, d.pk.win.data(), d.n, ctx->stream, lanes, d.lane_st, d.lane_ev);
             if (e != hipSuccess) what = ba_phases_failed_launch();
         } else if (e == hipSuccess && !d.phase_graph) {
             hipGraph_t g = nullptr;
             e = hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal);
             if (e == hipSuccess) {
-                hipError_t el = launch_ba_phases(d.P, d.pk.win.data(), d.n, ctx->stream);
+                hipError_t el = launch_ba_phases(d.P, d.pk.win.data(), d.n, ctx->stream, lanes, d.lane_st, d.lane_ev);
                 e = hipStreamEndCapture(ctx->stream, &g);
                 if (el != hipSuccess) e = el, what = ba_phases_failed_launch();
             }

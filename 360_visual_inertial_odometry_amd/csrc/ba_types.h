@@ -68,6 +68,9 @@ struct BaPools {
     unsigned long long* prof;    // optional [n][VIO_BA_PROF_SLOTS] per-phase shader clocks (diagnostics), may be null
     int route;                   // 0: ba_window_kernel solves every window; 1: it solves the PnP windows
                                  // only and the phase kernels (ba_phases.inc) the others
+    int win_base;                // phase route: first window of a launch (sub-batches on their own streams)
+    int imu_in_back;             // phase route: the IMU candidate terms in an extra workgroup of the
+                                 // back-substitution grid (small batches) instead of at the end of ph_solve
 };
 
 // workspace sub-offsets (in doubles) relative to BaWin::o_ws

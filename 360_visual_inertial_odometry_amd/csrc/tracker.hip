@@ -29,6 +29,13 @@
 
 namespace vio360 {
 
+// LDS writes of this wave visible to its own later reads (no workgroup barrier)
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int reflect101(int p, int n) {
     if (n == 1) return 0;
     while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
@@ -1828,8 +1835,10 @@ hipError_t launch_ransac_raw(uint32_t seed, uint32_t* raw, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st) {
-    if (gen_samples) hipLaunchKernelGGL(ransac_sample_kernel<true>, dim3(1), dim3(RS_THREADS), 0, st, r);
-    else hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(RP_THREADS), 0, st, r);
+    // the compaction stays a 4-wave workgroup of its own (a 16-wave one, the sampler's, waits longer for a
+    // CU while GFTT pass 1 fills the chip from the side stream: measured slower fused)
+    hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(RP_THREADS), 0, st, r);
+    if (gen_samples) hipLaunchKernelGGL(ransac_sample_kernel<false>, dim3(1), dim3(RS_THREADS), 0, st, r);
     if (r.iters > 0) hipLaunchKernelGGL(ransac_hyp_kernel, dim3((r.iters + 3) / 4), dim3(256), 0, st, r);
     hipLaunchKernelGGL(ransac_select_kernel, dim3(1), dim3(256), 0, st, r);
     return hipGetLastError();
@@ -1872,14 +1881,14 @@ static hipError_t launch_select(const GfArgs& g, const unsigned long long* keys,
 }
 // Descending sort of the top-K buffer (n = min(n_top, topk_cap) keys) by rank: the keys are unique
 // (response bits << 32 | pixel address), so key i belongs at position #{keys > key i} -- the order
-// a descending radix sort of the buffer gives.  64 keys per workgroup (one per lane); each of the 8
-// waves counts over one eighth of the list, its comparand reads wave-uniform (scalar loads, 8 keys
-// per batch), the partial counts are summed in LDS and the key is written to its position.  The
-// post-cut buffer holds ~16 x max_corners keys: O(n^2 / 512) compares per lane-slot, no passes over
-// digits and no temporary storage.
-constexpr int TS_WAVES = 8;
+// a descending radix sort of the buffer gives.  64 keys per workgroup (one per lane); each of the 16
+// waves counts over one sixteenth of the list, staged through LDS in 512-key chunks (coalesced 8-key-per-
+// lane loads of the next chunk in flight while the current one is compared; ds_read_b128 broadcasts,
+// two comparands per read); the partial counts are summed in LDS and the key written to its position.
+constexpr int TS_WAVES = 16, TS_CHUNK = 512;
 __global__ void __launch_bounds__(64 * TS_WAVES) gftt_topk_sort_kernel(GfArgs G) {
     __shared__ unsigned int part[TS_WAVES][64];
+    __shared__ __align__(16) unsigned long long buf[TS_WAVES][TS_CHUNK];
     const unsigned int n = min(*G.n_top, G.topk_cap);
     const unsigned int i0 = blockIdx.x * 64;
     if (i0 >= n) return;
@@ -1889,17 +1898,33 @@ __global__ void __launch_bounds__(64 * TS_WAVES) gftt_topk_sort_kernel(GfArgs G)
     const unsigned int per = ((n + TS_WAVES - 1) / TS_WAVES + 7) & ~7u;
     const unsigned int j0 = min(n, wid * per), j1 = min(n, j0 + per);
     const unsigned long long* src = G.topk;
+    unsigned long long* mine = buf[wid];
     unsigned int cnt = 0;
-    const unsigned long long* q = src + j0;
-    const unsigned long long* q1 = src + j1;
-    for (; q + 8 <= q1; q += 8) {
-        unsigned long long c[8];
+    unsigned long long nx[TS_CHUNK / 64];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) c[u] = q[u];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) cnt += c[u] > k;
+    for (int u = 0; u < TS_CHUNK / 64; ++u) {  // key 0 (never > k) pads the last chunk
+        const unsigned int j = j0 + 64 * u + lane;
+        nx[u] = j < j1 ? src[j] : 0ull;
     }
-    for (; q < q1; ++q) cnt += *q > k;
+    for (unsigned int base = j0; base < j1; base += TS_CHUNK) {
+#pragma unroll
+        for (int u = 0; u < TS_CHUNK / 64; ++u) mine[64 * u + lane] = nx[u];
+        wave_lds_fence();
+        if (base + TS_CHUNK < j1) {
+#pragma unroll
+            for (int u = 0; u < TS_CHUNK / 64; ++u) {
+                const unsigned int j = base + TS_CHUNK + 64 * u + lane;
+                nx[u] = j < j1 ? src[j] : 0ull;
+            }
+        }
+        const ulonglong2* c2 = reinterpret_cast<const ulonglong2*>(mine);
+#pragma unroll 8
+        for (int q = 0; q < TS_CHUNK / 2; ++q) {
+            const ulonglong2 c = c2[q];
+            cnt += (c.x > k) + (c.y > k);
+        }
+        wave_lds_fence();  // every lane's reads of the chunk before the next chunk's writes
+    }
     part[wid][lane] = cnt;
     __syncthreads();
     if (wid == 0 && i < n) {

@@ -196,9 +196,13 @@ typedef struct {
     int32_t _pad2;
 } vio_ba_output;
 
+/* Any window size: windows whose reduced system fits one workgroup (LocalBA / FullBA / PnP with
+   K <= 16, VIBA with K <= 10) run on the windowed solver; larger ones (RunBA over hundreds of keyframes,
+   RunVIBA beyond 10 keyframes: Optimizer.cpp:304-486, 493-724) on the multi-kernel global path. */
 int vio_ba_solve(vio_ctx* ctx, const vio_ba_problem* prob, vio_ba_output* out);
 
-/* n independent windows in ONE device launch (one workgroup per window) */
+/* n independent windows in ONE device launch (one workgroup per window); problems beyond the windowed
+   path's bounds are solved one by one on the global path */
 int vio_ba_solve_batched(vio_ctx* ctx, const vio_ba_problem* probs, vio_ba_output* outs, int n);
 
 /*
@@ -206,6 +210,7 @@ int vio_ba_solve_batched(vio_ctx* ctx, const vio_ba_problem* probs, vio_ba_outpu
  * then vio_ba_batch_run() solves all windows from the resident copy with no host transfer.
  */
 typedef struct vio_ba_batch vio_ba_batch;
+/* windowed path only: VIO_ENOSYS for a window beyond its bounds (K > 16, VIBA K > 10) */
 int vio_ba_batch_create(vio_ctx* ctx, const vio_ba_problem* probs, int n, vio_ba_batch** out);
 int vio_ba_batch_run(vio_ba_batch* b);          /* async on the context stream */
 int vio_ba_batch_sync(vio_ba_batch* b);

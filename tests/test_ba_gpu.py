@@ -499,3 +499,41 @@ def test_global_ba_solve_paths_bitwise(vio, tmp_path):
         outs.append(np.load(f))
     a, b = outs
     assert np.array_equal(a["T"], b["T"]) and np.array_equal(a["l"], b["l"]) and np.array_equal(a["c"], b["c"])
+
+
+def test_batches_from_two_threads(vio, synth):
+    """INTEGRATION.md's threading model (one vio_ctx per host thread): two threads, each with its own
+    context on device 0, create and run phase-route batches at the same time — the per-device kernel
+    attribute set-up (dynamic LDS limits, set once under a lock) must be in place before either
+    thread's first launch.  Each thread's results equal the single-threaded solve's, bit for bit."""
+    import threading
+    probs = [vio.BaProblem(synth.config3(synth.SEED + i), variant=vio.VIO_BA_VI, max_iterations=5,
+                           fixed_iterations=1) for i in range(4)]
+    ref_ctx = vio.Context(0)
+    ref = ref_ctx.ba_solve(probs)
+    ref_ctx.close()
+    out, err = {}, []
+
+    def work(tid):
+        try:
+            ctx = vio.Context(0)
+            b = vio.BaBatch(ctx, probs[2 * tid:2 * tid + 2])
+            for _ in range(3):
+                b.run()
+            b.sync()
+            out[tid] = b.download()
+            b.close()
+            ctx.close()
+        except Exception as e:  # noqa: BLE001 - reported below
+            err.append(repr(e))
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+    assert not err, err
+    for tid in range(2):
+        for j, g in enumerate(out[tid]):
+            r = ref[2 * tid + j]
+            assert np.array_equal(g["T_wb"], r["T_wb"]) and np.array_equal(g["lm_xyz"], r["lm_xyz"]), (tid, j)
