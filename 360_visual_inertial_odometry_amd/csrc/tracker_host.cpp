@@ -95,6 +95,15 @@ struct erp_tracker {
     hipEvent_t fork = nullptr, join = nullptr, raw_done = nullptr;
     bool stage_timing = true;  // record the per-stage events (each marker costs the stream a few us)
     bool timed_run = false;    // the last run recorded them
+    // without stage markers the pipeline is captured once into a graph and replayed (the ~20 launches,
+    // event records and memsets of a run are otherwise enqueued one by one by the host, which the GPU
+    // outruns: the first pyramid kernel started ~18 us after the run's start event); re-captured when
+    // the point count, the parameters or the tracker's allocations change
+    hipGraphExec_t run_graph = nullptr;
+    int graph_n = -1;
+    size_t graph_allocs = 0;
+    erp_klt_params graph_klt{};
+    erp_tracker_params graph_prm{};
     bool ran = false;
     std::vector<void*> allocs;
 };
@@ -118,6 +127,8 @@ void tracker_free(erp_tracker* t) {
     t->allocs.clear();
     for (auto& e : t->ev)
         if (e) (void)hipEventDestroy(e);
+    if (t->run_graph) (void)hipGraphExecDestroy(t->run_graph);
+    t->run_graph = nullptr;
     if (t->side) (void)hipStreamDestroy(t->side);
     if (t->fork) (void)hipEventDestroy(t->fork);
     if (t->join) (void)hipEventDestroy(t->join);
@@ -492,21 +503,10 @@ int erp_tracker_set_points(erp_tracker* t, const float* pts, int n) {
     return VIO_OK;
 }
 
-int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p) {
-    if (!t || !p) return VIO_EINVAL;
-    int rc = check_klt(t->ctx, klt);
-    if (rc) return rc;
-    if (p->ransac_iters < 0 || p->max_corners < 0 || p->max_corners > t->max_corners || p->quality <= 0 ||
-        p->min_dist < 0) {
-        set_error(t->ctx, "bad erp_tracker_params");
-        return VIO_EINVAL;
-    }
-    VIO_DEVICE(t->ctx);
-    if ((rc = ensure_iters(t, std::max(p->ransac_iters, 1)))) return rc;
-    if ((rc = ensure_gftt(t, p->min_dist))) return rc;
+// the enqueue sequence of one pipeline run (directly, or into the stream capture of erp_tracker_run)
+static int enqueue_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p, int n, int radius) {
+    int rc;
     hipStream_t st = t->ctx->stream;
-    const int n = t->n_pts;
-    VIO_HIP(t->ctx, hipEventRecord(t->ev[0], st));
     // the eigenvalue map of the current frame does not depend on tracking: side stream
     VIO_HIP(t->ctx, hipEventRecord(t->fork, st));
     VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->fork, 0));
@@ -547,13 +547,6 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
     // CreateFeatureMask: discs of radius (int)min_dist around every kept point (bitmap cleared on the side
     // stream before raw_done, which the main stream waited for before RANSAC)
     if (n <= 0) VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->raw_done, 0));
-    const int radius = (int)p->min_dist;
-    if (radius != t->halfw_r) {
-        std::vector<int> hw = circle_half_widths(radius);
-        if ((rc = dalloc(t, &t->d_halfw, sizeof(int) * (radius + 1)))) return rc;
-        VIO_HIP(t->ctx, hipMemcpy(t->d_halfw, hw.data(), sizeof(int) * (radius + 1), hipMemcpyHostToDevice));
-        t->halfw_r = radius;
-    }
     if (n > 0 && radius > 0) {
         DiscArgs d{t->d_next, t->d_kept, nullptr, nullptr, t->d_disc, t->disc_words, t->W, t->H, radius,
                    t->d_halfw};
@@ -564,6 +557,60 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
     if ((rc = enqueue_gftt(t, t->lvl[1][0], t->lp[0], nullptr, 0, p->max_corners, p->quality, p->min_dist, true,
                            p->boundary_margin, p->polar_ratio, true, true)))
         return rc;
+    return VIO_OK;
+}
+
+
+int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p) {
+    if (!t || !p) return VIO_EINVAL;
+    int rc = check_klt(t->ctx, klt);
+    if (rc) return rc;
+    if (p->ransac_iters < 0 || p->max_corners < 0 || p->max_corners > t->max_corners || p->quality <= 0 ||
+        p->min_dist < 0) {
+        set_error(t->ctx, "bad erp_tracker_params");
+        return VIO_EINVAL;
+    }
+    VIO_DEVICE(t->ctx);
+    if ((rc = ensure_iters(t, std::max(p->ransac_iters, 1)))) return rc;
+    if ((rc = ensure_gftt(t, p->min_dist))) return rc;
+    hipStream_t st = t->ctx->stream;
+    const int n = t->n_pts;
+    // CreateFeatureMask's disc half-widths (a blocking upload: before any capture)
+    const int radius = (int)p->min_dist;
+    if (radius != t->halfw_r) {
+        std::vector<int> hw = circle_half_widths(radius);
+        if ((rc = dalloc(t, &t->d_halfw, sizeof(int) * (radius + 1)))) return rc;
+        VIO_HIP(t->ctx, hipMemcpy(t->d_halfw, hw.data(), sizeof(int) * (radius + 1), hipMemcpyHostToDevice));
+        t->halfw_r = radius;
+    }
+    VIO_HIP(t->ctx, hipEventRecord(t->ev[0], st));
+    const bool use_graph = !t->stage_timing;
+    if (use_graph && t->run_graph && t->graph_n == n && t->graph_allocs == t->allocs.size() &&
+        std::memcmp(&t->graph_klt, klt, sizeof *klt) == 0 && std::memcmp(&t->graph_prm, p, sizeof *p) == 0) {
+        VIO_HIP(t->ctx, hipGraphLaunch(t->run_graph, st));
+    } else {
+        if (t->run_graph) {
+            (void)hipGraphExecDestroy(t->run_graph);
+            t->run_graph = nullptr;
+        }
+        if (use_graph) VIO_HIP(t->ctx, hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        rc = enqueue_run(t, klt, p, n, radius);
+        if (use_graph) {
+            hipGraph_t g = nullptr;
+            hipError_t e = hipStreamEndCapture(st, &g);
+            if (rc == VIO_OK && e == hipSuccess) e = hipGraphInstantiate(&t->run_graph, g, nullptr, nullptr, 0);
+            if (g) (void)hipGraphDestroy(g);
+            if (rc) return rc;
+            if (e != hipSuccess) return hip_fail(t->ctx, e, "tracker graph capture");
+            t->graph_n = n;
+            t->graph_allocs = t->allocs.size();
+            t->graph_klt = *klt;
+            t->graph_prm = *p;
+            VIO_HIP(t->ctx, hipGraphLaunch(t->run_graph, st));
+        } else if (rc) {
+            return rc;
+        }
+    }
     VIO_HIP(t->ctx, hipEventRecord(t->ev[4], st));
     t->ran = true;
     t->timed_run = t->stage_timing;

@@ -9,6 +9,7 @@ for n in 1 3; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
     d=gpurun_out/pmc_gba/n$n/$ctr
     rm -rf $d
+    mkdir -p gpurun_out/pmc_gba/n$n
     timeout -k 10 240 rocprofv3 --pmc $ctr -d $d -o run --output-format csv -- python3 tools/gba_run.py $n > $d.log 2>&1
     rc=$?; echo "n=$n $ctr rc=$rc $(tail -1 $d.log | cut -c1-160)"
     if [ $rc -ne 0 ]; then exit $rc; fi
