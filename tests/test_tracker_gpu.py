@@ -179,6 +179,40 @@ def test_pipeline_full_size_config1(vio, gpu_ctx, synth):
     assert np.array_equal(res["corners"], corners)
 
 
+def test_pipeline_graph_replay_bitwise(vio, gpu_ctx, synth):
+    """Without stage markers erp_tracker_run captures the pipeline into a graph and replays it: the
+    replayed runs give bitwise the directly launched run's outputs, and a changed parameter set or point
+    count is re-captured (config-1 pair at 1920x960)."""
+    a, b, _ = synth.config1(1920, 960)
+    Wf, Hf = 1920, 960
+    pts = oracle_lib.gftt(a, region_mask(Wf, Hf), 200, float(np.float32(0.01)), 30.0)
+    klt = vio.default_klt_params()
+    t = vio.Tracker(gpu_ctx, Wf, Hf, max_points=512, max_corners=512)
+    t.upload(0, a)
+    t.upload(1, b)
+
+    def run(prm, p, markers):
+        t.set_points(p)
+        t.set_stage_timing(markers)
+        t.run(prm, klt)
+        t.sync()
+        r = t.download()
+        return {k: r[k].copy() for k in ("next", "status", "kept", "corners")}
+
+    prm = vio.default_tracker_params(max_corners=200, seed=1)
+    ref = run(prm, pts, True)
+    for _ in range(3):  # capture, then two replays
+        g = run(prm, pts, False)
+        for k in ref:
+            assert np.array_equal(ref[k], g[k]), k
+    prm2 = vio.default_tracker_params(max_corners=150, seed=3)
+    ref2 = run(prm2, pts[:120], True)
+    g2 = run(prm2, pts[:120], False)
+    for k in ref2:
+        assert np.array_equal(ref2[k], g2[k]), k
+    t.close()
+
+
 def test_pipeline_on_device_resized_frames(vio, gpu_ctx, synth):
     """The demo frame path (app/main.cpp:199-204): 3840x1920 camera frames INTER_AREA-resized on the
     device into the tracker's 960x480 slots give bitwise the pipeline on oracle-resized frames."""
