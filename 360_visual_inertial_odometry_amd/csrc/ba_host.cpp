@@ -271,8 +271,8 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     // fills the chip with 2 groups per window and halves ph_solve's partial sums; smaller batches keep
     // more, shorter groups (latency)
     const char* gse = std::getenv("VIO_BA_SCHUR_GS");  // experiment override
-    // (>= PH_GS_MIN = 5, the workspace sizing of ba_phases.inc; 1..4 measured slower at 1 and 32 windows)
-    const int gs = gse ? std::max(5, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : 5;
+    // (>= PH_GS_MIN = 1, the workspace sizing of ba_phases.inc)
+    const int gs = gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : pk.win.size() > 32 ? 5 : 2;
     for (BaWin& w : pk.win) w.gs = gs;
     UP(pk.win, win, const BaWin*);
     UP(pk.pose_raw, pose_raw, const double*);

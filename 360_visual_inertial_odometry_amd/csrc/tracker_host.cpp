@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <random>
@@ -507,14 +508,18 @@ int erp_tracker_set_points(erp_tracker* t, const float* pts, int n) {
 static int enqueue_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p, int n, int radius) {
     int rc;
     hipStream_t st = t->ctx->stream;
-    // the eigenvalue map of the current frame does not depend on tracking: side stream
+    // the host enqueues the main stream's pyramids and LK first (the GPU starts on them at once), then
+    // the side stream's work, which is needed only from RANSAC on: the RANSAC draws' raw stream (seed
+    // only), the GFTT counters / histogram / top-K reset, the disc bitmap clear, then GFTT pass 1 (the
+    // eigenvalue map of the current frame does not depend on tracking) once the pyramids are built
     VIO_HIP(t->ctx, hipEventRecord(t->fork, st));
+    if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK
     VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->fork, 0));
-    {  // the RANSAC draws' raw stream depends on the seed only
+    {
         hipError_t e = launch_ransac_raw(p->ransac_seed, t->d_raw, t->side);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac_raw_kernel");
     }
-    {  // off the main stream's path: the GFTT counters / histogram / top-K reset and the disc bitmap clear
+    {
         GfArgs gr;
         std::memset(&gr, 0, sizeof gr);
         gr.hist = t->d_hist;
@@ -525,7 +530,6 @@ static int enqueue_run(erp_tracker* t, const erp_klt_params* klt, const erp_trac
         VIO_HIP(t->ctx, hipMemsetAsync(t->d_disc, 0, sizeof(uint32_t) * t->disc_words * t->H, t->side));
         VIO_HIP(t->ctx, hipEventRecord(t->raw_done, t->side));  // raw draws, reset and cleared discs: one wait
     }
-    if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK
     {  // GFTT pass 1 shares the chip with the latency-bound LK / RANSAC, not with the pyramids
         VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->ev[1], 0));
         hipError_t e =
@@ -584,7 +588,14 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
         t->halfw_r = radius;
     }
     VIO_HIP(t->ctx, hipEventRecord(t->ev[0], st));
-    const bool use_graph = !t->stage_timing;
+    // graph replay (VIO_TRK_GRAPH=1, without stage markers): measured slower on ROCm 7.2 -- the replayed
+    // graph ran the side stream's GFTT pass 1 after the main stream's kernels instead of beside them
+    // (0.245 -> 0.450 ms per run); the run is enqueued directly by default
+    static const bool graph_env = [] {
+        const char* v = std::getenv("VIO_TRK_GRAPH");
+        return v && v[0] == '1';
+    }();
+    const bool use_graph = graph_env && !t->stage_timing;
     if (use_graph && t->run_graph && t->graph_n == n && t->graph_allocs == t->allocs.size() &&
         std::memcmp(&t->graph_klt, klt, sizeof *klt) == 0 && std::memcmp(&t->graph_prm, p, sizeof *p) == 0) {
         VIO_HIP(t->ctx, hipGraphLaunch(t->run_graph, st));

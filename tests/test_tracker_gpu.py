@@ -180,9 +180,9 @@ def test_pipeline_full_size_config1(vio, gpu_ctx, synth):
 
 
 def test_pipeline_graph_replay_bitwise(vio, gpu_ctx, synth):
-    """Without stage markers erp_tracker_run captures the pipeline into a graph and replays it: the
-    replayed runs give bitwise the directly launched run's outputs, and a changed parameter set or point
-    count is re-captured (config-1 pair at 1920x960)."""
+    """Runs without stage markers (the bench's timed mode; with VIO_TRK_GRAPH=1 captured into a graph
+    and replayed) give bitwise the outputs of a run with them, also after the parameter set and the
+    point count change (config-1 pair at 1920x960)."""
     a, b, _ = synth.config1(1920, 960)
     Wf, Hf = 1920, 960
     pts = oracle_lib.gftt(a, region_mask(Wf, Hf), 200, float(np.float32(0.01)), 30.0)
