@@ -272,7 +272,7 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     // more, shorter groups (latency)
     const char* gse = std::getenv("VIO_BA_SCHUR_GS");  // experiment override
     // (>= PH_GS_MIN = 1, the workspace sizing of ba_phases.inc)
-    const int gs = gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : pk.win.size() > 32 ? 5 : 2;
+    const int gs = gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : 5;
     for (BaWin& w : pk.win) w.gs = gs;
     UP(pk.win, win, const BaWin*);
     UP(pk.pose_raw, pose_raw, const double*);
