@@ -1,10 +1,12 @@
 #!/bin/bash
-# A/B of a BA build variant (tools/probe/libvio360_<v>.so) against the in-tree library: ba_quick timings
+# A/B of libvio360 builds on one box: phase-route batch timing at 1 / 32 / 256 windows per library
 set -u
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-v=$1
-timeout -k 10 200 python3 tools/ba_quick.py > gpurun_out/ba_quick_base.log 2>&1 || exit 1
-echo base; grep -E "windows=" gpurun_out/ba_quick_base.log
-VIO360_LIB=tools/probe/libvio360_$v.so timeout -k 10 200 python3 tools/ba_quick.py > gpurun_out/ba_quick_$v.log 2>&1 || exit 1
-echo $v; grep -E "windows=|cfg3" gpurun_out/ba_quick_$v.log
+export VIO_BA_PHASES=1
+for rep in 1 2; do
+for lib in "$@"; do
+  for W in 1 32 256; do
+    echo "$(basename $lib) $(VIO360_LIB=$lib timeout -k 10 120 python3 tools/ba_batch_run.py $W 20 | tail -1)" || exit 1
+  done
+done
+done
