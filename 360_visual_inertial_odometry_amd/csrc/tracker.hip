@@ -22,6 +22,8 @@
 #include <float.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstring>
 #include <mutex>
 #include <hipcub/hipcub.hpp>
 
@@ -212,12 +214,42 @@ __device__ __forceinline__ void lk_region(uint8_t* Jr, int& rx0, int& ry0, const
 // calcOpticalFlowPyrLK for one point per workgroup (LK_WAVES waves): the patch pixels are spread over
 // all lanes (<= LK_NIT each), the window sums are exact integer workgroup sums, so every order gives
 // the sequential values; the per-iteration update is computed by every thread from the same totals.
-__global__ void __launch_bounds__(LK_THREADS) lk_kernel(LkArgs A) {
+template <int NT>
+__device__ void ransac_raw_body(uint32_t seed, uint32_t* raw, uint32_t* mt);  // (RANSAC section)
+constexpr int LK_AUX_BLOCKS = 17;  // LkAux: one workgroup for the raw draws, 16 for the reset and the bitmap clear
+__device__ void lk_aux(const LkAux& X, int b) {
+    if (b == 0) {
+        __shared__ uint32_t mt[624];
+        if (X.raw) ransac_raw_body<LK_THREADS>(X.seed, X.raw, mt);
+        return;
+    }
+    const size_t t = (size_t)(b - 1) * LK_THREADS + threadIdx.x, stride = (size_t)(LK_AUX_BLOCKS - 1) * LK_THREADS;
+    if (X.hist) {  // gftt_reset_kernel's work
+        if (t == 0) {
+            X.scal[2] = X.scal[3] = X.scal[4] = 0;
+            X.scal[6] = X.scal[7] = X.scal[8] = X.scal[9] = 0;
+            X.scal[10] = X.scal[11] = 0;
+        }
+        for (size_t i = t; i < (size_t)GF_BUCKETS; i += stride) X.hist[i] = 0u;
+        for (size_t i = t; i < X.topk_cap; i += stride) X.topk[i] = 0ull;
+    }
+    if (X.disc) {
+        const size_t n4 = X.disc_words / 4;
+        uint4* d4p = reinterpret_cast<uint4*>(X.disc);
+        for (size_t i = t; i < n4; i += stride) d4p[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (size_t i = 4 * n4 + t; i < X.disc_words; i += stride) X.disc[i] = 0u;
+    }
+}
+
+__global__ void __launch_bounds__(LK_THREADS) lk_kernel(LkArgs A, LkAux X) {
     __shared__ LkShared S;
     __shared__ double red[LK_WAVES];
     const int tid = threadIdx.x;
     const int pt = blockIdx.x;
-    if (pt >= A.n) return;  // whole workgroup
+    if (pt >= A.n) {  // whole workgroup
+        lk_aux(X, pt - A.n);
+        return;
+    }
     const int win = A.win;
     const float hw = (win - 1) * 0.5f;
     const float FLT_SCALE = 1.f / (1 << 20);
@@ -528,8 +560,9 @@ __device__ void ransac_sample_seq(const RansacArgs& R, Mt19937& g, int n) {
 // the first RS_RAW tempered outputs of mt19937(seed): seeding recurrence, RS_BLOCKS twists of the
 // 624-word state (three dependency-free phases each) and tempering.  Depends on the seed only, so
 // the tracker pipeline runs it on its side stream while the frames are processed.
-__global__ void __launch_bounds__(RS_THREADS) ransac_raw_kernel(uint32_t seed, uint32_t* raw) {
-    __shared__ uint32_t mt[624];
+template <int NT>
+__device__ void ransac_raw_body(uint32_t seed, uint32_t* raw, uint32_t* mt) {
+    static_assert(NT >= 227, "one twist element per thread and phase");
     const int tid = threadIdx.x;
     if (tid == 0) {  // seeding recurrence (sequential, 623 steps)
         uint32_t v = seed;
@@ -554,15 +587,20 @@ __global__ void __launch_bounds__(RS_THREADS) ransac_raw_kernel(uint32_t seed, u
             if (i < hi[ph]) mt[i] = nv;
             __syncthreads();
         }
-        if (tid < 624) {
-            uint32_t y = mt[tid];
+        for (int i = tid; i < 624; i += NT) {
+            uint32_t y = mt[i];
             y ^= y >> 11;
             y ^= (y << 7) & 0x9d2c5680u;
             y ^= (y << 15) & 0xefc60000u;
             y ^= y >> 18;
-            raw[624 * blk + tid] = y;
+            raw[624 * blk + i] = y;
         }
+        __syncthreads();  // the next twist overwrites mt
     }
+}
+__global__ void __launch_bounds__(RS_THREADS) ransac_raw_kernel(uint32_t seed, uint32_t* raw) {
+    __shared__ uint32_t mt[624];
+    ransac_raw_body<RS_THREADS>(seed, raw, mt);
 }
 
 // PREP: the input compaction (ransac_prep_body) first, in the same workgroup (one launch fewer on the
@@ -1513,6 +1551,69 @@ __device__ __forceinline__ bool lm_disc(const GfArgs& G, int x, int y) {
     return G.disc_bits && ((G.disc_bits[(size_t)y * G.disc_words + (x >> 5)] >> (x & 31)) & 1u);
 }
 
+// Tiles whose eig positions all lie at least one pixel inside the image (no reflected box positions):
+// the Sobel sums roll down a column (three source reads per cov position instead of nine: the
+// horizontal difference / smoothing of each source row kept for the next two), cov in planar LDS, and
+// eig from rolling vertical sums of horizontal triple sums (nine cov reads per position instead of 27).
+// The box sums are exact, so any summation order gives the ky / kx order's bits: each f32 product is a
+// multiple of 2^-47 (|Sobel| <= 1020 and the scale 1/3060 make a nonzero product >= scale^2 > 2^-24,
+// whose ulp is >= 2^-47) below 1/8 in magnitude, so every partial sum of nine fits 53 bits.
+template <int TY>
+__device__ void lm_eig_interior(LmShared<TY>& S) {
+    constexpr int CH = LmShared<TY>::CH, EH = LmShared<TY>::EH, CG = 3;  // CG row groups per column
+    static_assert(CG * LM_CW <= 256 && CG * LM_EW <= 256, "one column of a row group per thread");
+    float(*cv)[CH][LM_CW] = reinterpret_cast<float(*)[CH][LM_CW]>(&S.cov[0][0][0]);
+    const float scale = (float)(1.0 / 3060.0);
+    const int t = threadIdx.x;
+    if (t < CG * LM_CW) {  // cov column cx (image x = ox-2+cx: source columns cx+13 .. cx+15), rows [r0, r1)
+        const int cx = t % LM_CW, g = t / LM_CW, r0 = g * CH / CG, r1 = (g + 1) * CH / CG;
+        const int c0 = cx + 13;
+        int d[3], m[3];  // per source row: x difference, x smoothing
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint8_t* r = S.src[r0 + i];
+            d[i] = r[c0 + 2] - r[c0];
+            m[i] = r[c0] + 2 * r[c0 + 1] + r[c0 + 2];
+        }
+        for (int cy = r0; cy < r1; ++cy) {
+            const uint8_t* r = S.src[cy + 2];
+            d[2] = r[c0 + 2] - r[c0];
+            m[2] = r[c0] + 2 * r[c0 + 1] + r[c0 + 2];
+            const int sx = d[0] + 2 * d[1] + d[2], sy = m[2] - m[0];
+            const float dx = (float)sx * scale, dy = (float)sy * scale;
+            cv[0][cy][cx] = dx * dx;
+            cv[1][cy][cx] = dx * dy;
+            cv[2][cy][cx] = dy * dy;
+            d[0] = d[1]; d[1] = d[2];
+            m[0] = m[1]; m[1] = m[2];
+        }
+    }
+    __syncthreads();
+    if (t < CG * LM_EW) {  // eig column ex (cov columns ex .. ex+2), rows [e0, e1) (cov rows ey .. ey+2)
+        const int ex = t % LM_EW, g = t / LM_EW, e0 = g * EH / CG, e1 = (g + 1) * EH / CG;
+        double h[3][3];  // [cov row slot][component]: horizontal triple sums
+        auto hsum = [&](int cy, double* o) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) o[j] = ((double)cv[j][cy][ex] + (double)cv[j][cy][ex + 1]) + (double)cv[j][cy][ex + 2];
+        };
+        hsum(e0, h[0]);
+        hsum(e0 + 1, h[1]);
+        for (int ey = e0; ey < e1; ++ey) {
+            hsum(ey + 2, h[2]);
+            const double s0 = (h[0][0] + h[1][0]) + h[2][0], s1 = (h[0][1] + h[1][1]) + h[2][1],
+                         s2 = (h[0][2] + h[1][2]) + h[2][2];
+            const float a = (float)s0 * 0.5f, b = (float)s1, c = (float)s2 * 0.5f;
+            S.eig[ey][ex] = (a + c) - sqrtf((a - c) * (a - c) + b * b);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                h[0][j] = h[1][j];
+                h[1][j] = h[2][j];
+            }
+        }
+    }
+    __syncthreads();
+}
+
 // eig at the LM_EW x LM_EH positions of the tile at (ox, oy) into S.eig (the gf_eig_tile
 // arithmetic: Sobel on reflect101 neighbours, f32 products, f64 3x3 box sums in ky / kx order)
 template <int TY>
@@ -1536,6 +1637,10 @@ __device__ void lm_eig_tile(const GfArgs& G, int ox, int oy, LmShared<TY>& S) {
             }
         }
         __syncthreads();
+    }
+    if (ox >= 2 && ox + LM_EW <= W && oy >= 2 && oy + LM_EH <= H) {  // every eig position >= 1 px inside
+        lm_eig_interior(S);
+        return;
     }
     const float scale = (float)(1.0 / 3060.0);
     for (int e = threadIdx.x; e < LM_CW * LM_CH; e += 256) {
@@ -1606,21 +1711,26 @@ __global__ void __launch_bounds__(256) gftt_lmax_kernel(GfArgs G) {
     if (threadIdx.x == 0) s_cnt = 0;
     lm_eig_tile<LM_TY>(G, ox, oy, S);
     uint32_t m = 0, kmax = 0;
-    const int lane = threadIdx.x & 63;
-    for (int e = threadIdx.x; e < LM_TX * LM_TY; e += 256) {
-        const int ty = e / LM_TX, tx = e % LM_TX;
-        const int X = ox + tx, Y = oy + ty;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // lane = tile column, wave = a band of LM_TY / 4 rows: the 3x3 maximum from rolling row maxima of
+    // three eig values (no NaN: "no neighbour > v" is "v >= the 3x3 maximum", v included)
+    static_assert(LM_TX == 64 && LM_TY % 4 == 0, "one tile column per lane, four row bands");
+    constexpr int RB = LM_TY / 4;
+    const int tx = lane, X = ox + tx;
+    auto rmax = [&](int ey) { return fmaxf(fmaxf(S.eig[ey][tx], S.eig[ey][tx + 1]), S.eig[ey][tx + 2]); };
+    float hm0 = rmax(wid * RB), hm1 = rmax(wid * RB + 1);
+    for (int ty = wid * RB; ty < wid * RB + RB; ++ty) {
+        const float hm2 = rmax(ty + 2);
+        const int Y = oy + ty;
         bool c = false;
         float v = 0.f;
         if (X < G.W && Y < G.H && lm_static_in(G, X, Y)) {
             v = S.eig[ty + 1][tx + 1];
             m = max(m, ord_f32(v));
-            if (v > 0.f && X >= 1 && X < G.W - 1 && Y >= 1 && Y < G.H - 1) {
-                c = true;
-                for (int ky = 0; ky < 3; ++ky)
-                    for (int kx = 0; kx < 3; ++kx) c = c && !(S.eig[ty + ky][tx + kx] > v);
-            }
+            c = v > 0.f && X >= 1 && X < G.W - 1 && Y >= 1 && Y < G.H - 1 && !(fmaxf(fmaxf(hm0, hm1), hm2) > v);
         }
+        hm0 = hm1;
+        hm1 = hm2;
         const unsigned long long bal = __ballot(c);
         const int cnt = __popcll(bal);
         unsigned int base = 0;
@@ -1835,9 +1945,13 @@ hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int fra
     hipLaunchKernelGGL(pyr_down_kernel, g, dim3(256), 0, st, s, d);
     return hipGetLastError();
 }
-hipError_t launch_lk(const LkArgs& a, hipStream_t st) {
-    if (a.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(lk_kernel, dim3(a.n), dim3(LK_THREADS), 0, st, a);
+hipError_t launch_lk(const LkArgs& a, hipStream_t st, const LkAux* aux) {
+    LkAux x;
+    std::memset(&x, 0, sizeof x);
+    if (aux) x = *aux;
+    const int n = a.n > 0 ? a.n : 0, blocks = n + (aux ? LK_AUX_BLOCKS : 0);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(lk_kernel, dim3(blocks), dim3(LK_THREADS), 0, st, a, x);
     return hipGetLastError();
 }
 size_t ransac_raw_words() { return RS_RAW; }

@@ -93,7 +93,7 @@ struct erp_tracker {
     hipEvent_t ev[6] = {};
     // the GFTT eigenvalue map runs on a side stream, overlapped with pyramids / LK / RANSAC
     hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr, raw_done = nullptr;
+    hipEvent_t join = nullptr, pyr_done = nullptr;  // side stream: waits for the pyramids / joined before the GFTT tail
     bool stage_timing = true;  // record the per-stage events (each marker costs the stream a few us)
     bool timed_run = false;    // the last run recorded them
     // without stage markers the pipeline is captured once into a graph and replayed (the ~20 launches,
@@ -131,9 +131,8 @@ void tracker_free(erp_tracker* t) {
     if (t->run_graph) (void)hipGraphExecDestroy(t->run_graph);
     t->run_graph = nullptr;
     if (t->side) (void)hipStreamDestroy(t->side);
-    if (t->fork) (void)hipEventDestroy(t->fork);
     if (t->join) (void)hipEventDestroy(t->join);
-    if (t->raw_done) (void)hipEventDestroy(t->raw_done);
+    if (t->pyr_done) (void)hipEventDestroy(t->pyr_done);
 }
 
 int ensure_iters(erp_tracker* t, int iters) {
@@ -223,9 +222,8 @@ int tracker_alloc(erp_tracker* t) {
     for (auto& e : t->ev)
         if (hipEventCreate(&e) != hipSuccess) return hip_fail(t->ctx, hipErrorUnknown, "hipEventCreate");
     if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&t->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t->raw_done, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&t->pyr_done, hipEventDisableTiming) != hipSuccess)
         return hip_fail(t->ctx, hipErrorUnknown, "side stream / events");
     return VIO_OK;
 }
@@ -260,7 +258,9 @@ int check_klt(vio_ctx* ctx, const erp_klt_params* p) {
     return VIO_OK;
 }
 
-int enqueue_lk(erp_tracker* t, const erp_klt_params* p, int n, bool pyr_built = false) {
+// aux (the tracker pipeline): extra workgroups of the LK launch (LkAux); the ev[1] stage marker between the
+// pyramids and LK then only with stage timing (an event record costs the stream ~6 us before the next launch)
+int enqueue_lk(erp_tracker* t, const erp_klt_params* p, int n, bool pyr_built = false, const LkAux* aux = nullptr) {
     LkArgs a;
     std::memset(&a, 0, sizeof a);
     int top = lk_top_level(t, p->win, p->max_level);
@@ -279,8 +279,8 @@ int enqueue_lk(erp_tracker* t, const erp_klt_params* p, int n, bool pyr_built = 
     double eps = std::min(std::max((double)p->epsilon, 0.0), 10.0);
     a.eps2 = eps * eps;
     a.min_eig = p->min_eig_threshold;
-    if (t->ev[1]) (void)hipEventRecord(t->ev[1], t->ctx->stream);
-    hipError_t e = launch_lk(a, t->ctx->stream);
+    if (t->ev[1] && (!aux || t->stage_timing)) (void)hipEventRecord(t->ev[1], t->ctx->stream);
+    hipError_t e = launch_lk(a, t->ctx->stream, aux);
     if (e != hipSuccess) return hip_fail(t->ctx, e, "lk_kernel");
     return VIO_OK;
 }
@@ -508,30 +508,29 @@ int erp_tracker_set_points(erp_tracker* t, const float* pts, int n) {
 static int enqueue_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p, int n, int radius) {
     int rc;
     hipStream_t st = t->ctx->stream;
-    // the host enqueues the main stream's pyramids and LK first (the GPU starts on them at once), then
-    // the side stream's work, which is needed only from RANSAC on: the RANSAC draws' raw stream (seed
-    // only), the GFTT counters / histogram / top-K reset, the disc bitmap clear, then GFTT pass 1 (the
-    // eigenvalue map of the current frame does not depend on tracking) once the pyramids are built
-    VIO_HIP(t->ctx, hipEventRecord(t->fork, st));
-    if ((rc = enqueue_lk(t, klt, n))) return rc;  // records ev[1] between pyramids and LK
-    VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->fork, 0));
+    // main stream: pyramids, then LK, whose launch also carries the RANSAC draws' raw stream (seed only),
+    // the GFTT counters / histogram / top-K reset and the disc bitmap clear in extra workgroups (on the
+    // side stream they cost the main stream a cross-stream wait before RANSAC); side stream: GFTT pass 1
+    // (the eigenvalue map of the current frame does not depend on tracking) once the pyramids are built,
+    // beside LK / RANSAC (from the start of the run, beside the pyramids: measured 6 % slower)
     {
-        hipError_t e = launch_ransac_raw(p->ransac_seed, t->d_raw, t->side);
-        if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac_raw_kernel");
+        LkAux x;
+        std::memset(&x, 0, sizeof x);
+        x.raw = t->d_raw;
+        x.seed = p->ransac_seed;
+        x.hist = t->d_hist;
+        x.topk = t->d_topk;
+        x.topk_cap = t->topk_cap;
+        x.scal = t->d_scal;
+        x.disc = t->d_disc;
+        x.disc_words = (size_t)t->disc_words * t->H;
+        int top = lk_top_level(t, klt->win, klt->max_level);
+        if ((rc = build_pyramids(t, top))) return rc;
+        VIO_HIP(t->ctx, hipEventRecord(t->pyr_done, st));
+        if ((rc = enqueue_lk(t, klt, n, true, &x))) return rc;
     }
     {
-        GfArgs gr;
-        std::memset(&gr, 0, sizeof gr);
-        gr.hist = t->d_hist;
-        gr.topk = t->d_topk;
-        gr.topk_cap = t->topk_cap;
-        hipError_t e = launch_gftt_reset(gr, t->d_scal, t->side);
-        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_reset_kernel");
-        VIO_HIP(t->ctx, hipMemsetAsync(t->d_disc, 0, sizeof(uint32_t) * t->disc_words * t->H, t->side));
-        VIO_HIP(t->ctx, hipEventRecord(t->raw_done, t->side));  // raw draws, reset and cleared discs: one wait
-    }
-    {  // GFTT pass 1 shares the chip with the latency-bound LK / RANSAC, not with the pyramids
-        VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->ev[1], 0));
+        VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->pyr_done, 0));
         hipError_t e =
             launch_gftt_lmax(gf_lmax_args(t, t->lvl[1][0], t->lp[0], p->boundary_margin, p->polar_ratio), t->side);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_lmax_kernel");
@@ -541,16 +540,13 @@ static int enqueue_run(erp_tracker* t, const erp_klt_params* klt, const erp_trac
     RansacArgs r = ransac_args(t, n, 1, p->ransac_iters, p->ransac_seed, p->ransac_thresh_rad, p->polar_ratio,
                                p->boundary_margin, t->d_pts, t->d_next);
     if (n > 0) {
-        VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->raw_done, 0));
         hipError_t e = launch_ransac(r, true, st);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac kernels");
     } else {
         VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal, 0, 2 * sizeof(int), st));
     }
     if (t->stage_timing) VIO_HIP(t->ctx, hipEventRecord(t->ev[3], st));
-    // CreateFeatureMask: discs of radius (int)min_dist around every kept point (bitmap cleared on the side
-    // stream before raw_done, which the main stream waited for before RANSAC)
-    if (n <= 0) VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->raw_done, 0));
+    // CreateFeatureMask: discs of radius (int)min_dist around every kept point (bitmap cleared in the LK launch)
     if (n > 0 && radius > 0) {
         DiscArgs d{t->d_next, t->d_kept, nullptr, nullptr, t->d_disc, t->disc_words, t->W, t->H, radius,
                    t->d_halfw};

@@ -119,7 +119,20 @@ struct DiscArgs {
 };
 
 hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int frames, hipStream_t st);
-hipError_t launch_lk(const LkArgs& a, hipStream_t st);
+// work riding in extra workgroups of the LK launch (tracker pipeline, off LK's critical path and
+// without a cross-stream wait): the RANSAC draws' raw mt19937 words, the GFTT counters / histogram /
+// top-K reset and the disc bitmap clear (null pointers: none)
+struct LkAux {
+    uint32_t* raw;
+    uint32_t seed;
+    unsigned int* hist;
+    unsigned long long* topk;
+    unsigned int topk_cap;
+    int* scal;
+    uint32_t* disc;
+    size_t disc_words;  // total 32-bit words of the bitmap
+};
+hipError_t launch_lk(const LkArgs& a, hipStream_t st, const LkAux* aux = nullptr);
 // the tempered mt19937 stream of a seed (independent of the points: may run on another stream)
 hipError_t launch_ransac_raw(uint32_t seed, uint32_t* raw, hipStream_t st);
 size_t ransac_raw_words();

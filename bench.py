@@ -61,8 +61,16 @@ def ba_traffic(args):
 
 
 def klt_traffic():
-    """PMC HBM bytes of one ERP-KLT pipeline run: per-launch bytes x launches per run (lk_kernel runs once)."""
-    k, src = pmc_traffic()
+    """PMC HBM bytes of one ERP-KLT pipeline run: per-launch bytes x launches per run (lk_kernel runs once).
+    Source: the newest tracker-only summary (tools/gpu_trk_pmc.sh -> profiles/r*_pmc_traffic_klt.json),
+    else the bench-wide one."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_klt.json")))
+    if files:
+        with open(files[-1]) as f:
+            k = json.load(f)["kernels"]
+    else:
+        k, src = pmc_traffic()
     if not k or "lk_kernel" not in k:
         return None
     runs = k["lk_kernel"]["dispatches"]
