@@ -485,20 +485,24 @@ ctx.close()
 
 
 def test_global_ba_solve_paths_bitwise(vio, tmp_path):
-    """The persistent triangular solves and the per-step kernels (VIO_GBA_PERSISTENT_SOLVE=0, the
-    fallback beyond 256 blocks) reduce every row dot the same way: the same solution bits."""
+    """Every schedule of the global path gives the default's solution bits: the per-step triangular
+    solves (VIO_GBA_PERSISTENT_SOLVE=0, the fallback beyond 256 blocks: every row dot reduced the same
+    way), separate update / diagonal / panel launches instead of the fused step (VIO_GBA_FUSE_M=0),
+    direct launches instead of the replayed graph (VIO_GBA_GRAPH=0): each tile receives its column
+    updates in column order in all of them."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = []
-    for flag in ("1", "0"):
-        f = str(tmp_path / f"gba_{flag}.npz")
-        env = dict(os.environ, VIO_GBA_PERSISTENT_SOLVE=flag)
-        subprocess.run([sys.executable, "-c", _GBA_AB, root, f], env=env, check=True, timeout=100)
+    variants = [{}, {"VIO_GBA_PERSISTENT_SOLVE": "0"}, {"VIO_GBA_FUSE_M": "0"}, {"VIO_GBA_GRAPH": "0"}]
+    for i, v in enumerate(variants):
+        f = str(tmp_path / f"gba_{i}.npz")
+        subprocess.run([sys.executable, "-c", _GBA_AB, root, f], env=dict(os.environ, **v), check=True, timeout=100)
         outs.append(np.load(f))
-    a, b = outs
-    assert np.array_equal(a["T"], b["T"]) and np.array_equal(a["l"], b["l"]) and np.array_equal(a["c"], b["c"])
+    a = outs[0]
+    for v, b in zip(variants[1:], outs[1:]):
+        assert np.array_equal(a["T"], b["T"]) and np.array_equal(a["l"], b["l"]) and np.array_equal(a["c"], b["c"]), v
 
 
 def test_batches_from_two_threads(vio, synth):
