@@ -581,11 +581,10 @@ __global__ void __launch_bounds__(256) chol_trsm_kernel(double* S, int n, int k,
 // trailing update: A_ij -= A_ik A_jk^T for k < j <= i (lower block triangle), one tile per block.
 // part 0: every tile; part 1: the first trailing column only (j = k+1, the next step's diagonal
 // block and panel); part 2: the rest (j >= k+2) — the look-ahead split of gba_launch_cholesky.
-__global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k, int part) {
-    __shared__ double As[NB][NB + 1];
-    __shared__ double Bs[NB][NB + 1];
-    // blockIdx.x -> (i, j) with 0 <= jj <= ii < m, i = k+1+ii, j = k+1+jj
-    const long long t = blockIdx.x;
+// tile t of the update (one workgroup); As / Bs: NB x (NB + 1) doubles of LDS each
+__device__ __forceinline__ void syrk_tile(double* S, int n, int k, int part, long long t, double (*As)[NB + 1],
+                                          double (*Bs)[NB + 1]) {
+    // t -> (i, j) with 0 <= jj <= ii < m, i = k+1+ii, j = k+1+jj
     int ii = 0, jj = 0;
     if (part == 1) {
         ii = (int)t;
@@ -629,6 +628,11 @@ __global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k,
                 const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
                 if (i != j || c <= r) C[(size_t)r * n + c] = cv[ti][tj][q] - acc[ti][tj][q];
             }
+}
+__global__ void __launch_bounds__(256) chol_syrk_kernel(double* S, int n, int k, int part) {
+    __shared__ double As[NB][NB + 1];
+    __shared__ double Bs[NB][NB + 1];
+    syrk_tile(S, n, k, part, blockIdx.x, As, Bs);
 }
 
 // forward substitution step k: y_k = Linv_kk b_k (every block recomputes it from the final b_k;
@@ -772,11 +776,22 @@ __device__ __forceinline__ void flag_publish(int* f) {
 // and chol_trsm_kernel's, in the same order: bitwise the three-launch step.  k == 0: no update.
 // Dynamic LDS: CHOL_DIAG_LDS bytes.  flag: 0 pending, 1 L_kk^-1 final, 2 the block is not positive
 // definite.
+// Workgroups past the step's m + 1 (trail > 0: `trail` of them) apply step k-1's trailing update right of
+// block column k (chol_syrk_kernel part 2 of step k-1, its tiles in order): disjoint from block column k,
+// after panel k-1 (the previous launch) and before step k+1 (the next), so the look-ahead needs no second
+// stream for it.
 __global__ void __launch_bounds__(256) chol_step_kernel(double* S, int n, int k, double* Linv, int* fail, int* flag,
-                                                        int* tmo) {
+                                                        int* tmo, int trail) {
     extern __shared__ double dyn[];
     double (*As)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(dyn);
     double (*Bs)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(dyn + NB * TLD);
+    {
+        const int m1 = n / NB - k;  // the step's own workgroups
+        if ((int)blockIdx.x >= m1) {
+            if ((int)blockIdx.x - m1 < trail) syrk_tile(S, n, k - 1, 2, (long long)blockIdx.x - m1, As, Bs);
+            return;
+        }
+    }
     __shared__ int bad_s, ok_s;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r0 = 32 * (wid >> 1), c0 = 32 * (wid & 1);
@@ -1278,6 +1293,7 @@ hipError_t gba_cholesky_attributes() {
     return e;
 }
 constexpr int kGbaFuseM = 96;  // chol_step_kernel for steps with at most this many block rows (config 5: every step)
+constexpr long long kGbaFuseTrail = 2500;  // trailing updates of at most this many tiles in the next step's launch
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
     int* tmo = A.flags ? A.flags + FLAG_STRIDE * 2 * (size_t)nblk : nullptr;  // timeout word of the Cholesky + solves
@@ -1309,20 +1325,35 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     }();
     int* sflag = A.flags + FLAG_STRIDE * (2 * (size_t)nblk + 1);
     if ((e = hipMemsetAsync(sflag, 0, sizeof(int) * FLAG_STRIDE * (size_t)nblk, s)) != hipSuccess) return e;
-    auto step = [&](int k) {  // column k-1's update of block column k (k > 0), diagonal block k, panel k
+    // trail: tiles of step k-1's trailing update (part 2) run as extra workgroups of step k's launch
+    auto step = [&](int k, int trail) {  // column k-1's update of block column k (k > 0), diagonal block k, panel k
         const int m = nblk - k - 1;
         if (m + 1 <= fuse_m) {
-            hipLaunchKernelGGL(chol_step_kernel, dim3(m + 1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv, fail,
-                               sflag + FLAG_STRIDE * k, tmo);
+            hipLaunchKernelGGL(chol_step_kernel, dim3(m + 1 + trail), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv,
+                               fail, sflag + FLAG_STRIDE * k, tmo, trail);
             return;
         }
+        if (trail > 0)
+            hipLaunchKernelGGL(chol_syrk_kernel, dim3(trail), dim3(256), 0, s, A.S, n, k - 1, 2);
         if (k > 0) hipLaunchKernelGGL(chol_syrk_kernel, dim3(m + 1), dim3(256), 0, s, A.S, n, k - 1, 1);
         hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv, fail);
         if (m > 0) hipLaunchKernelGGL(chol_trsm_kernel, dim3(m), dim3(256), 0, s, A.S, n, k, (const double*)A.Linv);
     };
-    step(0);
+    // trailing updates of at most fuse_trail tiles (the late steps, where the cross-stream round trip of
+    // the look-ahead costs more than the update) ride in the next step's launch; larger ones overlap it on
+    // the side stream
+    static const long long fuse_trail = [] {
+        const char* v = std::getenv("VIO_GBA_FUSE_TRAIL");
+        return v ? std::atoll(v) : kGbaFuseTrail;
+    }();
+    step(0, 0);
     for (int k = 0; k + 1 < nblk; ++k) {
         const int m = nblk - k - 1;  // trailing block rows of step k
+        const long long tiles = (long long)(m - 1) * m / 2;  // its trailing update right of block column k+1
+        if (m >= 2 && tiles <= fuse_trail && m <= fuse_m) {
+            step(k + 1, (int)tiles);
+            continue;
+        }
         if ((e = hipEventRecord(ev_panel, s)) != hipSuccess) return e;  // panel k final
         if (m >= 2) {
             if ((e = hipStreamWaitEvent(r, ev_panel, 0)) != hipSuccess) return e;
@@ -1330,7 +1361,7 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
                                k, 2);
             if ((e = hipEventRecord(ev_rest, r)) != hipSuccess) return e;
         }
-        step(k + 1);
+        step(k + 1, 0);
         if (m >= 2 && (e = hipStreamWaitEvent(s, ev_rest, 0)) != hipSuccess) return e;
     }
     return hipGetLastError();
