@@ -2,6 +2,7 @@
 // by the host LM loop in ba_global_host.cpp.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "vio360.h"
@@ -84,6 +85,17 @@ struct GbaArgs {
     double* imu_cost;         // [K] per-factor cost (scratch of the fixed-order sum)
     double* Himu;             // [ni][ni] J^T J of the IMU factors (imu-space)
 };
+// GbaArgs crosses translation units (ba_global_host.cpp fills it; ba_global.hip and ba_kernel.hip's
+// gba_imu.inc read it): its layout is pinned here, in every TU that includes this header, and each of
+// those TUs exports its compiled-in signature (gba_layout_sig_*) for the runtime cross-check in
+// vio_ctx_create.  Change a member => update these numbers (and the build rebuilds every user).
+static_assert(sizeof(GbaArgs) == 640, "GbaArgs layout changed: update the pinned size");
+static_assert(offsetof(GbaArgs, flags) == 488 && offsetof(GbaArgs, is_vi) == 496 &&
+              offsetof(GbaArgs, S) == 448 && offsetof(GbaArgs, Himu) == 632, "GbaArgs offsets changed");
+constexpr uint64_t gba_layout_sig() {
+    return (uint64_t)sizeof(GbaArgs) << 48 | (uint64_t)offsetof(GbaArgs, flags) << 32 |
+           (uint64_t)offsetof(GbaArgs, is_vi) << 16 | (uint64_t)offsetof(GbaArgs, Himu);
+}
 
 // the word a timed-out inter-workgroup wait of the Cholesky / triangular solves sets (cleared at the start
 // of every gba_launch_cholesky); nonzero after a step means a device fault, not a failed factorisation

@@ -29,6 +29,8 @@
 
 namespace vio360 {
 
+uint64_t gba_layout_sig_ba_global() { return gba_layout_sig(); }
+
 constexpr int GT = 256;  // threads per block of the element-wise kernels
 
 __device__ __forceinline__ double wave_sum_d(double v) {

@@ -18,6 +18,9 @@
 
 namespace vio360 {
 
+uint64_t ba_layout_sig_ba_global_host() { return ba_layout_sig(); }
+uint64_t gba_layout_sig_ba_global_host() { return gba_layout_sig(); }
+
 namespace {
 
 struct DevBufs {

@@ -271,8 +271,8 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     // fills the chip with 2 groups per window and halves ph_solve's partial sums; smaller batches keep
     // more, shorter groups (latency)
     const char* gse = std::getenv("VIO_BA_SCHUR_GS");  // experiment override
-    // (>= PH_GS_MIN = 1, the workspace sizing of ba_phases.inc)
-    const int gs = gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : 5;
+    // (>= PH_GS_MIN = 5, the workspace sizing of ba_phases.inc; 1..4 measured slower at 1 and 32 windows)
+    const int gs = gse ? std::max(5, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : 5;
     for (BaWin& w : pk.win) w.gs = gs;
     UP(pk.win, win, const BaWin*);
     UP(pk.pose_raw, pose_raw, const double*);
@@ -510,9 +510,21 @@ int vio_ctx_set_ba_route(vio_ctx* ctx, int route) {
 
 static std::string g_create_error;
 
+int vio_layout_check(void) {
+    const uint64_t ba = ba_layout_sig(), gba = gba_layout_sig_ba_global();
+    return ba == ba_layout_sig_ba_kernel() && ba == ba_layout_sig_ba_global_host() &&
+                   gba == gba_layout_sig_ba_kernel() && gba == gba_layout_sig_ba_global_host()
+               ? VIO_OK
+               : VIO_EDEVICE;
+}
+
 int vio_ctx_create(int device, vio_ctx** out) {
     if (!out) return VIO_EINVAL;
     *out = nullptr;
+    if (vio_layout_check() != VIO_OK) {
+        g_create_error = "translation units disagree on the BaWin/BaPools/GbaArgs layout (stale object: rebuild)";
+        return VIO_EDEVICE;
+    }
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= 0) {
@@ -581,6 +593,7 @@ int vio_ba_batch_create(vio_ctx* ctx, const vio_ba_problem* probs, int n, vio_ba
 int vio_ba_batch_run(vio_ba_batch* b) {
     if (!b) return VIO_EINVAL;
     vio_ctx* ctx = b->ctx;
+    VIO_DEVICE(ctx);
     if (b->dev.timing_pending) {  // fold the previous run's time in before re-recording
         VIO_HIP(ctx, hipEventSynchronize(b->dev.ev1));
         float ms = 0.f;
@@ -614,17 +627,20 @@ int vio_ba_batch_set_preint(vio_ba_batch* b, const vio_preint* src, int count, i
 
 int vio_ba_batch_sync(vio_ba_batch* b) {
     if (!b) return VIO_EINVAL;
+    VIO_DEVICE(b->ctx);
     VIO_HIP(b->ctx, hipStreamSynchronize(b->ctx->stream));
     return VIO_OK;
 }
 
 int vio_ba_batch_download(vio_ba_batch* b, vio_ba_output* outs) {
     if (!b || !outs) return VIO_EINVAL;
+    VIO_DEVICE(b->ctx);
     return download_batch(b->ctx, b->dev, outs);
 }
 
 int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count) {
     if (!b || !avg_ms || !count) return VIO_EINVAL;
+    VIO_DEVICE(b->ctx);
     if (b->dev.timing_pending) {
         VIO_HIP(b->ctx, hipEventSynchronize(b->dev.ev1));
         float ms = 0.f;
@@ -642,6 +658,7 @@ int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count) {
 
 int vio_ba_batch_profile(vio_ba_batch* b, int enable) {
     if (!b) return VIO_EINVAL;
+    VIO_DEVICE(b->ctx);
     if (enable && !b->dev.prof_buf) {
         VIO_HIP(b->ctx, hipMalloc(&b->dev.prof_buf, sizeof(unsigned long long) * VIO_BA_PROF_SLOTS * b->dev.n));
         VIO_HIP(b->ctx, hipMemsetAsync(b->dev.prof_buf, 0, sizeof(unsigned long long) * VIO_BA_PROF_SLOTS * b->dev.n, b->ctx->stream));
@@ -656,6 +673,7 @@ int vio_ba_batch_profile(vio_ba_batch* b, int enable) {
 
 int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out) {
     if (!b || !out || !b->dev.prof_buf) return VIO_EINVAL;
+    VIO_DEVICE(b->ctx);
     constexpr int NS = VIO_BA_PROF_SLOTS;
     std::vector<unsigned long long> v(NS * b->dev.n);
     VIO_HIP(b->ctx, hipMemcpyAsync(v.data(), b->dev.prof_buf, sizeof(unsigned long long) * v.size(),
@@ -753,6 +771,7 @@ int vio_ba_record_unpack(const void* record, size_t record_bytes, vio_ba_output*
 
 int vio_ba_solve_batched(vio_ctx* ctx, const vio_ba_problem* probs, vio_ba_output* outs, int n) {
     if (!ctx || !probs || !outs || n <= 0) return VIO_EINVAL;
+    VIO_DEVICE(ctx);
     // problems beyond one workgroup's reduced system (K > 16: RunBA over hundreds of keyframes,
     // config 5) take the multi-kernel global path, one problem at a time
     bool any_global = false;

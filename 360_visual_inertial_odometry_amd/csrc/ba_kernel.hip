@@ -20,11 +20,15 @@
 #include <mutex>
 
 #include "ba_types.h"
+#include "ba_global.h"
 #include "ba_factor_dev.h"
 #include "chol_dev.h"
 #include "lie_dev.h"
 
 namespace vio360 {
+
+uint64_t ba_layout_sig_ba_kernel() { return ba_layout_sig(); }
+uint64_t gba_layout_sig_ba_kernel() { return gba_layout_sig(); }
 
 constexpr int NI_MAX = 3 * VI_KMAX + 6;
 // per-window workspace after ba_ws_layout(): IMU sqrt-information, imu-space H and g

@@ -3,6 +3,7 @@
 // (src/optimization/Optimizer.cpp:83-966).  All arrays are pooled over the batch; each window
 // carries element offsets into the pools.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #include "vio360.h"
@@ -72,6 +73,23 @@ struct BaPools {
     int imu_in_back;             // phase route: the IMU candidate terms in an extra workgroup of the
                                  // back-substitution grid (small batches) instead of at the end of ph_solve
 };
+// BaWin / BaPools cross translation units (ba_host.cpp packs them, ba_kernel.hip reads them): pinned
+// here in every TU that includes this header, and cross-checked at run time (ba_layout_sig).
+static_assert(sizeof(BaWin) == 448 && offsetof(BaWin, gravity) == 304 && offsetof(BaWin, o_ws) == 424 &&
+              offsetof(BaWin, o_tr) == 440, "BaWin layout changed: update the pinned offsets");
+static_assert(sizeof(BaPools) == 208 && offsetof(BaPools, prof) == 184 && offsetof(BaPools, route) == 192 &&
+              offsetof(BaPools, imu_in_back) == 200, "BaPools layout changed: update the pinned offsets");
+constexpr uint64_t ba_layout_sig() {
+    return (uint64_t)sizeof(BaWin) << 48 | (uint64_t)offsetof(BaWin, o_ws) << 32 |
+           (uint64_t)sizeof(BaPools) << 16 | (uint64_t)offsetof(BaPools, imu_in_back);
+}
+// the signatures each TU was compiled with (ba_layout_sig / gba_layout_sig of ba_global.h), compared by
+// vio_layout_check
+uint64_t ba_layout_sig_ba_kernel();
+uint64_t ba_layout_sig_ba_global_host();
+uint64_t gba_layout_sig_ba_kernel();
+uint64_t gba_layout_sig_ba_global_host();
+uint64_t gba_layout_sig_ba_global();
 
 // workspace sub-offsets (in doubles) relative to BaWin::o_ws
 struct BaWsLayout {

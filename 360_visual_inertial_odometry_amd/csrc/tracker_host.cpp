@@ -113,6 +113,7 @@ namespace {
 
 template <class T>
 int dalloc(erp_tracker* t, T** p, size_t bytes) {
+    DeviceScope scope(t->ctx->device);  // every tracker buffer lives on the context's device
     void* q = nullptr;
     if (hipMalloc(&q, std::max<size_t>(bytes, 64)) != hipSuccess) {
         set_error(t->ctx, "hipMalloc failed in the tracker");
@@ -500,6 +501,7 @@ int erp_tracker_set_points(erp_tracker* t, const float* pts, int n) {
         return VIO_EINVAL;
     }
     t->n_pts = n;
+    VIO_DEVICE(t->ctx);
     if (n) VIO_HIP(t->ctx, hipMemcpyAsync(t->d_pts, pts, sizeof(float) * 2 * n, hipMemcpyHostToDevice, t->ctx->stream));
     return VIO_OK;
 }
@@ -626,12 +628,14 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
 
 int erp_tracker_sync(erp_tracker* t) {
     if (!t) return VIO_EINVAL;
+    VIO_DEVICE(t->ctx);
     VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
     return VIO_OK;
 }
 
 int erp_tracker_download(erp_tracker* t, float* next, uint8_t* status, uint8_t* kept, float* corners, int* n_corners) {
     if (!t) return VIO_EINVAL;
+    VIO_DEVICE(t->ctx);
     VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
     const int n = t->n_pts;
     if (n && next) VIO_HIP(t->ctx, hipMemcpy(next, t->d_next, sizeof(float) * 2 * n, hipMemcpyDeviceToHost));
@@ -655,6 +659,7 @@ int erp_tracker_set_stage_timing(erp_tracker* t, int on) {
 int erp_tracker_stage_ms(erp_tracker* t, double* pyr_ms, double* lk_ms, double* ransac_ms, double* gftt_ms,
                          double* total_ms) {
     if (!t || !t->ran) return VIO_EINVAL;
+    VIO_DEVICE(t->ctx);
     VIO_HIP(t->ctx, hipEventSynchronize(t->ev[4]));
     float a = -1, b = -1, c = -1, d = -1, e = 0;
     if (t->timed_run) {
@@ -677,6 +682,7 @@ int erp_klt_track(vio_ctx* ctx, const uint8_t* prev, const uint8_t* curr, int W,
     if (!ctx || !prev || !curr || n < 0 || (n > 0 && (!pts || !next || !status))) return VIO_EINVAL;
     int rc = check_klt(ctx, params);
     if (rc) return rc;
+    VIO_DEVICE(ctx);
     erp_tracker* t = nullptr;
     if ((rc = erp_tracker_create(ctx, W, H, std::max(n, 1), 0, &t))) return rc;
     if (!(rc = upload_frame(t, 0, prev, stride)) && !(rc = upload_frame(t, 1, curr, stride)) &&
@@ -698,6 +704,7 @@ int erp_gftt(vio_ctx* ctx, const uint8_t* img, const uint8_t* mask, int W, int H
              double quality, double min_dist, float* out_xy, int* n_out) {
     if (!ctx || !img || !n_out || W < 3 || H < 3 || quality <= 0 || min_dist < 0 || max_corners < 0) return VIO_EINVAL;
     if (max_corners == 0) max_corners = W * H;  // "no limit"
+    VIO_DEVICE(ctx);
     erp_tracker* t = nullptr;
     int rc = erp_tracker_create(ctx, W, H, 1, max_corners, &t);
     if (rc) return rc;
@@ -728,6 +735,7 @@ int erp_rot_ransac(vio_ctx* ctx, const float* p0, const float* p1, int n, int W,
     }
     for (int i = 0; i < 3 * iters; ++i)
         if (samples[i] < 0 || samples[i] >= n) { set_error(ctx, "RANSAC sample index out of range"); return VIO_EINVAL; }
+    VIO_DEVICE(ctx);
     erp_tracker* t = nullptr;
     int rc = erp_tracker_create(ctx, std::max(W, 8), std::max(H, 8), n, 0, &t);
     if (rc) return rc;
@@ -887,6 +895,7 @@ int erp_frontend_create(vio_ctx* ctx, int W, int H, const erp_frontend_params* p
         p->max_features_per_grid <= 0 || p->min_distance < 0 || p->quality_level <= 0)
         return VIO_EINVAL;
     *out = nullptr;
+    VIO_DEVICE(ctx);
     erp_frontend* f = new erp_frontend();
     f->p = *p;
     f->W = W; f->H = H;
@@ -908,6 +917,7 @@ int erp_frontend_track(erp_frontend* f, const uint8_t* img, int stride, int* n_f
     if (!f || !img) return VIO_EINVAL;
     erp_tracker* t = f->t;
     vio_ctx* ctx = t->ctx;
+    VIO_DEVICE(ctx);
     hipStream_t st = ctx->stream;
     int rc;
     if ((rc = upload_frame(t, 1, img, stride))) return rc;

@@ -57,6 +57,10 @@ void vio_ctx_destroy(vio_ctx* ctx);
 /* last error message of this context (or of the last failed vio_ctx_create when ctx==NULL) */
 const char* vio_ctx_last_error(const vio_ctx* ctx);
 int vio_abi_version(void);
+/* VIO_OK when every translation unit of this library was compiled against the same layout of its
+ * internal cross-TU argument structs (a stale object after a header change is reported as VIO_EDEVICE
+ * here and by vio_ctx_create instead of faulting a kernel); needs no GPU */
+int vio_layout_check(void);
 
 /* Window-BA execution route of this context's later solves / batches (both routes give the same
    results to roundoff; within a route results do not depend on the batch):
