@@ -230,6 +230,26 @@ def test_config4_fixture_reproduces(vio, synth):
         assert o["initial_cost"] == ref[i]["initial_cost"]
 
 
+def test_config3_cloud_fixture_reproduces(vio, synth):
+    """tests/golden/config3_cloud.json (the converged config-3 GPU bar) is this oracle's cloud: the
+    unperturbed solve and two members regenerate exactly, and the cloud is wider than SURVEY §8c's
+    bar where the GPU test widens it (so the widening is the reference's own sensitivity)."""
+    import json
+    import oracle_lib
+    ref = json.load(open(os.path.join(GOLDEN, "config3_cloud.json")))
+    w = synth.config3()
+    o = oracle_lib.ba_solve(vio, vio.BaProblem(w, variant=vio.VIO_BA_VI))
+    assert o["iterations"] == ref["oracle"]["iterations"] and o["final_cost"] == ref["oracle"]["final_cost"]
+    for m in (ref["members"][1], ref["members"][4]):
+        c = oracle_lib.ba_solve(vio, vio.BaProblem(dict(w, lm_xyz=w["lm_xyz"] * (1 + m["e"])), variant=vio.VIO_BA_VI))
+        assert c["iterations"] == m["iterations"]
+        assert np.abs(o["T_wb"][:, :3, 3] - c["T_wb"][:, :3, 3]).max() == m["pos_m"]
+        assert np.abs(o["bg"] - c["bg"]).max() == m["bg"]
+    mx = ref["max"]
+    assert mx["pos_m"] > 1e-4 and mx["lm_m"] > 1e-3 and mx["bg"] > 1e-4 and mx["cost_rel"] > 1e-6
+    assert ref["iterations_range"][1] - ref["iterations_range"][0] > 2
+
+
 # ---- Schur complement: the reference's own Ceres fixtures -----------------------------------------
 class OracleBsm(C.Structure):
     """oracle_bsm (oracle/ba_oracle.c): block-sparse matrix of the generic Schur eliminator."""
