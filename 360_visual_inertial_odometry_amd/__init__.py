@@ -23,6 +23,7 @@ EXPORTS = [
     "vio_abi_version", "vio_ctx_create", "vio_ctx_destroy", "vio_ctx_last_error",
     "vio_ba_solve", "vio_ba_solve_batched", "vio_ba_batch_create", "vio_ba_batch_run",
     "vio_ba_batch_sync", "vio_ba_batch_download", "vio_ba_batch_kernel_ms", "vio_ba_batch_destroy",
+    "vio_ba_batch_route",
     "vio_ba_batch_profile", "vio_ba_batch_phase_cycles",
     "erp_klt_track", "erp_gftt", "erp_rot_ransac", "erp_ransac_samples", "erp_tracker_create",
     "erp_tracker_upload", "erp_tracker_device_frame", "erp_tracker_swap", "erp_tracker_set_points",
@@ -68,6 +69,7 @@ def lib():
     L.vio_ba_batch_sync.argtypes = [C.c_void_p]
     L.vio_ba_batch_download.argtypes = [C.c_void_p, C.POINTER(abi.VioBaOutput)]
     L.vio_ba_batch_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+    L.vio_ba_batch_route.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.vio_ba_batch_destroy.argtypes = [C.c_void_p]
     L.vio_ba_batch_profile.argtypes = [C.c_void_p, C.c_int]
     L.vio_ba_batch_phase_cycles.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
@@ -183,7 +185,7 @@ class Context:
             pass
 
     # ---- bundle adjustment ----
-    ROUTE_AUTO, ROUTE_PHASES, ROUTE_SINGLE_KERNEL = 0, 1, 2
+    ROUTE_AUTO, ROUTE_PHASES, ROUTE_SINGLE_KERNEL, ROUTE_CLUSTER = 0, 1, 2, 3
 
     def set_ba_route(self, route):
         """vio_ctx_set_ba_route: execution route of later window solves on this context."""
@@ -622,6 +624,14 @@ class BaBatch:
         ms, cnt = C.c_double(), C.c_int()
         self.ctx.check(lib().vio_ba_batch_kernel_ms(self.h, C.byref(ms), C.byref(cnt)), "vio_ba_batch_kernel_ms")
         return ms.value, cnt.value
+
+    ROUTES = {1: "phases", 2: "single-kernel", 3: "cluster"}
+
+    def route(self):
+        """vio_ba_batch_route: (route name, workgroups per window of the cluster route or 0)"""
+        r, c = C.c_int(), C.c_int()
+        self.ctx.check(lib().vio_ba_batch_route(self.h, C.byref(r), C.byref(c)), "vio_ba_batch_route")
+        return self.ROUTES.get(r.value, str(r.value)), c.value
 
     PHASES = ["setup", "eval+J", "linearise", "step-prep", "schur-gemm", "cholesky", "backsub",
               "candidate", "eval-cost", "control", "post", "schur-fill", "schur-prefetch", "schur-assemble", "imu-eval", "imu-normal-eq",

@@ -27,6 +27,8 @@ hipError_t launch_ba_phases(const BaPools& P, const BaWin* hw, int n, hipStream_
 size_t ba_phase_doubles(int K, int L, int N, int T);  // sized for the smallest group (most partials)
 const char* ba_phases_failed_launch();
 hipError_t ba_phases_prepare(const BaWin* hw, int n);
+int ba_cluster_members(const BaWin* hw, int n, int max_per_window);
+hipError_t launch_ba_cluster(const BaPools& P, int n, int C, hipStream_t stream);
 bool global_ba_applicable(const vio_ba_problem& p);
 int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out);
 size_t ba_ws_extra_doubles();
@@ -245,11 +247,28 @@ struct BaDevice {
     hipStream_t lane_st[kPhLanesMax - 1] = {};  // side streams of the phase route's sub-batches
     hipEvent_t lane_ev[kPhLanesMax] = {};       // their fork / join events
     bool reusable = false;                 // vio_ba_batch: replayed many times (graph); one-shot solves launch directly
+    int cluster_C = 0;                     // cluster route: workgroups per window (0: another route)
     double ms_sum = 0.0;
     int ms_count = 0;
     bool timing_pending = false;
     std::vector<int32_t> perm_host;
 };
+
+static bool env_flag(const char* name) {
+    const char* e = std::getenv(name);
+    return e && e[0] == '1';
+}
+// the cluster route (one persistent launch, ba_phases.inc ph_cluster_kernel) for batches of up to
+// kClusterMaxWindows windows: a window's serial chain (prep, solve) then pays no kernel boundaries and
+// its Schur groups overlap the step control / bookkeeping; larger batches fill the chip with the phase
+// kernels
+constexpr int kClusterMaxWindows = 32;
+static bool cluster_wanted(const vio_ctx* ctx, int n) {
+    static const bool mono = env_flag("VIO_BA_MONOLITHIC"), phases = env_flag("VIO_BA_PHASES");
+    if (ctx->ba_route == VIO_BA_ROUTE_CLUSTER) return true;
+    if (ctx->ba_route != VIO_BA_ROUTE_AUTO || mono || phases) return false;
+    return n <= kClusterMaxWindows;
+}
 
 static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     Packed& pk = d.pk;
@@ -271,8 +290,14 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     // fills the chip with 2 groups per window and halves ph_solve's partial sums; smaller batches keep
     // more, shorter groups (latency)
     const char* gse = std::getenv("VIO_BA_SCHUR_GS");  // experiment override
-    // (>= PH_GS_MIN = 5, the workspace sizing of ba_phases.inc; 1..4 measured slower at 1 and 32 windows)
-    const int gs = gse ? std::max(5, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : 5;
+    // (1..4 measured slower at 1 and 32 windows on the phase route); the cluster route: one chunk per
+    // group, the group's member owns its landmarks
+    static const int cmax = [] {
+        const char* v = std::getenv("VIO_BA_CLUSTER_C");  // experiment override: members per window
+        return v ? std::atoi(v) : 0;
+    }();
+    d.cluster_C = cluster_wanted(ctx, d.n) ? ba_cluster_members(pk.win.data(), d.n, cmax) : 0;
+    const int gs = d.cluster_C ? 1 : gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : 5;
     for (BaWin& w : pk.win) w.gs = gs;
     UP(pk.win, win, const BaWin*);
     UP(pk.pose_raw, pose_raw, const double*);
@@ -319,6 +344,10 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     d.P.out_sum = (double*)ptr;
     if ((rc = alloc(sizeof(vio_ba_iteration) * pk.tr_total, &ptr)) != VIO_OK) return rc;
     d.P.out_trace = (vio_ba_iteration*)ptr;
+    if (d.cluster_C) {
+        if ((rc = alloc(sizeof(int) * PH_SYNC_INTS * (size_t)d.n, &ptr)) != VIO_OK) return rc;
+        d.P.csync = (int*)ptr;
+    }
     VIO_HIP(ctx, hipEventCreate(&d.ev0));
     VIO_HIP(ctx, hipEventCreate(&d.ev1));
     return VIO_OK;
@@ -340,8 +369,23 @@ static void free_batch(BaDevice& d) {
         if (ev) (void)hipEventDestroy(ev), ev = nullptr;
 }
 
+// the cluster route's per-window error words (a bounded hand-off wait that expired): VIO_EDEVICE
+static int check_cluster(vio_ctx* ctx, BaDevice& d) {
+    if (!d.cluster_C || !d.P.csync) return VIO_OK;
+    std::vector<int> sync((size_t)PH_SYNC_INTS * d.n);
+    VIO_HIP(ctx, hipMemcpyAsync(sync.data(), d.P.csync, sizeof(int) * sync.size(), hipMemcpyDeviceToHost, ctx->stream));
+    VIO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < d.n; ++i)
+        if (sync[(size_t)PH_SYNC_INTS * i + 192]) {
+            set_error(ctx, "cluster route: a hand-off wait timed out (workgroups not co-resident?)");
+            return VIO_EDEVICE;
+        }
+    return VIO_OK;
+}
+
 static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
     Packed& pk = d.pk;
+    if (int rc = check_cluster(ctx, d)) return rc;
     std::vector<double> out(pk.out_total);
     std::vector<uint8_t> u8(pk.N_total), bad(pk.L_total);
     std::vector<int32_t> si(SI_COUNT * d.n);
@@ -412,10 +456,6 @@ static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
 // single-kernel solver.  Within a route a window's result does not depend on the batch it is in.
 // vio_ctx_set_ba_route / VIO_BA_MONOLITHIC=1 / VIO_BA_PHASES=1 select a route explicitly (A/B runs,
 // tests); per-window phase profiling runs on ba_window_kernel.
-static bool env_flag(const char* name) {
-    const char* e = std::getenv(name);
-    return e && e[0] == '1';
-}
 static bool force_monolithic(const vio_ctx* ctx, const BaDevice& d) {
     static const bool mono = env_flag("VIO_BA_MONOLITHIC"), phases = env_flag("VIO_BA_PHASES");
     if (phases || ctx->ba_route == VIO_BA_ROUTE_PHASES) return false;
@@ -427,15 +467,16 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     if (timed) VIO_HIP(ctx, hipEventRecord(d.ev0, ctx->stream));
     bool any_pnp = false, any_other = false;
     for (const BaWin& w : d.pk.win) (w.is_pnp ? any_pnp : any_other) = true;
-    const bool phases = any_other && !force_monolithic(ctx, d);
-    d.P.route = phases ? 1 : 0;
+    const bool cluster = any_other && d.cluster_C > 0;
+    const bool phases = !cluster && any_other && !force_monolithic(ctx, d);
+    d.P.route = phases || cluster ? 1 : 0;
     // IMU candidate terms beside the back-substitution walk for small batches (a single window's serial
     // path is then shorter); in ph_solve for larger ones (ph_back keeps 4 waves per SIMD, no scratch)
     static const int imu_back_max = [] {
         const char* v = std::getenv("VIO_BA_IMU_BACK_MAX");  // experiment override
         return v ? std::atoi(v) : 8;
     }();
-    d.P.imu_in_back = d.n <= imu_back_max ? 1 : 0;
+    d.P.imu_in_back = cluster || d.n <= imu_back_max ? 1 : 0;  // cluster: the leader, beside the walks
     d.P.win_base = 0;
     // sub-batches of the phase route on their own streams (launch_ba_phases): large batches only
     static const int lanes_env = [] {
@@ -459,7 +500,23 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     }
     hipError_t e = hipSuccess;
     const char* what = "ba_window_kernel launch";
-    if (phases) {
+    if (cluster) {
+        what = "ph_cluster_kernel";
+        if (!d.reusable) {
+            e = launch_ba_cluster(d.P, d.n, d.cluster_C, ctx->stream);
+        } else if (!d.phase_graph) {
+            hipGraph_t g = nullptr;
+            e = hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal);
+            if (e == hipSuccess) {
+                hipError_t el = launch_ba_cluster(d.P, d.n, d.cluster_C, ctx->stream);
+                e = hipStreamEndCapture(ctx->stream, &g);
+                if (el != hipSuccess) e = el;
+            }
+            if (e == hipSuccess) e = hipGraphInstantiate(&d.phase_graph, g, nullptr, nullptr, 0);
+            if (g) (void)hipGraphDestroy(g);
+        }
+        if (e == hipSuccess && d.reusable) e = hipGraphLaunch(d.phase_graph, ctx->stream);
+    } else if (phases) {
         // ~70 launches per solve: a reusable batch captures them once into a graph (same arguments
         // every run) and replays it; a one-shot solve launches them directly
         e = ba_phases_prepare(d.pk.win.data(), d.n);
@@ -503,7 +560,7 @@ extern "C" {
 int vio_abi_version(void) { return VIO360_ABI_VERSION; }
 
 int vio_ctx_set_ba_route(vio_ctx* ctx, int route) {
-    if (!ctx || route < VIO_BA_ROUTE_AUTO || route > VIO_BA_ROUTE_SINGLE_KERNEL) return VIO_EINVAL;
+    if (!ctx || route < VIO_BA_ROUTE_AUTO || route > VIO_BA_ROUTE_CLUSTER) return VIO_EINVAL;
     ctx->ba_route = route;
     return VIO_OK;
 }
@@ -629,7 +686,7 @@ int vio_ba_batch_sync(vio_ba_batch* b) {
     if (!b) return VIO_EINVAL;
     VIO_DEVICE(b->ctx);
     VIO_HIP(b->ctx, hipStreamSynchronize(b->ctx->stream));
-    return VIO_OK;
+    return check_cluster(b->ctx, b->dev);
 }
 
 int vio_ba_batch_download(vio_ba_batch* b, vio_ba_output* outs) {
@@ -653,6 +710,17 @@ int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count) {
     *avg_ms = b->dev.ms_count ? b->dev.ms_sum / b->dev.ms_count : 0.0;
     b->dev.ms_sum = 0.0;
     b->dev.ms_count = 0;
+    return VIO_OK;
+}
+
+int vio_ba_batch_route(vio_ba_batch* b, int* route, int* workgroups_per_window) {
+    if (!b || !route) return VIO_EINVAL;
+    bool any_other = false;
+    for (const BaWin& w : b->dev.pk.win) any_other |= !w.is_pnp;
+    *route = any_other && b->dev.cluster_C > 0 ? VIO_BA_ROUTE_CLUSTER
+             : any_other && !force_monolithic(b->ctx, b->dev) ? VIO_BA_ROUTE_PHASES
+                                                                : VIO_BA_ROUTE_SINGLE_KERNEL;
+    if (workgroups_per_window) *workgroups_per_window = b->dev.cluster_C;
     return VIO_OK;
 }
 

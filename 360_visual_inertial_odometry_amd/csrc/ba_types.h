@@ -16,6 +16,7 @@ constexpr int VI_KMAX = 10;     // VIBA windows on the windowed path: K <= 10 (n
 constexpr int BA_NF_MAX = 96;    // reduced (Schur) system size bound: 6*15 poses or 54+30+6 (VIBA K=10)
 constexpr int BA_STAGE = 3392;   // doubles of LDS for the Schur k-panels (chunk depth derived per tile count)
 constexpr int BA_GCOL = 256;     // max k rows per Schur chunk
+constexpr int PH_SYNC_INTS = 512; // cluster route: ints of hand-off state per window (2 KB)
 
 // per-window descriptor (host-packed, read-only on device)
 struct BaWin {
@@ -72,13 +73,16 @@ struct BaPools {
     int win_base;                // phase route: first window of a launch (sub-batches on their own streams)
     int imu_in_back;             // phase route: the IMU candidate terms in an extra workgroup of the
                                  // back-substitution grid (small batches) instead of at the end of ph_solve
+    int* csync;                  // cluster route: per-window hand-off counters / flags / records
+                                 // [n][PH_SYNC_INTS], zeroed before every launch (ba_phases.inc)
 };
 // BaWin / BaPools cross translation units (ba_host.cpp packs them, ba_kernel.hip reads them): pinned
 // here in every TU that includes this header, and cross-checked at run time (ba_layout_sig).
 static_assert(sizeof(BaWin) == 448 && offsetof(BaWin, gravity) == 304 && offsetof(BaWin, o_ws) == 424 &&
               offsetof(BaWin, o_tr) == 440, "BaWin layout changed: update the pinned offsets");
-static_assert(sizeof(BaPools) == 208 && offsetof(BaPools, prof) == 184 && offsetof(BaPools, route) == 192 &&
-              offsetof(BaPools, imu_in_back) == 200, "BaPools layout changed: update the pinned offsets");
+static_assert(sizeof(BaPools) == 216 && offsetof(BaPools, prof) == 184 && offsetof(BaPools, route) == 192 &&
+              offsetof(BaPools, imu_in_back) == 200 && offsetof(BaPools, csync) == 208,
+              "BaPools layout changed: update the pinned offsets");
 constexpr uint64_t ba_layout_sig() {
     return (uint64_t)sizeof(BaWin) << 48 | (uint64_t)offsetof(BaWin, o_ws) << 32 |
            (uint64_t)sizeof(BaPools) << 16 | (uint64_t)offsetof(BaPools, imu_in_back);

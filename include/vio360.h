@@ -62,13 +62,18 @@ int vio_abi_version(void);
  * here and by vio_ctx_create instead of faulting a kernel); needs no GPU */
 int vio_layout_check(void);
 
-/* Window-BA execution route of this context's later solves / batches (both routes give the same
-   results to roundoff; within a route results do not depend on the batch):
-   AUTO (default) = phase kernels for LocalBA / BA / VIBA windows, single kernel for PnP windows;
-   PHASES / SINGLE_KERNEL force one route for every non-PnP window (PnP always runs single-kernel). */
+/* Window-BA execution route of this context's later solves / batches (the routes give the same
+   results to roundoff, each with its own fixed summation order; within a route results do not depend
+   on the batch):
+   AUTO (default) = the cluster route for batches of up to 32 LocalBA / BA / VIBA windows (when the
+   device can hold every workgroup of the batch at once), the phase kernels for larger batches; PnP
+   windows always run single-kernel.
+   PHASES / SINGLE_KERNEL / CLUSTER force one route for every non-PnP window (CLUSTER falls back to the
+   phase kernels when the batch does not fit the device at once). */
 #define VIO_BA_ROUTE_AUTO 0
 #define VIO_BA_ROUTE_PHASES 1
 #define VIO_BA_ROUTE_SINGLE_KERNEL 2
+#define VIO_BA_ROUTE_CLUSTER 3
 int vio_ctx_set_ba_route(vio_ctx* ctx, int route);
 
 /* ----------------------------------------------------------------------------------------- */
@@ -227,6 +232,9 @@ int vio_ba_batch_set_preint(vio_ba_batch* b, const vio_preint* src, int count, i
 int vio_ba_batch_download(vio_ba_batch* b, vio_ba_output* outs);
 /* average device time (ms) of the solver kernel over the runs since the last reset */
 int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count);
+/* the route the batch's LocalBA / BA / VIBA windows run on (VIO_BA_ROUTE_PHASES / _SINGLE_KERNEL /
+   _CLUSTER; fixed at vio_ba_batch_create), and for the cluster route the workgroups per window */
+int vio_ba_batch_route(vio_ba_batch* b, int* route, int* workgroups_per_window);
 void vio_ba_batch_destroy(vio_ba_batch* b);
 /* diagnostics: per-phase shader-clock accounting of the solver kernel (sum over windows of the
    last run; VIO_BA_PROF_SLOTS slots, named in the Python mirror's BaBatch.PHASES) */

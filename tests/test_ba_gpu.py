@@ -132,13 +132,15 @@ def test_lm_trace_matches_oracle(vio, gpu_ctx, all_cases, tc):
     p = vio.BaProblem(w, variant=var, **kw)
     o = oracle_lib.ba_solve(vio, p)
     cloud = oracle_cloud(vio, w, var, **kw)
-    solo = gpu_ctx.ba_solve([p])[0]            # phase route (default)
-    gpu_ctx.set_ba_route(gpu_ctx.ROUTE_SINGLE_KERNEL)
+    solo = gpu_ctx.ba_solve([p])[0]            # cluster route (default for small batches)
     try:
+        gpu_ctx.set_ba_route(gpu_ctx.ROUTE_SINGLE_KERNEL)
         mono = gpu_ctx.ba_solve([p])[0]        # single-kernel route
+        gpu_ctx.set_ba_route(gpu_ctx.ROUTE_PHASES)
+        phases = gpu_ctx.ba_solve([p])[0]      # phase kernels (the route of large batches)
     finally:
         gpu_ctx.set_ba_route(gpu_ctx.ROUTE_AUTO)
-    for g in (solo, mono):
+    for g in (solo, mono, phases):
         assert len(g["trace"]["cost"]) == g["iterations"]
         compare_traces(o, g, cloud, fixed, min(min_prefix, o["iterations"]))
 
@@ -307,6 +309,45 @@ def test_routes_agree(vio, synth, gpu_ctx):
         assert np.abs(big[i]["T_wb"] - solo["T_wb"]).max() <= 1e-7
         assert np.abs(big[i]["lm_xyz"] - solo["lm_xyz"]).max() <= 1e-6
         assert abs(big[i]["final_cost"] - solo["final_cost"]) <= 1e-8 * solo["final_cost"]
+
+
+def test_cluster_route_bitwise_across_member_counts(vio, synth, gpu_ctx):
+    """The cluster route's results do not depend on how many workgroups a window gets: a window solved
+    alone (one member workgroup per landmark chunk) and inside a 32-window batch (several chunks per
+    member) agree bit for bit (chunk partials and Schur groups are per chunk, summed in chunk order by
+    the leader), and a second run of the batch reproduces them."""
+    ws = [synth.config3(synth.SEED + i) for i in range(32)]
+    probs = [vio.BaProblem(w, variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1) for w in ws]
+    big = gpu_ctx.ba_solve(probs)
+    big2 = gpu_ctx.ba_solve(probs)
+    for i in (0, 13, 31):
+        solo = gpu_ctx.ba_solve([probs[i]])[0]
+        for key in ("T_wb", "lm_xyz", "obs_chi2", "vel", "bg", "ba"):
+            assert np.array_equal(big[i][key], solo[key]), (i, key)
+            assert np.array_equal(big[i][key], big2[i][key]), (i, key)
+        assert big[i]["final_cost"] == solo["final_cost"] and big[i]["iterations"] == solo["iterations"]
+
+
+def test_cluster_and_phase_routes_agree(vio, synth, gpu_ctx):
+    """The cluster route (one landmark chunk per Schur group) and the phase kernels (5 chunks per group
+    for small batches) sum the Schur partials in different groupings: equal to roundoff on fixed
+    10-iteration solves, step decisions identical."""
+    ws = [synth.config3(synth.SEED + i) for i in range(4)] + [synth.config2()]
+    probs = [vio.BaProblem(w, variant=vio.VIO_BA_VI if i < 4 else vio.VIO_BA_LOCAL, max_iterations=10,
+                           fixed_iterations=1) for i, w in enumerate(ws)]
+    cl = gpu_ctx.ba_solve(probs)
+    gpu_ctx.set_ba_route(gpu_ctx.ROUTE_PHASES)
+    try:
+        ph = gpu_ctx.ba_solve(probs)
+    finally:
+        gpu_ctx.set_ba_route(gpu_ctx.ROUTE_AUTO)
+    for a, b in zip(cl, ph):
+        assert a["iterations"] == b["iterations"]
+        assert (a["num_successful_steps"], a["num_unsuccessful_steps"]) == (b["num_successful_steps"],
+                                                                           b["num_unsuccessful_steps"])
+        assert np.abs(a["T_wb"] - b["T_wb"]).max() <= 1e-7
+        assert np.abs(a["lm_xyz"] - b["lm_xyz"]).max() <= 1e-6
+        assert abs(a["final_cost"] - b["final_cost"]) <= 1e-8 * b["final_cost"]
 
 
 def test_mixed_variant_batch(vio, gpu_ctx, all_cases):
