@@ -20,6 +20,7 @@
 #include <float.h>
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 
 #include "ba_factor_dev.h"
@@ -736,17 +737,17 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 __device__ __forceinline__ void st_sc1(double* p, double v) {
     __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// bounded spins: each poll is an sc1 load round trip (~1-2 us under load), so 2^19 polls give up after
-// about a second, orders of magnitude above any legitimate wait (a whole LM iteration is ~6 ms); a
-// timed-out wait sets the solve's timeout word, which the host reports as a device error
-constexpr int kSpinMax = 1 << 19;
+// bounded spins (chol_dev.h wait_expired: 2 s of wall clock, orders of magnitude above any legitimate
+// wait -- a whole LM iteration is ~5 ms); a timed-out wait sets the solve's timeout word, which the host
+// reports as a device error
 __device__ __forceinline__ bool flag_wait(int* f) {
     // bounded spin: a producer that never arrives ends the wait instead of hanging the GPU
-    for (int it = 0; it < kSpinMax; ++it) {
+    const unsigned long long t0 = wait_clock();
+    for (;;) {
         if (__hip_atomic_load((gint*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
+        if (wait_expired(t0)) return false;
         __builtin_amdgcn_s_sleep(1);
     }
-    return false;
 }
 // triangular-solve hand-off without a flag: the consumer polls the 64 values themselves (set to this
 // NaN pattern before the solve; each 8-B value is stored whole), one round trip instead of flag +
@@ -754,15 +755,16 @@ __device__ __forceinline__ bool flag_wait(int* f) {
 constexpr unsigned long long kUnsetBits = ~0ull;
 __device__ __forceinline__ bool poll_block(const double* p, double& v) {
     bool pend = true;
-    for (int it = 0; it < kSpinMax; ++it) {
+    const unsigned long long t0 = wait_clock();
+    for (;;) {
         if (pend) {
             v = ld_sc1(p);
             pend = (unsigned long long)__double_as_longlong(v) == kUnsetBits;
         }
         if (__ballot(pend) == 0ull) return true;
+        if (wait_expired(t0)) return false;
         __builtin_amdgcn_s_sleep(1);
     }
-    return false;
 }
 __device__ __forceinline__ void flag_publish(int* f) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1300,7 +1302,13 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
     int* tmo = A.flags ? A.flags + FLAG_STRIDE * 2 * (size_t)nblk : nullptr;  // timeout word of the Cholesky + solves
     if (tmo) {
-        const hipError_t e0 = hipMemsetAsync(tmo, 0, sizeof(int), s);
+        // (VIO_GBA_TEST_TIMEOUT=1: the word starts set, as after a timed-out wait -- the host's device-error
+        // path, exercised by tests/test_ba_gpu.py::test_wait_timeouts_report_device_errors)
+        static std::atomic<int> test_tmo{[] {
+            const char* v = std::getenv("VIO_GBA_TEST_TIMEOUT");
+            return v && v[0] == '1' ? 1 : 0;
+        }()};  // one-shot: the first factorisation of the process only
+        const hipError_t e0 = hipMemsetAsync(tmo, test_tmo.exchange(0) ? 1 : 0, sizeof(int), s);
         if (e0 != hipSuccess) return e0;
     }
     hipStream_t r = A.side;

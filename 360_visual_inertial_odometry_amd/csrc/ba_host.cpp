@@ -477,6 +477,11 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
         return v ? std::atoi(v) : 8;
     }();
     d.P.imu_in_back = cluster || d.n <= imu_back_max ? 1 : 0;  // cluster: the leader, beside the walks
+    static const int chol_variant = [] {
+        const char* v = std::getenv("VIO_BA_CHOL");  // experiment override: 0 chol6_solve2, 1 chol_mw_solve2
+        return v ? std::atoi(v) : 0;
+    }();
+    d.P.chol_variant = chol_variant;
     d.P.win_base = 0;
     // sub-batches of the phase route on their own streams (launch_ba_phases): large batches only
     static const int lanes_env = [] {

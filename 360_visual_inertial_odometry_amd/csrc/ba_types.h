@@ -73,6 +73,7 @@ struct BaPools {
     int win_base;                // phase route: first window of a launch (sub-batches on their own streams)
     int imu_in_back;             // phase route: the IMU candidate terms in an extra workgroup of the
                                  // back-substitution grid (small batches) instead of at the end of ph_solve
+    int chol_variant;            // window reduced solve: 0 chol6_solve2, 1 chol_mw_solve2 (chol_dev.h)
     int* csync;                  // cluster route: per-window hand-off counters / flags / records
                                  // [n][PH_SYNC_INTS], zeroed before every launch (ba_phases.inc)
 };
@@ -81,7 +82,8 @@ struct BaPools {
 static_assert(sizeof(BaWin) == 448 && offsetof(BaWin, gravity) == 304 && offsetof(BaWin, o_ws) == 424 &&
               offsetof(BaWin, o_tr) == 440, "BaWin layout changed: update the pinned offsets");
 static_assert(sizeof(BaPools) == 216 && offsetof(BaPools, prof) == 184 && offsetof(BaPools, route) == 192 &&
-              offsetof(BaPools, imu_in_back) == 200 && offsetof(BaPools, csync) == 208,
+              offsetof(BaPools, imu_in_back) == 200 && offsetof(BaPools, chol_variant) == 204 &&
+              offsetof(BaPools, csync) == 208,
               "BaPools layout changed: update the pinned offsets");
 constexpr uint64_t ba_layout_sig() {
     return (uint64_t)sizeof(BaWin) << 48 | (uint64_t)offsetof(BaWin, o_ws) << 32 |

@@ -22,6 +22,14 @@ __device__ __forceinline__ double rsq_nr(double p) {
     return r;
 }
 
+// Wall-clock bound of an inter-workgroup wait: s_memrealtime counts a constant 100 MHz clock, so the
+// bound does not depend on how long one poll takes (an sc1 load round trip is 0.1-2 us depending on
+// placement and load).  A wait that has not completed after kWaitTicks (2 s: a whole global-BA LM
+// iteration is ~5 ms, a window solve ~1 ms) gives up, and the caller reports a device error.
+constexpr unsigned long long kWaitTicks = 200000000ull;
+__device__ __forceinline__ unsigned long long wait_clock() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ bool wait_expired(unsigned long long t0) { return wait_clock() - t0 > kWaitTicks; }
+
 // LDS writes of this wave visible to its own later reads (no workgroup barrier)
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -337,6 +345,114 @@ __device__ bool chol6_solve2(double* A0, int n0, double* A1, int n1, int lda, do
         }
         __syncthreads();
     }
+    return true;
+}
+
+// One system of chol_mw_solve2 on waves [w0, w0 + NW) of the workgroup: lane i holds row i (i < n;
+// lane n holds the right-hand side) restricted to the wave's CB columns [CB v, CB v + CB), v = wave - w0.
+// Pivot j: its owner wave (j / CB) factors it (rsq + Newton), writes L[:, j] to colbuf and updates its
+// own next column first (look-ahead: the next pivot's chain overlaps the other waves' bulk updates);
+// after the workgroup barrier every wave applies L[:, j] to its remaining columns (A[i][k] -= L[i][j]
+// L[k][j], m ascending per element: the textbook left-to-right sum of every L[i][k]).  nsteps (>= n,
+// uniform) is the barrier count both systems share.  L goes back over A (row stride lda; the rhs row
+// becomes y = L^-1 b), 1 / L[j][j] to dinv.  Returns nonzero on a non-positive pivot (owner waves).
+template <int NW, int CB, int NSMAX>
+__device__ __forceinline__ int chol_mw_factor(double* A, int lda, int n, int nsteps, int w0, double* colbuf,
+                                              double* dinv) {
+    const int t = (int)threadIdx.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6) - w0;
+    const bool part = wv >= 0 && wv < NW;
+    double d[CB];
+    const int cbase = CB * wv;
+    if (part) {
+        const double* arow = A + (lane <= n ? lane : n) * lda;
+#pragma unroll
+        for (int q = 0; q < CB; ++q) {
+            const int k = cbase + q;
+            const double v = k < n ? arow[k] : 0.0;
+            d[q] = lane < n ? (k <= lane ? v : 0.0) : (lane == n ? v : 0.0);
+        }
+    }
+    int bad = 0;
+    double piv_next = 0.0;
+#pragma unroll
+    for (int j = 0; j < NSMAX; ++j) {
+        if (j >= nsteps) break;  // uniform: both systems stop together
+        const bool act = j < n;
+        const int o = j / CB, q = j % CB;
+        double* cb = colbuf + (j & 1) * 64;
+        if (act && part && wv == o) {
+            const double piv = q == 0 ? readlane_d(d[0], j) : piv_next;
+            bad |= !(piv > 0.0);
+            const double r = rsq_nr(piv);
+            double c = lane == j ? piv * r : d[q] * r;
+            if (lane < j) c = 0.0;
+            d[q] = c;
+            cb[lane] = c;
+            if (lane == j) dinv[j] = r;
+            if (q + 1 < CB && j + 1 < n) {
+                const double c1 = readlane_d(c, j + 1);
+                d[q + 1] -= c * c1;
+                piv_next = readlane_d(d[q + 1], j + 1);
+            }
+        }
+        __syncthreads();
+        if (act && part) {
+            const double ci = cb[lane];
+#pragma unroll
+            for (int qq = 0; qq < CB; ++qq) {
+                const int k = cbase + qq;
+                const double lk = cb[k < 63 ? k : 63];
+                if (k > j && !(wv == o && qq == q + 1)) d[qq] -= ci * lk;
+            }
+        }
+    }
+    if (part && lane <= n) {
+        double* w = A + lane * lda;
+#pragma unroll
+        for (int q = 0; q < CB; ++q) {
+            const int k = cbase + q;
+            if (k < n) w[k] = (k <= lane || lane == n) ? d[q] : 0.0;
+        }
+    }
+    return bad;
+}
+// L^T x = y by one wave (lane = column m), column-oriented from the last row: x may alias nothing in A
+template <int NMAX>
+__device__ __forceinline__ void chol_mw_backward(const double* A, int lda, int n, const double* dinv, double* x,
+                                                 int lane) {
+    double tt = lane < n ? A[n * lda + lane] : 0.0;
+    const double dv = lane < n ? dinv[lane] : 0.0;
+#pragma unroll
+    for (int m = NMAX - 1; m >= 0; --m) {
+        if (m < n) {
+            const double e = lane < m ? A[m * lda + lane] : 0.0;
+            const double xm = readlane_d(tt * dv, m);
+            tt = lane == m ? xm : tt - e * xm;
+        }
+    }
+    if (lane < n) x[lane] = tt;
+}
+// The window's block-diagonal reduced system: the pose block (n0 <= 54) over waves 0-1 and the velocity /
+// bias block (n1 <= 54) over waves 2-3, 27 columns per wave, one code path (the per-wave system chosen by
+// pointer), both systems sharing the per-pivot barriers (see chol_mw_factor); right-hand sides as row
+// n_s of each block.  Returns false (uniformly) on a non-positive pivot.  colbuf: 256 doubles, dinv0 /
+// dinv1: n_s doubles, flag: one LDS int.
+__device__ inline bool chol_mw_solve2(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1,
+                                      double* colbuf, double* dinv0, double* dinv1, int* flag) {
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int nsteps = n0 > n1 ? n0 : n1;
+    if (threadIdx.x == 0) *flag = 0;
+    __syncthreads();
+    const bool s1 = wid >= 2;
+    const int bad = chol_mw_factor<2, 27, 54>(s1 ? A1 : A0, lda, s1 ? n1 : n0, nsteps, s1 ? 2 : 0,
+                                             colbuf + (s1 ? 128 : 0), s1 ? dinv1 : dinv0);
+    if (bad) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+    if (*flag) return false;
+    if (wid == 0 || (wid == 2 && n1 > 0))
+        chol_mw_backward<54>(s1 ? A1 : A0, lda, s1 ? n1 : n0, s1 ? dinv1 : dinv0, s1 ? x1 : x0, lane);
+    __syncthreads();
     return true;
 }
 
