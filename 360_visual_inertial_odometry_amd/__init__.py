@@ -69,7 +69,8 @@ def lib():
     L.vio_ba_batch_sync.argtypes = [C.c_void_p]
     L.vio_ba_batch_download.argtypes = [C.c_void_p, C.POINTER(abi.VioBaOutput)]
     L.vio_ba_batch_kernel_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int)]
-    L.vio_ba_batch_route.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    if hasattr(L, "vio_ba_batch_route") or "VIO360_LIB" not in os.environ:  # (A/B runs may load older builds)
+        L.vio_ba_batch_route.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.vio_ba_batch_destroy.argtypes = [C.c_void_p]
     L.vio_ba_batch_profile.argtypes = [C.c_void_p, C.c_int]
     L.vio_ba_batch_phase_cycles.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]

@@ -191,7 +191,7 @@ __device__ __forceinline__ int chol6_diag(double (&d)[6], int lane, double& my_i
     return bad;
 }
 template <int NT>
-__device__ bool chol6_solve2(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1, double* inv0,
+__device__ __forceinline__ bool chol6_solve2(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1, double* inv0,
                              double* inv1, int* flag) {
     const int t = (int)threadIdx.x, wid = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
     const int nb0 = n0 / 6, nb1 = n1 / 6, nb = nb0 > nb1 ? nb0 : nb1;
@@ -438,7 +438,7 @@ __device__ __forceinline__ void chol_mw_backward(const double* A, int lda, int n
 // pointer), both systems sharing the per-pivot barriers (see chol_mw_factor); right-hand sides as row
 // n_s of each block.  Returns false (uniformly) on a non-positive pivot.  colbuf: 256 doubles, dinv0 /
 // dinv1: n_s doubles, flag: one LDS int.
-__device__ inline bool chol_mw_solve2(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1,
+__device__ __forceinline__ bool chol_mw_solve2(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1,
                                       double* colbuf, double* dinv0, double* dinv1, int* flag) {
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int nsteps = n0 > n1 ? n0 : n1;

@@ -10,3 +10,10 @@ rc=$?; cat gpurun_out/route_ab.log; [ $rc -eq 0 ] || exit $rc
 VIO_BA_CHOL=1 timeout -k 10 240 python3 tools/ba_route_ab.py 1 32 256 > gpurun_out/route_ab_mw.log 2>&1
 rc=$?; cat gpurun_out/route_ab_mw.log; [ $rc -eq 0 ] || exit $rc
 bash tools/gpu_round.sh ${1:-r4a}
+rc=$?; [ $rc -eq 0 ] || exit $rc
+# global BA: the 76.8 KB Cholesky LDS layout (two fused-step workgroups per CU) against HEAD
+for rep in 1 2; do
+  for lib in 360_visual_inertial_odometry_amd/libvio360.so ab/lib_lds768.so; do
+    echo "$(basename $lib) $(VIO360_LIB=$lib timeout -k 10 200 python3 tools/gba_time.py 5 3 2>&1 | grep -v amdgpu.ids | tail -1)" || exit 1
+  done
+done

@@ -1,4 +1,5 @@
-"""Diagnostic: ph_solve_kernel shader-clock breakdown (phase route, VIO_BA_PHASES=1) for W windows."""
+"""Diagnostic: per-phase shader-clock breakdown of the window solver for W windows (default route for the
+batch size; VIO_BA_PHASES=1 forces the phase kernels).  Cluster-route slots: 8-12, 23."""
 import importlib
 import os
 import sys
@@ -7,7 +8,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402,F401
 
-os.environ["VIO_BA_PHASES"] = "1"
 vio = importlib.import_module("360_visual_inertial_odometry_amd")
 synth = importlib.import_module("360_visual_inertial_odometry_amd.synth")
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 1
@@ -15,6 +15,7 @@ ctx = vio.Context(0)
 probs = [vio.BaProblem(synth.config3(synth.SEED + i), variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1)
          for i in range(W)]
 b = vio.BaBatch(ctx, probs)
+print("route", b.route())
 b.profile(True)
 b.run(); b.sync()
 import ctypes as C
@@ -22,8 +23,9 @@ out = (C.c_ulonglong * 24)()
 ctx.check(vio.lib().vio_ba_batch_phase_cycles(b.h, out), "phase_cycles")
 names = {0: "prep U partials", 1: "prep imu", 2: "prep cost partials", 3: "prep imu normal eq", 4: "prep gradient",
          5: "prep finalize+diag", 6: "schur g0 landmark blocks", 15: "schur g0 zero panel", 7: "schur g0 fills",
-         13: "schur g0 mfma phases", 14: "schur g0 combine+write", 8: "chol diag tiles", 9: "chol panels", 10: "chol trailing", 11: "chol forward",
-         12: "chol backward",
+         13: "schur g0 mfma phases", 14: "schur g0 combine+write", 8: "chol diag / cl leader wait A", 9: "chol panels / cl leader wait B", 10: "chol trailing / cl leader imu",
+         11: "chol forward / cl member1 wait R",
+         12: "chol backward / cl member1 wait F", 23: "cl member1 walk",
          16: "solve assembly+partials", 17: "solve cholesky+solves", 18: "solve candidates+posecache",
          19: "solve imu model+cand", 20: "solve reductions", 21: "ctrl lane", 22: "ctrl copies"}
 tot = sum(out[i] for i in names)
