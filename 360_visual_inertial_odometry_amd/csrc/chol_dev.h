@@ -190,6 +190,35 @@ __device__ __forceinline__ int chol6_diag(double (&d)[6], int lane, double& my_i
     }
     return bad;
 }
+// L^T x = y by one wave, column-oriented (n <= 128, lane k holds t_k and t_{k+64}): for m from the
+// last row, x_m = t_m / L[m][m] (inv = 1 / diagonal), then every t_k (k < m) takes its term L[m][k] x_m
+// at once -- one broadcast and one FMA per step on the chain (the block version ran a 6-long dependent
+// chain per block on one thread plus two workgroup barriers per block).  y is row n of A (row stride
+// lda; the forward substitution rode along as that row); x may not alias A.
+__device__ __forceinline__ void chol_backward_wave(const double* A, int lda, int n, const double* inv, double* x,
+                                                   int lane) {
+    const double* y = A + (size_t)n * lda;
+    double t0 = lane < n ? y[lane] : 0.0, t1 = lane + 64 < n ? y[lane + 64] : 0.0;
+    double a0 = n > 0 && lane < n - 1 ? A[(size_t)(n - 1) * lda + lane] : 0.0;  // row m, loaded one step ahead
+    double a1 = n > 0 && lane + 64 < n - 1 ? A[(size_t)(n - 1) * lda + lane + 64] : 0.0;
+    for (int m = n - 1; m >= 0; --m) {
+        const double r0 = a0, r1 = a1;
+        if (m > 0) {  // the next row's entries, in flight during this step's chain
+            a0 = lane < m - 1 ? A[(size_t)(m - 1) * lda + lane] : 0.0;
+            a1 = lane + 64 < m - 1 ? A[(size_t)(m - 1) * lda + lane + 64] : 0.0;
+        }
+        const double tm = m < 64 ? readlane_d(t0, m) : readlane_d(t1, m - 64);
+        const double xm = tm * inv[m];
+        if (m < 64) t0 = lane == m ? xm : (lane < m ? t0 - r0 * xm : t0);
+        else {
+            t0 = t0 - r0 * xm;
+            t1 = lane + 64 == m ? xm : (lane + 64 < m ? t1 - r1 * xm : t1);
+        }
+    }
+    if (lane < n) x[lane] = t0;
+    if (lane + 64 < n) x[lane + 64] = t1;
+}
+
 template <int NT>
 __device__ __forceinline__ bool chol6_solve2(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1, double* inv0,
                              double* inv1, int* flag) {
@@ -309,42 +338,10 @@ __device__ __forceinline__ bool chol6_solve2(double* A0, int n0, double* A1, int
         __syncthreads();
         if (*flag) return false;
     }
-    // backward substitution, block by block from the last: y (row n_s) in place, x_s out
-    for (int j = nb - 1; j >= 0; --j) {
-        const int c0 = 6 * j;
-        if (t < 2 && j < (t == 0 ? nb0 : nb1)) {  // x_j = L_jj^-T y_j: one thread per system
-            double* A = t == 0 ? A0 : A1;
-            const double* inv = t == 0 ? inv0 : inv1;
-            double* x = t == 0 ? x0 : x1;
-            const double* y = A + (t == 0 ? n0 : n1) * lda;
-            double xv[6];
-#pragma unroll
-            for (int c = 5; c >= 0; --c) {
-                double v = y[c0 + c];
-#pragma unroll
-                for (int m = c + 1; m < 6; ++m) v -= A[(c0 + m) * lda + c0 + c] * xv[m];
-                xv[c] = v * inv[c0 + c];
-            }
-#pragma unroll
-            for (int c = 0; c < 6; ++c) x[c0 + c] = xv[c];
-        }
-        __syncthreads();
-        if (j == 0) break;
-        // y_k -= sum_m L[6j+m][k] x[6j+m] for k < 6j, both systems
-        const int m0 = j < nb0 ? c0 : 0, m1 = j < nb1 ? c0 : 0;
-        for (int e = t; e < m0 + m1; e += NT) {
-            const bool s1 = e >= m0;
-            double* A = s1 ? A1 : A0;
-            const double* x = s1 ? x1 : x0;
-            const int k = s1 ? e - m0 : e;
-            double* y = A + (s1 ? n1 : n0) * lda;
-            double v = y[k];
-#pragma unroll
-            for (int m = 0; m < 6; ++m) v -= A[(c0 + m) * lda + k] * x[c0 + m];
-            y[k] = v;
-        }
-        __syncthreads();
-    }
+    // backward substitution L^T x = y (y = row n_s): one wave per system, column-oriented (chol_backward_wave)
+    if (wid == 0 && nb0 > 0) chol_backward_wave(A0, lda, n0, inv0, x0, lane);
+    else if (wid == 1 && nb1 > 0) chol_backward_wave(A1, lda, n1, inv1, x1, lane);
+    __syncthreads();
     return true;
 }
 
