@@ -219,6 +219,45 @@ __device__ __forceinline__ void chol_backward_wave(const double* A, int lda, int
     if (lane + 64 < n) x[lane + 64] = t1;
 }
 
+// The 6x6 diagonal block at B (row stride lda, lower part current) factored by one whole wave, every lane
+// holding the whole block in registers (no cross-lane broadcast on the pivot chain): lane u < 6 writes
+// row u of L back and 1 / L[u][u] to inv[u].  Element by element the operations of chol6_diag (L[i][k]
+// -= L[i][c] L[k][c], c ascending; L[c][c] = p rsq(p)): the same bits.  Returns nonzero (every lane) on a
+// non-positive pivot.
+__device__ __forceinline__ int chol6_diag_wave(double* B, int lda, double* inv, int lane) {
+    double b[21];  // b[i (i + 1) / 2 + k] = entry (i, k), k <= i
+#pragma unroll
+    for (int i = 0, q = 0; i < 6; ++i)
+#pragma unroll
+        for (int k = 0; k <= i; ++k, ++q) b[q] = B[i * lda + k];
+    int bad = 0;
+    double r[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        const double piv = b[c * (c + 1) / 2 + c];
+        bad |= !(piv > 0.0);
+        r[c] = rsq_nr(piv);
+        b[c * (c + 1) / 2 + c] = piv * r[c];
+#pragma unroll
+        for (int i = c + 1; i < 6; ++i) b[i * (i + 1) / 2 + c] *= r[c];
+#pragma unroll
+        for (int i = c + 1; i < 6; ++i)
+#pragma unroll
+            for (int k = c + 1; k <= i; ++k) b[i * (i + 1) / 2 + k] -= b[i * (i + 1) / 2 + c] * b[k * (k + 1) / 2 + c];
+    }
+    if (lane < 6) {
+        double* w = B + lane * lda;
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+            if (lane == u) {
+#pragma unroll
+                for (int k = 0; k <= u; ++k) w[k] = b[u * (u + 1) / 2 + k];
+                inv[u] = r[u];
+            }
+    }
+    return bad;
+}
+
 template <int NT>
 __device__ __forceinline__ bool chol6_solve2(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1, double* inv0,
                              double* inv1, int* flag) {
@@ -227,22 +266,10 @@ __device__ __forceinline__ bool chol6_solve2(double* A0, int n0, double* A1, int
     // waves not factoring a diagonal block take the trailing-update tasks
     const int wfirst = nb1 > 0 ? 2 : 1, nworker = NT - 64 * wfirst, tw = t - 64 * wfirst;
     if (t == 0) *flag = 0;
-    // diagonal block 0 of each system
-    if (wid < 2 && lane < 6 && (wid == 0 ? nb0 : nb1) > 0) {
-        double* A = wid == 0 ? A0 : A1;
-        double* inv = wid == 0 ? inv0 : inv1;
-        double d[6];
-        const double* row = A + lane * lda;
-#pragma unroll
-        for (int m = 0; m < 6; ++m) d[m] = m <= lane ? row[m] : 0.0;
-        double my_inv = 0.0;
-        const int bad = chol6_diag(d, lane, my_inv);
-        double* w = A + lane * lda;
-#pragma unroll
-        for (int m = 0; m < 6; ++m)
-            if (m <= lane) w[m] = d[m];
-        inv[lane] = my_inv;
-        if (bad) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // diagonal block 0 of each system (its wave, every lane)
+    if (wid < 2 && (wid == 0 ? nb0 : nb1) > 0) {
+        const int bad = chol6_diag_wave(wid == 0 ? A0 : A1, lda, wid == 0 ? inv0 : inv1, lane);
+        if (bad && lane == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
     if (*flag) return false;
@@ -283,29 +310,27 @@ __device__ __forceinline__ bool chol6_solve2(double* A0, int n0, double* A1, int
             // look-ahead: this wave's system's next diagonal block, updated and factored by lanes 0..5
             const bool s1 = wid == 1;
             const int R = s1 ? R1 : R0;
-            if (lane < 6 && R >= 7) {  // a next diagonal block exists (6 matrix rows + the rhs row)
+            if (R >= 7) {  // a next diagonal block exists (6 matrix rows + the rhs row)
                 double* A = s1 ? A1 : A0;
                 double* inv = s1 ? inv1 : inv0;
-                const double* li = A + (r0 + lane) * lda + c0;
-                double l[6], d[6];
+                if (lane < 6) {  // lane u: row u of the block, updated by panel j
+                    const double* li = A + (r0 + lane) * lda + c0;
+                    double l[6];
 #pragma unroll
-                for (int m = 0; m < 6; ++m) l[m] = li[m];
+                    for (int m = 0; m < 6; ++m) l[m] = li[m];
 #pragma unroll
-                for (int kk = 0; kk < 6; ++kk) {
-                    const double* lk = A + (r0 + kk) * lda + c0;
-                    double a = kk <= lane ? A[(r0 + lane) * lda + r0 + kk] : 0.0;
+                    for (int kk = 0; kk < 6; ++kk) {
+                        if (kk > lane) continue;
+                        const double* lk = A + (r0 + kk) * lda + c0;
+                        double a = A[(r0 + lane) * lda + r0 + kk];
 #pragma unroll
-                    for (int m = 0; m < 6; ++m) a -= l[m] * lk[m];
-                    d[kk] = kk <= lane ? a : 0.0;
+                        for (int m = 0; m < 6; ++m) a -= l[m] * lk[m];
+                        A[(r0 + lane) * lda + r0 + kk] = a;
+                    }
                 }
-                double my_inv = 0.0;
-                const int bad = chol6_diag(d, lane, my_inv);
-                double* w = A + (r0 + lane) * lda + r0;
-#pragma unroll
-                for (int m = 0; m < 6; ++m)
-                    if (m <= lane) w[m] = d[m];
-                inv[r0 + lane] = my_inv;
-                if (bad) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                wave_lds_sync();
+                const int bad = chol6_diag_wave(A + r0 * lda + r0, lda, inv + r0, lane);
+                if (bad && lane == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         } else {
             const int S0 = R0 > 1 ? (R0 - 2) / 6 + 1 : 0, S1 = R1 > 1 ? (R1 - 2) / 6 + 1 : 0;
