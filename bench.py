@@ -817,8 +817,8 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK,
                 "traffic": ba_traffic(args),
-                "kernel": f"{head_route}-route step graph (ph_setup, ph_lin, ph_prep, ph_schur, ph_solve, ph_back, "
-                          "9 x [ph_ctrl, ph_prep || ph_schur, ph_solve, ph_back], ph_ctrl, ph_prep, ph_post)",
+                "kernel": f"{head_route}-route step graph (ph_setup, ph_lin, 10 x [ph_prep, ph_schur, ph_solve, "
+                          "ph_back], ph_prep, ph_post)",
                 "kernel_avg_ms": kms,
                 "kernel_launches": kcount,
                 "flops_per_launch": flops_iter * args.lm_iters,

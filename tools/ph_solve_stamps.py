@@ -26,8 +26,8 @@ names = {0: "prep U partials", 1: "prep imu", 2: "prep cost partials", 3: "prep 
          13: "schur g0 mfma phases", 14: "schur g0 combine+write", 8: "chol diag / cl leader wait A", 9: "chol panels / cl leader wait B", 10: "chol trailing / cl leader imu",
          11: "chol forward / cl member1 wait R",
          12: "chol backward / cl member1 wait F", 23: "cl member1 walk",
-         16: "solve assembly+partials", 17: "solve cholesky+solves", 18: "solve candidates+posecache",
-         19: "solve imu model+cand", 20: "solve reductions", 21: "ctrl lane", 22: "ctrl copies"}
+         16: "solve assembly+partials", 17: "solve cholesky+solves", 18: "solve small inputs+tables",
+         19: "solve pose tiles+partials", 20: "solve reductions", 21: "ctrl lane", 22: "ctrl copies"}
 tot = sum(out[i] for i in names)
 for i, n in names.items():
     print(f"W={W} {n:28s} cycles/window/iter {out[i] / W / 11:10.0f}  ({100 * out[i] / max(tot, 1):.1f}%)")
