@@ -542,7 +542,9 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
         }
         if (e == hipSuccess && d.reusable) e = hipGraphLaunch(d.phase_graph, ctx->stream);
     }
-    if (e == hipSuccess && (any_pnp || !phases)) e = launch_ba_windows(d.P, d.n, ctx->stream);
+    // the single-kernel solver: PnP windows, or every window when neither batched route runs (the cluster
+    // route has no window for it otherwise: an empty launch would cost the batch a kernel boundary)
+    if (e == hipSuccess && (any_pnp || (!phases && !cluster))) e = launch_ba_windows(d.P, d.n, ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, what);
     if (timed) {
         VIO_HIP(ctx, hipEventRecord(d.ev1, ctx->stream));

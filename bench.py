@@ -60,6 +60,24 @@ def ba_traffic(args):
     return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items() if n.startswith("ph_")) / steps
 
 
+def cfg2_traffic():
+    """PMC HBM bytes of one config-2 window solve (10 fixed LM iterations, one window, default route):
+    every window-BA kernel's bytes per launch x launches, per solve (tools/gpu_pmc_cfg2.sh over
+    tools/ba_batch_run.py -> profiles/r*_pmc_traffic_cfg2.json; a solve = one ph_cluster_kernel or
+    ph_setup_kernel launch)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_cfg2.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        k = json.load(f)["kernels"]
+    head = "ph_cluster_kernel" if "ph_cluster_kernel" in k else "ph_setup_kernel" if "ph_setup_kernel" in k else None
+    if head is None:
+        return None
+    return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items() if n.startswith("ph_")) / \
+        k[head]["dispatches"]
+
+
 def klt_traffic():
     """PMC HBM bytes of one ERP-KLT pipeline run: per-launch bytes x launches per run (lk_kernel runs once).
     Source: the newest tracker-only summary (tools/gpu_trk_pmc.sh -> profiles/r*_pmc_traffic_klt.json),
@@ -313,9 +331,10 @@ def config2_bench(vio, synth, ctx, lm_iters, cpu_seconds, want_cpu, windows=256)
         "batched": {"windows": windows, "window_iters_per_s": windows * lm_iters / wallm, "ms_per_step": wallm * 1e3},
         "iterations": res["iterations"],
         "roofline": {"bound": "mfma", "achieved": flops * lm_iters / (kms1 * 1e-3) / 1e12, "peak": FP64_PEAK / 1e12,
-                     "unit": "TFLOP/s", "frac": flops * lm_iters / (kms1 * 1e-3) / FP64_PEAK, "traffic": None,
+                     "unit": "TFLOP/s", "frac": flops * lm_iters / (kms1 * 1e-3) / FP64_PEAK, "traffic": cfg2_traffic(),
                      "flops_per_iteration": flops,
-                     "note": "one window: latency-bound (phase-route launch chain); SURVEY §8d flop convention"},
+                     "note": "one window: latency-bound (the window's serial LM chain); SURVEY §8d flop convention; "
+                             "traffic = PMC HBM bytes of one 10-iteration solve (committed profile)"},
         "cpu_baseline": None,
     }
     if want_cpu:
