@@ -642,7 +642,7 @@ class BaBatch:
         self.ctx.check(lib().vio_ba_batch_profile(self.h, int(enable)), "vio_ba_batch_profile")
 
     def phase_cycles(self):
-        out = (C.c_ulonglong * 24)()
+        out = (C.c_ulonglong * 32)()
         self.ctx.check(lib().vio_ba_batch_phase_cycles(self.h, out), "vio_ba_batch_phase_cycles")
         return {n: int(out[i]) for i, n in enumerate(self.PHASES)}
 

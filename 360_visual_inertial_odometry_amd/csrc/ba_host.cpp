@@ -296,7 +296,9 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
         const char* v = std::getenv("VIO_BA_CLUSTER_C");  // experiment override: members per window
         return v ? std::atoi(v) : 0;
     }();
-    d.cluster_C = cluster_wanted(ctx, d.n) ? ba_cluster_members(pk.win.data(), d.n, cmax) : 0;
+    // (an explicitly requested cluster route takes whatever members fit: no minimum per landmark chunk)
+    const int cm = cmax > 0 ? cmax : ctx->ba_route == VIO_BA_ROUTE_CLUSTER ? (1 << 20) : 0;
+    d.cluster_C = cluster_wanted(ctx, d.n) ? ba_cluster_members(pk.win.data(), d.n, cm) : 0;
     const int gs = d.cluster_C ? 1 : gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : 5;
     for (BaWin& w : pk.win) w.gs = gs;
     UP(pk.win, win, const BaWin*);
@@ -478,7 +480,7 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     }();
     d.P.imu_in_back = cluster || d.n <= imu_back_max ? 1 : 0;  // cluster: the leader, beside the walks
     static const int chol_variant = [] {
-        const char* v = std::getenv("VIO_BA_CHOL");  // experiment override: 0 chol6_solve2, 1 chol_mw_solve2
+        const char* v = std::getenv("VIO_BA_CHOL");  // experiment override: 0 chol6_solve2, 1 chol_mw_solve2, 2 chol_tile_solve2
         return v ? std::atoi(v) : 0;
     }();
     d.P.chol_variant = chol_variant;

@@ -73,7 +73,7 @@ struct BaPools {
     int win_base;                // phase route: first window of a launch (sub-batches on their own streams)
     int imu_in_back;             // phase route: the IMU candidate terms in an extra workgroup of the
                                  // back-substitution grid (small batches) instead of at the end of ph_solve
-    int chol_variant;            // window reduced solve: 0 chol6_solve2, 1 chol_mw_solve2 (chol_dev.h)
+    int chol_variant;            // window reduced solve: 0 chol6_solve2, 1 chol_mw_solve2, 2 chol_tile_solve2 (chol_dev.h)
     int* csync;                  // cluster route: per-window hand-off counters / flags / records
                                  // [n][PH_SYNC_INTS], zeroed before every launch (ba_phases.inc)
 };

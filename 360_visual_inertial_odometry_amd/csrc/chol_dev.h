@@ -5,6 +5,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 namespace vio360 {
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -367,6 +369,356 @@ __device__ __forceinline__ bool chol6_solve2(double* A0, int n0, double* A1, int
     if (wid == 0 && nb0 > 0) chol_backward_wave(A0, lda, n0, inv0, x0, lane);
     else if (wid == 1 && nb1 > 0) chol_backward_wave(A1, lda, n1, inv1, x1, lane);
     __syncthreads();
+    return true;
+}
+
+// Right-looking LLT with 6-column block steps of up to two independent SPD systems (the window's pose
+// block and velocity / bias block: the reference's IMU pose Jacobians are zero, Factors.cpp:1415-1475),
+// the trailing matrices held in REGISTERS as 16x16 MFMA tiles for the whole factorisation.  Roles (one
+// 256-thread workgroup): wave s < 2 factors system s; waves 2 and 3 own the lower tiles of both systems
+// (rows incl. the right-hand-side row n_s, padded to 16; tile g -> wave 2 + g % 2, slot g / 2).  Per
+// block column J (c0 = 6 J, the step index a compile-time constant on the tile waves):
+//   (a1) the tile waves apply panel J-1 to the tiles holding columns of block J (C -= P P^T on
+//        v_mfma_f64_16x16x4_f64, two k-steps, panel columns 6, 7 zero; panel rows < c0 zero, so
+//        finished entries never change) and write block column J (rows >= c0) to the column buffer E;
+//   (b)  after a barrier, wave s factors diagonal block J in registers (every lane the whole 6x6 block:
+//        no cross-lane broadcast on the pivot chain) and solves its panel row (lane l: row c0 + 6 + l, the
+//        rhs row included: the forward substitution rides along) into the panel buffer of parity J & 1,
+//        L into A_s, 1 / L[c][c] into dv;  meanwhile
+//   (a2) the tile waves apply panel J-1 (the other buffer) to their remaining tiles and invert the
+//        previous diagonal block (L_{J-1}^-1 for the blocked backward substitution, off-diagonal entries
+//        into the unused upper triangle of A_s);
+// then a barrier.  LDS traffic without divergent branches: masked-off lanes load clamped rows and store
+// to trash rows.  The backward substitution L^T x = y runs per 6-block with the inverted diagonal blocks.
+// Each L entry is the textbook value up to the summation order of the MFMA update.  scr:
+// chol_tile_scratch_doubles() of LDS (16-B aligned).  Returns false (uniformly) on a non-positive pivot.
+// Requires n_s % 6 == 0, n_s + 1 <= 64 (T_s <= 4 tile rows).
+using cd4 = __attribute__((ext_vector_type(4))) double;
+using cd2 = __attribute__((ext_vector_type(2))) double;
+constexpr int kTilePW = 8;     // panel / column-buffer row width (6 columns + 2 zero k-columns)
+constexpr int kTileRows = 112; // panel rows of both systems (7 tile rows)
+constexpr int kPanelStride = (kTileRows + 2) * kTilePW;  // + row kTileRows (always zero) + a trash row
+__host__ __device__ constexpr int chol_tile_rows(int n) { return n > 0 ? (n + 16) / 16 : 0; }
+__host__ __device__ constexpr bool chol_tile_fits(int n0, int n1) {
+    return n0 % 6 == 0 && n1 % 6 == 0 && chol_tile_rows(n0) <= 4 && chol_tile_rows(n1) <= 4 &&
+           chol_tile_rows(n0) + chol_tile_rows(n1) <= kTileRows / 16;
+}
+// panels (2 parities) | column buffer (kTileRows + a trash row) | inverse diagonals (2 x kTileRows)
+__host__ __device__ constexpr int chol_tile_scratch_doubles() { return 2 * kPanelStride + (kTileRows + 1) * kTilePW + 2 * kTileRows; }
+
+// v = vals[lane == idx ? q : ...]: the value of a per-lane index into a register array (select chain)
+template <int N>
+__device__ __forceinline__ double pick_d(const double (&vals)[N], int idx) {
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < N; ++q) v = idx == q ? vals[q] : v;
+    return v;
+}
+
+// L_JJ^-1 of the 6x6 lower block at B (row stride lda) with 1 / diagonal r: off-diagonal entries Linv[i][k]
+// (i > k) stored transposed at B[k lda + i] (the unused upper triangle), one store per lane (lanes < 15)
+__device__ __forceinline__ void chol6_inv_upper(double* B, int lda, const double* r, int lane, double* trash) {
+    double l[21], rr[6], v[21];
+#pragma unroll
+    for (int i = 0, q = 0; i < 6; ++i)
+#pragma unroll
+        for (int k = 0; k <= i; ++k, ++q) l[q] = B[i * lda + k];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) rr[c] = r[c];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {  // column c of the inverse: v[i][c], i >= c
+        v[c * (c + 1) / 2 + c] = rr[c];
+#pragma unroll
+        for (int i = c + 1; i < 6; ++i) {
+            double acc = 0.0;
+#pragma unroll
+            for (int m = c; m < i; ++m) acc += l[i * (i + 1) / 2 + m] * v[m * (m + 1) / 2 + c];
+            v[i * (i + 1) / 2 + c] = -rr[i] * acc;
+        }
+    }
+    // lane e < 15: off-diagonal entry e in row-major order (i, k), i > k
+    double off[15];
+    int oi = 0, ok = 0;
+#pragma unroll
+    for (int i = 1, e = 0; i < 6; ++i)
+#pragma unroll
+        for (int k = 0; k < i; ++k, ++e) {
+            off[e] = v[i * (i + 1) / 2 + k];
+            if (lane == e) { oi = i; ok = k; }
+        }
+    const double val = pick_d(off, lane);
+    *(lane < 15 ? B + ok * lda + oi : trash + (lane & 7)) = val;
+}
+
+// L^T x = y by one wave, 6-block column-oriented, n <= 63 (lane k holds t_k): y = row n of A, L below the
+// diagonal of A, the diagonal blocks' inverses as chol6_inv_upper left them (1 / L[c][c] in dv); the next
+// block's operands are requested before this block's chain.  x may not alias A.
+__device__ __forceinline__ void chol6_backward_blk(const double* A, int lda, int n, const double* dv, double* x, int lane) {
+    double t = A[(size_t)n * lda + (lane < n ? lane : 0)];
+    t = lane < n ? t : 0.0;
+    double li[21], lk[6];
+    auto fetch = [&](int c0) {
+#pragma unroll
+        for (int i = 0, q = 0; i < 6; ++i)
+#pragma unroll
+            for (int k = 0; k <= i; ++k, ++q) li[q] = i == k ? dv[c0 + i] : A[(c0 + k) * lda + c0 + i];  // Linv[i][k]
+#pragma unroll
+        for (int m = 0; m < 6; ++m) lk[m] = A[(c0 + m) * lda + lane];  // L[c0 + m][lane] (used for lane < c0)
+    };
+    if (n >= 6) fetch(n - 6);
+    for (int c0 = n - 6; c0 >= 0; c0 -= 6) {
+        double tj[6], cli[21], clk[6];
+#pragma unroll
+        for (int q = 0; q < 21; ++q) cli[q] = li[q];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) clk[m] = lane < c0 ? lk[m] : 0.0;
+        if (c0 >= 6) fetch(c0 - 6);
+#pragma unroll
+        for (int m = 0; m < 6; ++m) tj[m] = readlane_d(t, c0 + m);
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {  // x_m = sum_{i >= m} Linv[i][m] t_i
+            double acc = 0.0;
+#pragma unroll
+            for (int i = m; i < 6; ++i) acc += cli[i * (i + 1) / 2 + m] * tj[i];
+            t = lane == c0 + m ? acc : t - clk[m] * acc;
+        }
+    }
+    if (lane < n) x[lane] = t;
+}
+
+// f(std::integral_constant<int, 0>{}) ... f(std::integral_constant<int, N - 1>{}): indices as constants
+template <class F, int... Q>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Q...>) {
+    (f(std::integral_constant<int, Q>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// compile-time tile geometry of chol_tile_solve2: systems of T0 and T1 tile rows (T = (n + 16) / 16),
+// tile g of the lower tiles (system 0 row-major, then system 1) -> tile wave g % 2, slot g / 2
+template <int T0, int T1, int W>
+struct CholTiles {
+    static constexpr int NT0 = T0 * (T0 + 1) / 2, NTOT = NT0 + T1 * (T1 + 1) / 2;
+    static constexpr int NS = (NTOT - W + 1) / 2;  // slots of tile wave W
+    static constexpr int g(int q) { return W + 2 * q; }
+    static constexpr int sys(int q) { return g(q) >= NT0 ? 1 : 0; }
+    static constexpr int loc(int q) { return sys(q) ? g(q) - NT0 : g(q); }
+    static constexpr int a(int q) {
+        int gg = loc(q), r = 0;
+        while (gg > r) { gg -= r + 1; ++r; }
+        return r;
+    }
+    static constexpr int b(int q) { return loc(q) - a(q) * (a(q) + 1) / 2; }
+    static constexpr int soff(int q) { return sys(q) ? 16 * T0 : 0; }  // first row of the system in P / E
+};
+
+// the tile wave's part of chol_tile_solve2 (wave 2 + W): its tiles stay in registers for the whole
+// factorisation; two barriers per block column, matching the factoring waves' loop
+template <int T0, int T1, int W>
+__device__ __forceinline__ void chol_tile_wave(const double* A0, int n0, const double* A1, int n1, int lda, double* A0w,
+                                               double* A1w, double* Pb, double* E, double* dv, int nb0, int nb1, int nb,
+                                               int lane) {
+    using G = CholTiles<T0, T1, W>;
+    constexpr int NS = G::NS > 0 ? G::NS : 1;
+    double* const trash = E + kTileRows * kTilePW;
+    cd4 acc[NS];
+    static_for<NS>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        acc[q] = cd4{0.0, 0.0, 0.0, 0.0};
+        if constexpr (q < G::NS) {
+            constexpr int s = G::sys(q), ta = G::a(q), tb = G::b(q);
+            const double* A = s ? A1 : A0;
+            const int n = s ? n1 : n0;
+            const int col = 16 * tb + (lane & 15);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = 16 * ta + (lane >> 4) + 4 * i;
+                const bool in = row <= n && col <= row && col < n;
+                const double v = A[(in ? row : 0) * lda + (in ? col : 0)];
+                acc[q][i] = in ? v : 0.0;
+            }
+        }
+    });
+    __syncthreads();  // panels zeroed
+    // block steps as compile-time J (at most 64 / 6 + 1 for 4 tile rows): which slots hold block column
+    // J is then a constant, and panel J-1 is applied to those first (part 1), to the rest after the barrier
+    // (part 2); operands of a part's slots are requested before its MFMAs
+    constexpr int NBMAX = (16 * (T0 > T1 ? T0 : T1)) / 6 + 1;
+    static_for<NBMAX>([&](auto JJ) {
+        constexpr int J = decltype(JJ)::value, c0 = 6 * J;
+        if (J >= nb) return;  // uniform: the factoring waves' loop has nb steps
+        const double* P = Pb + ((J & 1) ^ 1) * kPanelStride;  // panel J-1
+        auto update = [&](auto Part1) {
+            constexpr bool part1 = decltype(Part1)::value;
+            double av[NS][2], bv[NS][2];
+            static_for<NS>([&](auto Q) {
+                constexpr int q = decltype(Q)::value;
+                if constexpr (q < G::NS) {
+                    constexpr int c16 = 16 * G::b(q);
+                    if constexpr (J > 0 && (c16 <= c0 + 5 && c16 + 15 >= c0) == part1) {
+                        constexpr int pa = G::soff(q) + 16 * G::a(q), pb = G::soff(q) + 16 * G::b(q);
+#pragma unroll
+                        for (int kh = 0; kh < 2; ++kh) {
+                            av[q][kh] = -P[(pa + (lane & 15)) * kTilePW + 4 * kh + (lane >> 4)];
+                            bv[q][kh] = P[(pb + (lane & 15)) * kTilePW + 4 * kh + (lane >> 4)];
+                        }
+                    }
+                }
+            });
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+                static_for<NS>([&](auto Q) {
+                    constexpr int q = decltype(Q)::value;
+                    if constexpr (q < G::NS) {
+                        constexpr int c16 = 16 * G::b(q);
+                        if constexpr (J > 0 && (c16 <= c0 + 5 && c16 + 15 >= c0) == part1)
+                            acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][kh], bv[q][kh], acc[q], 0, 0, 0);
+                    }
+                });
+        };
+        update(std::true_type{});
+        static_for<NS>([&](auto Q) {  // block column J out of the tiles holding it (others: the trash row)
+            constexpr int q = decltype(Q)::value;
+            if constexpr (q < G::NS) {
+                constexpr int s = G::sys(q), c16 = 16 * G::b(q), r16 = 16 * G::a(q), so = G::soff(q);
+                if constexpr (c16 <= c0 + 5 && c16 + 15 >= c0 && r16 + 15 >= c0) {
+                    const int col = c16 + (lane & 15), n = (J < (s ? nb1 : nb0)) ? (s ? n1 : n0) : -1;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = r16 + (lane >> 4) + 4 * i;
+                        const bool in = col >= c0 && col < c0 + 6 && row >= c0 && row <= n;
+                        *(in ? E + (so + row) * kTilePW + col - c0 : trash + (lane & 7)) = acc[q][i];
+                    }
+                }
+            }
+        });
+        __syncthreads();
+        if constexpr (J > 0) {
+            update(std::false_type{});
+            if (J - 1 < (W ? nb1 : nb0))  // the previous diagonal block's inverse (wave 2: system 0, wave 3: system 1)
+                chol6_inv_upper((W ? A1w : A0w) + (c0 - 6) * lda + c0 - 6, lda, dv + (W ? kTileRows : 0) + c0 - 6, lane, trash);
+        }
+        __syncthreads();
+    });
+}
+
+template <int T0, int T1>
+__device__ __forceinline__ bool chol_tile_solve2(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1,
+                                                 double* scr, int* flag, unsigned long long* tm = nullptr) {
+    static_assert(T0 <= 4 && T1 <= 4 && T0 + T1 <= kTileRows / 16, "chol_tile_solve2: one panel row per lane");
+    // tm (diagnostic, may be null): shader clocks of [set-up, factorisation, -, backward] seen by thread 0
+    unsigned long long tlast = tm ? __builtin_amdgcn_s_memtime() : 0;
+    auto tmark = [&](int slot) {
+        if (tm && threadIdx.x == 0) {
+            const unsigned long long tt = __builtin_amdgcn_s_memtime();
+            tm[slot] += tt - tlast;
+            tlast = tt;
+        }
+    };
+    const int t = (int)threadIdx.x, lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int nb0 = n0 / 6, nb1 = n1 / 6, nb = nb0 > nb1 ? nb0 : nb1;
+    constexpr int soff1 = 16 * T0;                     // system 1's first row in the panel / column buffers
+    double* const Pb = scr;                            // panel buffers, parity p at Pb + p * kPanelStride
+    double* const E = scr + 2 * kPanelStride;          // column buffer; row kTileRows: trash
+    double* const trash = E + kTileRows * kTilePW;
+    double* const dv = E + (kTileRows + 1) * kTilePW;  // 1 / L[c][c]: system 0 at dv, system 1 at dv + kTileRows
+    for (int e = t; e < 2 * kPanelStride; e += 256) Pb[e] = 0.0;
+    if (t == 0) *flag = 0;
+    tmark(0);
+    if (wid >= 2) {
+        if (wid == 2) chol_tile_wave<T0, T1, 0>(A0, n0, A1, n1, lda, A0, A1, Pb, E, dv, nb0, nb1, nb, lane);
+        else chol_tile_wave<T0, T1, 1>(A0, n0, A1, n1, lda, A0, A1, Pb, E, dv, nb0, nb1, nb, lane);
+    } else {
+        __syncthreads();  // panels zeroed, the tiles loaded
+        const int s = wid, n = s ? n1 : n0, nbs = s ? nb1 : nb0;
+        double* const A = s ? A1 : A0;
+        const double* const Es = E + (s ? soff1 : 0) * kTilePW;
+        double* const inv = dv + (s ? kTileRows : 0);
+        int bad = 0;
+        for (int J = 0; J < nb; ++J) {
+            const int c0 = 6 * J, par = J & 1;
+            __syncthreads();  // block column J in E
+            // (b) diagonal block J and the panel row below it, wave s for system s
+            if (J < nbs) {
+                double* const P = Pb + par * kPanelStride + (s ? soff1 : 0) * kTilePW;
+                double* const Ptrash = Pb + par * kPanelStride + (kTileRows + 1) * kTilePW;
+                const int rA = c0 + 6 + lane;
+                const bool live = rA <= n;
+                cd2 dr[6][3], er[3];
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) dr[i][p] = *reinterpret_cast<const cd2*>(Es + (c0 + i) * kTilePW + 2 * p);
+                const double* erow = Es + (live ? rA : n) * kTilePW;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) er[p] = *reinterpret_cast<const cd2*>(erow + 2 * p);
+                double l[21], ea[6];
+#pragma unroll
+                for (int i = 0, qq = 0; i < 6; ++i)
+#pragma unroll
+                    for (int k = 0; k <= i; ++k, ++qq) l[qq] = dr[i][k >> 1][k & 1];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) ea[c] = er[c >> 1][c & 1];
+                double r[6];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) {
+                    const double piv = l[c * (c + 1) / 2 + c];
+                    bad |= !(piv > 0.0);
+                    r[c] = rsq_nr(piv);
+                    l[c * (c + 1) / 2 + c] = piv * r[c];
+#pragma unroll
+                    for (int i = c + 1; i < 6; ++i) l[i * (i + 1) / 2 + c] *= r[c];
+#pragma unroll
+                    for (int i = c + 1; i < 6; ++i)
+#pragma unroll
+                        for (int k = c + 1; k <= i; ++k) l[i * (i + 1) / 2 + k] -= l[i * (i + 1) / 2 + c] * l[k * (k + 1) / 2 + c];
+                    // the panel's column c as soon as L's column c is known
+#pragma unroll
+                    for (int m = 0; m < c; ++m) ea[c] -= ea[m] * l[c * (c + 1) / 2 + m];
+                    ea[c] *= r[c];
+                }
+                // panel row (or the trash row), the previous panel's rows of this buffer zeroed (lanes < 12)
+                double* prow = live ? P + rA * kTilePW : Ptrash;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) *reinterpret_cast<cd2*>(prow + 2 * p) = cd2{ea[2 * p], ea[2 * p + 1]};
+                const int zr = c0 - 6 + lane;
+                double* zrow = (lane < 12 && zr >= 0) ? P + zr * kTilePW : Ptrash;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) *reinterpret_cast<cd2*>(zrow + 2 * p) = cd2{0.0, 0.0};
+                // L: the panel row, the diagonal block (lane u < 36: entry (u / 6, u % 6), zeros above), 1 / L[c][c]
+                double* arow = live ? A + rA * lda + c0 : trash;
+#pragma unroll
+                for (int c = 0; c < 6; ++c) arow[c] = ea[c];
+                double full[36];
+#pragma unroll
+                for (int i = 0; i < 6; ++i)
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) full[6 * i + k] = k <= i ? l[i * (i + 1) / 2 + k] : 0.0;
+                const double lv = pick_d(full, lane);
+                *(lane < 36 ? A + (c0 + lane / 6) * lda + c0 + lane % 6 : trash + (lane & 7)) = lv;
+                *(lane < 6 ? inv + c0 + lane : trash + (lane & 7)) = pick_d(r, lane);
+            }
+            __syncthreads();  // panel J in P
+        }
+        if (bad && lane == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    tmark(1);
+    if (*flag) return false;
+    // the last diagonal blocks' inverses, then the backward substitution by wave s
+    if (wid >= 2) {
+        const int s = wid - 2, nbs = s ? nb1 : nb0;
+        if (nbs > 0)
+            chol6_inv_upper((s ? A1 : A0) + 6 * (nbs - 1) * lda + 6 * (nbs - 1), lda, dv + (s ? kTileRows : 0) + 6 * (nbs - 1),
+                            lane, E + kTileRows * kTilePW);
+    }
+    __syncthreads();
+    if (wid == 0 && nb0 > 0) chol6_backward_blk(A0, lda, n0, dv, x0, lane);
+    else if (wid == 1 && nb1 > 0) chol6_backward_blk(A1, lda, n1, dv + kTileRows, x1, lane);
+    __syncthreads();
+    tmark(3);
     return true;
 }
 

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VIO360_ABI_VERSION 3
+#define VIO360_ABI_VERSION 4
 
 /* ----------------------------------------------------------------------------------------- */
 /* error codes                                                                                */
@@ -239,7 +239,7 @@ void vio_ba_batch_destroy(vio_ba_batch* b);
 /* diagnostics: per-phase shader-clock accounting of the solver kernel (sum over windows of the
    last run; VIO_BA_PROF_SLOTS slots, named in the Python mirror's BaBatch.PHASES) */
 int vio_ba_batch_profile(vio_ba_batch* b, int enable);
-#define VIO_BA_PROF_SLOTS 24
+#define VIO_BA_PROF_SLOTS 32
 int vio_ba_batch_phase_cycles(vio_ba_batch* b, unsigned long long* out /* [VIO_BA_PROF_SLOTS] */);
 
 /*

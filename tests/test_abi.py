@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol(vio):
 
 
 def test_abi_version(vio):
-    assert vio.lib().vio_abi_version() == 3
+    assert vio.lib().vio_abi_version() == 4  # 4: VIO_BA_PROF_SLOTS 24 -> 32
 
 
 STRUCTS = {

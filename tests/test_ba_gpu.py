@@ -318,10 +318,15 @@ def test_cluster_route_bitwise_across_member_counts(vio, synth, gpu_ctx):
     the leader), and a second run of the batch reproduces them."""
     ws = [synth.config3(synth.SEED + i) for i in range(32)]
     probs = [vio.BaProblem(w, variant=vio.VIO_BA_VI, max_iterations=10, fixed_iterations=1) for w in ws]
-    big = gpu_ctx.ba_solve(probs)
-    big2 = gpu_ctx.ba_solve(probs)
+    gpu_ctx.set_ba_route(gpu_ctx.ROUTE_CLUSTER)  # (auto gives a 32-window batch the phase kernels)
+    try:
+        big = gpu_ctx.ba_solve(probs)
+        big2 = gpu_ctx.ba_solve(probs)
+        solos = {i: gpu_ctx.ba_solve([probs[i]])[0] for i in (0, 13, 31)}
+    finally:
+        gpu_ctx.set_ba_route(gpu_ctx.ROUTE_AUTO)
     for i in (0, 13, 31):
-        solo = gpu_ctx.ba_solve([probs[i]])[0]
+        solo = solos[i]
         for key in ("T_wb", "lm_xyz", "obs_chi2", "vel", "bg", "ba"):
             assert np.array_equal(big[i][key], solo[key]), (i, key)
             assert np.array_equal(big[i][key], big2[i][key]), (i, key)

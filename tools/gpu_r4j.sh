@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 4 (j): reduced-solve probe, stamps at one window (VIO_BA_CHOL=2), route A/B (default vs
+# VIO_BA_CHOL=2) at 1 / 16 / 32 / 256 windows, BA GPU tests with VIO_BA_CHOL=2
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 60 ./tools/probe/cholmw_probe > gpurun_out/cholmw_j.log 2>&1; grep -E "V1|V4" gpurun_out/cholmw_j.log
+VIO_BA_CHOL=2 timeout -k 10 60 python3 tools/ph_solve_stamps.py 1 > gpurun_out/stamps_cluster_1j.log 2>&1 || { cat gpurun_out/stamps_cluster_1j.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/stamps_cluster_1j.log
+timeout -k 10 200 python3 tools/ba_route_ab.py 1 16 32 256 > gpurun_out/route_ab_j0.log 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/route_ab_j0.log; [ $rc -eq 0 ] || exit $rc
+VIO_BA_CHOL=2 timeout -k 10 200 python3 tools/ba_route_ab.py 1 16 32 256 > gpurun_out/route_ab_j2.log 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/route_ab_j2.log; [ $rc -eq 0 ] || exit $rc
+VIO_BA_CHOL=2 timeout -k 10 600 python -u -m pytest tests/test_ba_gpu.py -m gpu -x -q --timeout 180 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_ba_j.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_ba_j.log; [ $rc -eq 0 ] || { grep -E "^FAILED|Error|assert" gpurun_out/pytest_ba_j.log | head -10; exit $rc; }

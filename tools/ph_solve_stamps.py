@@ -19,7 +19,7 @@ print("route", b.route())
 b.profile(True)
 b.run(); b.sync()
 import ctypes as C
-out = (C.c_ulonglong * 24)()
+out = (C.c_ulonglong * 32)()
 ctx.check(vio.lib().vio_ba_batch_phase_cycles(b.h, out), "phase_cycles")
 names = {0: "prep U partials", 1: "prep imu", 2: "prep cost partials", 3: "prep imu normal eq", 4: "prep gradient",
          5: "prep finalize+diag", 6: "schur g0 landmark blocks", 15: "schur g0 zero panel", 7: "schur g0 fills",
@@ -27,7 +27,8 @@ names = {0: "prep U partials", 1: "prep imu", 2: "prep cost partials", 3: "prep 
          11: "chol forward / cl member1 wait R",
          12: "chol backward / cl member1 wait F", 23: "cl member1 walk",
          16: "solve assembly+partials", 17: "solve cholesky+solves", 18: "solve small inputs+tables",
-         19: "solve pose tiles+partials", 20: "solve reductions", 21: "ctrl lane", 22: "ctrl copies"}
+         19: "solve pose tiles+partials", 20: "solve reductions", 21: "ctrl lane", 22: "ctrl copies",
+         24: "cl imu loads", 25: "cl imu model change", 26: "cl imu factors", 27: "cl imu cost", 28: "cl imu normal eq"}
 tot = sum(out[i] for i in names)
 for i, n in names.items():
     print(f"W={W} {n:28s} cycles/window/iter {out[i] / W / 11:10.0f}  ({100 * out[i] / max(tot, 1):.1f}%)")

@@ -5,6 +5,7 @@
 //   V2  chol_mw: lane = row, the columns split over NW waves (CB columns each), one s_barrier per pivot,
 //       the pivot column published through LDS, look-ahead of the owner's next column; 54 alone
 //   V3  chol_mw on both: 54 over waves 0-2 (18 columns each) + 36 over wave 3 (one wave)
+//   V4  chol_tile_solve2 on both (trailing matrix in MFMA tile registers, 6-column block steps)
 // Diagnostic only (tools/, not shipped).  Build: hipcc --offload-arch=gfx950 -O3 -std=c++17
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -115,6 +116,8 @@ __global__ void __launch_bounds__(256, 1) probe(const double* gA, const double* 
     __shared__ double Lb[2][64 * 65];
     __shared__ double dv[2][64];
     __shared__ int flag;
+    __shared__ unsigned long long tsum[16];
+    if (threadIdx.x < 16) tsum[threadIdx.x] = 0;
     unsigned long long tot = 0;
     for (int r = 0; r < reps; ++r) {
         // system 0 at S (rows 0..n0, rhs row n0), system 1 at S + (n0 + 1) * LD + n0 (rhs row n1)
@@ -137,6 +140,8 @@ __global__ void __launch_bounds__(256, 1) probe(const double* gA, const double* 
             const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
             if (wv < 3) chol_mw<3, 18, 56, 54>(S, LD, n0, 0, scr[0], Lb[0], 65, dv[0], xs[0]);
             else chol_mw<1, 40, 40, 36, 18>(A1, LD, n1, 3, scr[2], Lb[1], 65, dv[1], xs[1]);
+        } else if (V == 4) {
+            chol_tile_solve2<4, 3>(S, n0, A1, n1, LD, xs[0], xs[1], &Lb[0][0], &flag, tsum);
         }
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         tot += t1 - t0;
@@ -147,6 +152,15 @@ __global__ void __launch_bounds__(256, 1) probe(const double* gA, const double* 
         gx[64 + threadIdx.x] = xs[1][threadIdx.x];
     }
     if (threadIdx.x == 0) *cyc = tot / reps;
+    if (V == 4 && threadIdx.x == 0)
+        printf("   V4 phases per solve: set-up %llu  factor %llu  -- %llu  backward %llu\n", tsum[0] / reps, tsum[1] / reps,
+               tsum[2] / reps, tsum[3] / reps);
+    if (V == 4 && threadIdx.x == 0)
+        printf("   V4 tile wave: (a1) %llu  barrier1 %llu  (a2) %llu  inverse %llu  barrier2 %llu\n", tsum[4] / reps,
+               tsum[5] / reps, tsum[6] / reps, tsum[7] / reps, tsum[8] / reps);
+    if (V == 4 && threadIdx.x == 0)
+        printf("   V4 diag wave: wait %llu  loads %llu  factor+panel %llu  stores %llu\n", tsum[9] / reps, tsum[10] / reps,
+               tsum[11] / reps, tsum[12] / reps);
 }
 
 static void make_spd(int n, double* A /* (n+1) x 64, lower + rhs row */, unsigned seed) {
@@ -186,10 +200,11 @@ int main() {
     hipMalloc(&dc, 8);
     hipMemcpy(dA, A, sizeof(A), hipMemcpyHostToDevice);
     hipMemcpy(dB, B, sizeof(B), hipMemcpyHostToDevice);
-    void (*fns[4])(const double*, const double*, int, int, int, double*, unsigned long long*) = {probe<0>, probe<1>,
-                                                                                                 probe<2>, probe<3>};
-    const char* names[4] = {"chol6_solve2 54", "chol6_solve2 54+36", "chol_mw 4x16 54", "chol_mw 3x18 54 + 1x40 36"};
-    for (int v = 0; v < 4; ++v) {
+    void (*fns[5])(const double*, const double*, int, int, int, double*, unsigned long long*) = {probe<0>, probe<1>,
+                                                                                                 probe<2>, probe<3>, probe<4>};
+    const char* names[5] = {"chol6_solve2 54", "chol6_solve2 54+36", "chol_mw 4x16 54", "chol_mw 3x18 54 + 1x40 36",
+                            "chol_tile_solve2 54+36"};
+    for (int v = 0; v < 5; ++v) {
         for (int rep = 0; rep < 2; ++rep) {
             hipLaunchKernelGGL(fns[v], dim3(1), dim3(256), 0, 0, dA, dB, n0, n1, reps, dx, dc);
             if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
@@ -198,7 +213,7 @@ int main() {
         double x[128];
         hipMemcpy(&cyc, dc, 8, hipMemcpyDeviceToHost);
         hipMemcpy(x, dx, sizeof(x), hipMemcpyDeviceToHost);
-        const double r0 = resid(n0, A, x), r1 = (v == 1 || v == 3) ? resid(n1, B, x + 64) : 0.0;
+        const double r0 = resid(n0, A, x), r1 = (v == 1 || v == 3 || v == 4) ? resid(n1, B, x + 64) : 0.0;
         printf("V%d %-28s cycles/solve %7llu  resid %.2e %.2e\n", v, names[v], cyc, r0, r1);
     }
     return 0;
