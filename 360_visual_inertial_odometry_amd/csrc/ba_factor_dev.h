@@ -137,6 +137,40 @@ __device__ __forceinline__ int factor_eval(const double* pc, const double* Rcb_r
     return 0;
 }
 
+// The Jacobian tail of factor_eval_ap at camera-frame point (x, y, z), |P| = L, 1 / L = iL: A = Jw R_cb_raw
+// (2x3, weighted) and Pb = R_bw Pw + t_bw.  Returns false (A, Pb untouched) where the Jacobian is zero.
+__device__ __forceinline__ bool factor_ap_tail(double x, double y, double z, double L, double iL, const double* Rbw,
+                                               const double* tbw, const double* Pw, const double* Rcb_raw, double cols,
+                                               double rows, const double* Lw, double* A, double* Pb) {
+    constexpr double inv2pi = 1.0 / (2.0 * M_PI), invpi = 1.0 / M_PI;
+    double xz2 = x * x + z * z, L2 = L * L;
+    if (xz2 < 1e-10 || L2 < 1e-10) return false;
+    double xzn = sqrt(xz2);
+    const double ixzn = 1.0 / xzn, ixz2 = ixzn * ixzn, iL2 = iL * iL, iL2xzn = iL2 * ixzn;
+    const double cu = cols * inv2pi, cv = rows * invpi;
+    double Jc[6];
+    Jc[0] = -cu * z * ixz2;
+    Jc[1] = 0.0;
+    Jc[2] = cu * x * ixz2;
+    Jc[3] = cv * (x * y) * iL2xzn;
+    Jc[4] = -cv * xzn * iL2;
+    Jc[5] = cv * (y * z) * iL2xzn;
+    double Jw[6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        Jw[j] = Lw[0] * Jc[j];
+        Jw[3 + j] = Lw[2] * Jc[j] + Lw[3] * Jc[3 + j];
+    }
+    m3vec(Rbw, Pw, Pb);
+    Pb[0] += tbw[0]; Pb[1] += tbw[1]; Pb[2] += tbw[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            A[3 * i + j] = Jw[3 * i] * Rcb_raw[j] + Jw[3 * i + 1] * Rcb_raw[3 + j] + Jw[3 * i + 2] * Rcb_raw[6 + j];
+    return true;
+}
+
 // BAFactor::Evaluate as factor_eval, returning the Jacobian in compressed form: A = Jw R_cb_raw (2x3,
 // weighted) and Pb (point in the body frame); J_pose / J_point follow as in jac_from_ap.
 __device__ __forceinline__ int factor_eval_ap(const double* pc, const double* Rcb_raw, const double* Pw, double uo,
@@ -178,33 +212,37 @@ __device__ __forceinline__ int factor_eval_ap(const double* pc, const double* Rc
     }
     r[0] = Lw[0] * du;
     r[1] = Lw[2] * du + Lw[3] * dv;
-    double xz2 = x * x + z * z, L2 = L * L;
-    if (xz2 < 1e-10 || L2 < 1e-10) return 0;
-    jzero = false;
-    double xzn = sqrt(xz2);
-    const double ixzn = 1.0 / xzn, ixz2 = ixzn * ixzn, iL2 = iL * iL, iL2xzn = iL2 * ixzn;
-    const double cu = cols * inv2pi, cv = rows * invpi;
-    double Jc[6];
-    Jc[0] = -cu * z * ixz2;
-    Jc[1] = 0.0;
-    Jc[2] = cu * x * ixz2;
-    Jc[3] = cv * (x * y) * iL2xzn;
-    Jc[4] = -cv * xzn * iL2;
-    Jc[5] = cv * (y * z) * iL2xzn;
-    double Jw[6];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        Jw[j] = Lw[0] * Jc[j];
-        Jw[3 + j] = Lw[2] * Jc[j] + Lw[3] * Jc[3 + j];
-    }
-    m3vec(Rbw, Pw, Pb);
-    Pb[0] += tbw[0]; Pb[1] += tbw[1]; Pb[2] += tbw[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-            A[3 * i + j] = Jw[3 * i] * Rcb_raw[j] + Jw[3 * i + 1] * Rcb_raw[3 + j] + Jw[3 * i + 2] * Rcb_raw[6 + j];
+    jzero = !factor_ap_tail(x, y, z, L, iL, Rbw, tbw, Pw, Rcb_raw, cols, rows, Lw, A, Pb);
     return 0;
+}
+
+// The compressed Jacobian of factor_eval_ap at a point whose residual was linearised with Jacobian scale asc
+// (the Huber / Corrector scale, 0 when the Jacobian was zero: outlier, degenerate or out-of-range residual):
+// A = asc Jw R_cb_raw and Pb, recomputed from the point and the pose cache at the linearisation point (pcl:
+// Rbw(9) tbw(3) Rcw(9) tcw(3), i.e. pose_cache_one's output from offset 12) with factor_eval_ap's own
+// operations (factor_ap_tail).  The window solver's phase kernels keep only r and asc per observation
+// (24 B instead of 88 B) and rebuild A / Pb where they are used.
+__device__ __forceinline__ void factor_ap_at(const double* pcl, const double* Rcb_raw, const double* Pw, double cols,
+                                             double rows, const double* Lw, double asc, double* A, double* Pb) {
+    if (asc == 0.0) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) A[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Pb[i] = 0.0;
+        return;
+    }
+    const double* Rbw = pcl;
+    const double* tbw = pcl + 9;
+    const double* Rcw = pcl + 12;
+    const double* tcw = pcl + 21;
+    double Pc[3];
+    m3vec(Rcw, Pw, Pc);
+    Pc[0] += tcw[0]; Pc[1] += tcw[1]; Pc[2] += tcw[2];
+    const double L = nrm3(Pc);
+    const double iL = 1.0 / L;
+    factor_ap_tail(Pc[0], Pc[1], Pc[2], L, iL, Rbw, tbw, Pw, Rcb_raw, cols, rows, Lw, A, Pb);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) A[i] *= asc;
 }
 
 // compute_chi_square (Factors.cpp:212-265, 544-612), unweighted e^T Info e
