@@ -288,10 +288,10 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     d.P.field = (type)ptr;
     // landmark chunks per Schur split-k group (phase route): a full config-4 shard (>= 256 windows)
     // fills the chip with 2 groups per window and halves ph_solve's partial sums; smaller batches keep
-    // more, shorter groups (latency)
+    // more, shorter groups (latency): 3 below 64 windows, 5 up to 255 (sweep of 2/3/4/5/10 at 1..256
+    // windows, profiles/r4e_gs_sweep.log); the cluster route: one chunk per group, the group's member owns
+    // its landmarks
     const char* gse = std::getenv("VIO_BA_SCHUR_GS");  // experiment override
-    // (1..4 measured slower at 1 and 32 windows on the phase route); the cluster route: one chunk per
-    // group, the group's member owns its landmarks
     static const int cmax = [] {
         const char* v = std::getenv("VIO_BA_CLUSTER_C");  // experiment override: members per window
         return v ? std::atoi(v) : 0;
@@ -299,7 +299,7 @@ static int upload_batch(vio_ctx* ctx, BaDevice& d) {
     // (an explicitly requested cluster route takes whatever members fit: no minimum per landmark chunk)
     const int cm = cmax > 0 ? cmax : ctx->ba_route == VIO_BA_ROUTE_CLUSTER ? (1 << 20) : 0;
     d.cluster_C = cluster_wanted(ctx, d.n) ? ba_cluster_members(pk.win.data(), d.n, cm) : 0;
-    const int gs = d.cluster_C ? 1 : gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : 5;
+    const int gs = d.cluster_C ? 1 : gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : pk.win.size() >= 64 ? 5 : 3;
     for (BaWin& w : pk.win) w.gs = gs;
     UP(pk.win, win, const BaWin*);
     UP(pk.pose_raw, pose_raw, const double*);

@@ -142,6 +142,10 @@ __global__ void __launch_bounds__(256, 1) probe(const double* gA, const double* 
             else chol_mw<1, 40, 40, 36, 18>(A1, LD, n1, 3, scr[2], Lb[1], 65, dv[1], xs[1]);
         } else if (V == 4) {
             chol_tile_solve2<4, 3>(S, n0, A1, n1, LD, xs[0], xs[1], &Lb[0][0], &flag, tsum);
+        } else if (V == 5) {
+            chol_tile_solve2<4, 0>(S, n0, A1, 0, LD, xs[0], xs[1], &Lb[0][0], &flag, tsum);
+        } else if (V == 6) {
+            chol_tile_solve2<3, 0>(A1, n1, S, 0, LD, xs[1], xs[0], &Lb[0][0], &flag, tsum);
         }
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         tot += t1 - t0;
@@ -200,11 +204,11 @@ int main() {
     hipMalloc(&dc, 8);
     hipMemcpy(dA, A, sizeof(A), hipMemcpyHostToDevice);
     hipMemcpy(dB, B, sizeof(B), hipMemcpyHostToDevice);
-    void (*fns[5])(const double*, const double*, int, int, int, double*, unsigned long long*) = {probe<0>, probe<1>,
-                                                                                                 probe<2>, probe<3>, probe<4>};
-    const char* names[5] = {"chol6_solve2 54", "chol6_solve2 54+36", "chol_mw 4x16 54", "chol_mw 3x18 54 + 1x40 36",
-                            "chol_tile_solve2 54+36"};
-    for (int v = 0; v < 5; ++v) {
+    void (*fns[7])(const double*, const double*, int, int, int, double*, unsigned long long*) = {
+        probe<0>, probe<1>, probe<2>, probe<3>, probe<4>, probe<5>, probe<6>};
+    const char* names[7] = {"chol6_solve2 54", "chol6_solve2 54+36", "chol_mw 4x16 54", "chol_mw 3x18 54 + 1x40 36",
+                            "chol_tile_solve2 54+36", "chol_tile_solve2 54", "chol_tile_solve2 36"};
+    for (int v = 0; v < 7; ++v) {
         for (int rep = 0; rep < 2; ++rep) {
             hipLaunchKernelGGL(fns[v], dim3(1), dim3(256), 0, 0, dA, dB, n0, n1, reps, dx, dc);
             if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
@@ -213,7 +217,7 @@ int main() {
         double x[128];
         hipMemcpy(&cyc, dc, 8, hipMemcpyDeviceToHost);
         hipMemcpy(x, dx, sizeof(x), hipMemcpyDeviceToHost);
-        const double r0 = resid(n0, A, x), r1 = (v == 1 || v == 3 || v == 4) ? resid(n1, B, x + 64) : 0.0;
+        const double r0 = v == 6 ? 0.0 : resid(n0, A, x), r1 = (v == 1 || v == 3 || v == 4 || v == 6) ? resid(n1, B, x + 64) : 0.0;
         printf("V%d %-28s cycles/solve %7llu  resid %.2e %.2e\n", v, names[v], cyc, r0, r1);
     }
     return 0;
