@@ -583,10 +583,16 @@ __global__ void __launch_bounds__(256) chol_trsm_kernel(double* S, int n, int k,
 
 // trailing update: A_ij -= A_ik A_jk^T for k < j <= i (lower block triangle), one tile per block.
 // part 0: every tile; part 1: the first trailing column only (j = k+1, the next step's diagonal
-// block and panel); part 2: the rest (j >= k+2) — the look-ahead split of gba_launch_cholesky.
+// block and panel); part 2: the rest (j >= k+2) — the look-ahead split of gba_launch_cholesky; part 3:
+// part 2 without its first tile, the diagonal block (k+2, k+2) (the chained schedule's diagonal
+// workgroup applies that one itself, chol_chain_kernel).
 // tile t of the update (one workgroup); As / Bs: NB x (NB + 1) doubles of LDS each
 __device__ __forceinline__ void syrk_tile(double* S, int n, int k, int part, long long t, double (*As)[NB + 1],
                                           double (*Bs)[NB + 1]) {
+    if (part == 3) {
+        part = 2;
+        ++t;
+    }
     // t -> (i, j) with 0 <= jj <= ii < m, i = k+1+ii, j = k+1+jj
     int ii = 0, jj = 0;
     if (part == 1) {
@@ -772,37 +778,41 @@ __device__ __forceinline__ void flag_publish(int* f) {
     if (threadIdx.x == 0) __hip_atomic_store((gint*)f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Fused Cholesky step for block column k (the critical chain of the look-ahead schedule in one
-// launch): workgroup 0 applies column k-1's update to the diagonal block (k, k) and factors it
-// (diag_block_lds), publishing L_kk^-1 through a flag (hand-off as above); workgroup i >= 1 applies
-// column k-1's update to the panel block (k+i, k) while the diagonal block is factored, waits for the
-// flag and multiplies by L_kk^-T.  The arithmetic is chol_syrk_kernel's (part 1), chol_diag_kernel's
-// and chol_trsm_kernel's, in the same order: bitwise the three-launch step.  k == 0: no update.
-// Dynamic LDS: CHOL_DIAG_LDS bytes.  flag: 0 pending, 1 L_kk^-1 final, 2 the block is not positive
-// definite.
-// Workgroups past the step's m + 1 (trail > 0: `trail` of them) apply step k-1's trailing update right of
-// block column k (chol_syrk_kernel part 2 of step k-1, its tiles in order): disjoint from block column k,
-// after panel k-1 (the previous launch) and before step k+1 (the next), so the look-ahead needs no second
-// stream for it.
-__global__ void __launch_bounds__(256) chol_step_kernel(double* S, int n, int k, double* Linv, int* fail, int* flag,
-                                                        int* tmo, int trail) {
+// Chained Cholesky launch k (the critical chain of the look-ahead schedule, one launch per block
+// column, no waits inside): workgroup b < m = nblk - k - 1 forms the panel block L_{k+1+b, k}: column
+// k-1's update of S_{k+1+b, k}, then the product with L_kk^-T (L_kk^-1 is final: the previous launch
+// wrote it).  Workgroup 0 then goes on to the next diagonal block d = k+1: column k-1's update of S_dd
+// (the first tile of chol_syrk_kernel part 2 of step k-1, which the trailing update therefore leaves
+// out: part 3), column k's update with the panel block L_{d,k} it has just formed (still in LDS, no
+// hand-off), the factor and L_dd^-1 (diag_block_lds).  Launch k = -1: workgroup 0 factors block 0.
+// The arithmetic is chol_syrk_kernel's, chol_diag_kernel's and chol_trsm_kernel's in the same order:
+// bitwise the three-launch schedule.  Workgroups past m (trail > 0: `trail` of them) apply step k-1's
+// trailing update right of block column k+1 (part 3 of step k-1, its tiles in order): disjoint from
+// block columns k and k+1 and from S_dd, after panel k-1 (the previous launch) and before launch k+1,
+// so the look-ahead needs no second stream for it.  Dynamic LDS: CHOL_DIAG_LDS bytes.  fail: set by a
+// non-positive pivot; later launches then do nothing (the host rejects the step).
+__global__ void __launch_bounds__(256) chol_chain_kernel(double* S, int n, int k, double* Linv, int* fail, int trail) {
     extern __shared__ double dyn[];
     double (*As)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(dyn);
     double (*Bs)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(dyn + NB * TLD);
-    {
-        const int m1 = n / NB - k;  // the step's own workgroups
-        if ((int)blockIdx.x >= m1) {
-            if ((int)blockIdx.x - m1 < trail) syrk_tile(S, n, k - 1, 2, (long long)blockIdx.x - m1, As, Bs);
-            return;
-        }
+    const int nblk = n / NB, own = k >= 0 ? nblk - k - 1 : 1;  // the launch's own workgroups
+    if ((int)blockIdx.x >= own) {
+        if ((int)blockIdx.x - own < trail) syrk_tile(S, n, k - 1, 3, (long long)blockIdx.x - own, As, Bs);
+        return;
     }
-    __shared__ int bad_s, ok_s;
+    if (*fail) return;
+    __shared__ int bad_s;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r0 = 32 * (wid >> 1), c0 = 32 * (wid & 1);
-    const bool diag = blockIdx.x == 0;
-    const int i = k + (int)blockIdx.x;
+    const bool lead = blockIdx.x == 0;
+    const int d = k + 1;  // workgroup 0: the next diagonal block
+    constexpr int PER = NB * NB / 256;
+    // every global load of the workgroup first: the panel block, the diagonal block (workgroup 0),
+    // column k-1's operand blocks, L_kk^-1
+    double cv[2][2][4], dv[2][2][4], va[PER], vb[PER], vl[PER];
+    const int i = k + 1 + (int)blockIdx.x;
     double* C = S + (size_t)i * NB * n + (size_t)k * NB;
-    double cv[2][2][4];
+    double* D = S + (size_t)d * NB * n + (size_t)d * NB;
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -810,17 +820,39 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* S, int n, int k,
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
-                cv[ti][tj][q] = (!diag || c <= r) ? C[(size_t)r * n + c] : 0.0;
+                cv[ti][tj][q] = k >= 0 ? C[(size_t)r * n + c] : 0.0;
+                dv[ti][tj][q] = lead && c <= r ? D[(size_t)r * n + c] : 0.0;
             }
-    if (k > 0) {  // C -= A_{i,k-1} A_{k,k-1}^T
+    if (k > 0) {
         const double* Aik = S + (size_t)i * NB * n + (size_t)(k - 1) * NB;
         const double* Ajk = S + (size_t)k * NB * n + (size_t)(k - 1) * NB;
-        stage_tiles(As, Bs, Aik, (size_t)n, Ajk, (size_t)n);
-        __syncthreads();
-        d4 acc[2][2];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = threadIdx.x + 256 * u, r = e / NB, c = e % NB;
+            va[u] = Aik[(size_t)r * n + c];
+            vb[u] = Ajk[(size_t)r * n + c];
+        }
+    }
+    if (k >= 0) {
+        const double* Li = Linv + (size_t)k * NB * NB;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) vl[u] = Li[threadIdx.x + 256 * u];
+    }
+    auto to_lds = [&](double (*X)[NB + 1], const double* v) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            X[e / NB][e % NB] = v[u];
+        }
+    };
+    auto tile_product = [&](d4 acc[2][2]) {  // acc = As Bs^T
+#pragma unroll
         for (int a = 0; a < 2; ++a)
+#pragma unroll
             for (int b = 0; b < 2; ++b) acc[a][b] = d4{0, 0, 0, 0};
         mfma_tile_ABt(As, Bs, acc, wid, lane);
+    };
+    auto sub = [&](double (&x)[2][2][4], d4 acc[2][2], bool lower) {  // x -= acc (lower: c <= r only)
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -828,11 +860,72 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* S, int n, int k,
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
-                    if (!diag || c <= r) cv[ti][tj][q] = cv[ti][tj][q] - acc[ti][tj][q];
+                    if (!lower || c <= r) x[ti][tj][q] = x[ti][tj][q] - acc[ti][tj][q];
                 }
+    };
+    d4 acc[2][2];
+    if (k > 0) {  // column k-1: S_ik -= A_{i,k-1} A_{k,k-1}^T, and (workgroup 0, i = d) S_dd -= A_{d,k-1} A_{d,k-1}^T
+        to_lds(As, va);
+        to_lds(Bs, vb);
+        __syncthreads();
+        tile_product(acc);
+        sub(cv, acc, false);
+        if (lead) {
+            __syncthreads();
+            to_lds(Bs, va);
+            __syncthreads();
+            tile_product(acc);
+            sub(dv, acc, true);
+        }
         __syncthreads();  // every wave is done with As / Bs
     }
-    // the updated block into As (for the diagonal block: the T area of chol_diag_kernel, upper part 0)
+    if (k >= 0) {  // L_ik = S_ik L_kk^-T
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                    As[r][c] = cv[ti][tj][q];
+                }
+        to_lds(Bs, vl);
+        __syncthreads();
+        tile_product(acc);
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                    C[(size_t)r * n + c] = acc[ti][tj][q];
+                }
+        if (!lead) return;
+        __syncthreads();
+        // column k: S_dd -= L_dk L_dk^T with the panel block just formed (the stored values)
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                    As[r][c] = acc[ti][tj][q];
+                    Bs[r][c] = acc[ti][tj][q];
+                }
+        __syncthreads();
+        d4 acc2[2][2];
+        tile_product(acc2);
+        sub(dv, acc2, true);
+        __syncthreads();
+    }
+    // the diagonal block d: into the T area (As, upper part 0), factor, L_dd and L_dd^-1 out
+    double* T = dyn;
+    double* X = T + NB * TLD;
+    double* LB = X + NB * TLD;
+    double* LT = LB + 4 * 256;
+    double* P = LT + 256;
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -840,62 +933,20 @@ __global__ void __launch_bounds__(256) chol_step_kernel(double* S, int n, int k,
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
-                As[r][c] = cv[ti][tj][q];
+                As[r][c] = dv[ti][tj][q];
             }
-    if (diag) {
-        double* T = dyn;
-        double* X = T + NB * TLD;
-        double* LB = X + NB * TLD;
-        double* LT = LB + 4 * 256;
-        double* P = LT + 256;
-        for (int e = threadIdx.x; e < NB * NB; e += 256) X[(e >> 6) * TLD + (e & 63)] = 0.0;
-        __syncthreads();
-        const int bad = diag_block_lds(T, X, LB, LT, P, bad_s);
-        if (!bad) {
-            double* Li = Linv + (size_t)k * NB * NB;
-            for (int e = threadIdx.x; e < NB * NB; e += 256) {
-                const int r = e >> 6, c = e & 63;
-                if (c <= r) C[(size_t)r * n + c] = T[r * TLD + c];
-                st_sc1(Li + e, X[r * TLD + c]);
-            }
-        } else if (threadIdx.x == 0) {
-            *fail = 1;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store((gint*)flag, bad ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int e = threadIdx.x; e < NB * NB; e += 256) X[(e >> 6) * TLD + (e & 63)] = 0.0;
+    __syncthreads();
+    if (diag_block_lds(T, X, LB, LT, P, bad_s)) {
+        if (threadIdx.x == 0) *fail = 1;
         return;
     }
-    if (threadIdx.x == 0) {
-        const bool arrived = flag_wait(flag);
-        ok_s = arrived && __hip_atomic_load((gint*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
-        if (!arrived) *tmo = 1;  // a device fault, not a failed factorisation
+    double* Li = Linv + (size_t)d * NB * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += 256) {
+        const int r = e >> 6, c = e & 63;
+        if (c <= r) D[(size_t)r * n + c] = T[r * TLD + c];
+        Li[e] = X[r * TLD + c];
     }
-    __syncthreads();
-    if (!ok_s) return;
-    {   // L_kk^-1 (published with sc1 stores) into Bs with sc1 loads, all in flight before the LDS stores
-        const double* Li = Linv + (size_t)k * NB * NB;
-        constexpr int PER = NB * NB / 256;
-        double v[PER];
-#pragma unroll
-        for (int u = 0; u < PER; ++u) v[u] = ld_sc1(Li + threadIdx.x + 256 * u);
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int e = threadIdx.x + 256 * u;
-            Bs[e / NB][e % NB] = v[u];
-        }
-    }
-    __syncthreads();
-    d4 acc[2][2];
-    for (int a = 0; a < 2; ++a)
-        for (int b = 0; b < 2; ++b) acc[a][b] = d4{0, 0, 0, 0};
-    mfma_tile_ABt(As, Bs, acc, wid, lane);
-    for (int ti = 0; ti < 2; ++ti)
-        for (int tj = 0; tj < 2; ++tj)
-            for (int q = 0; q < 4; ++q) {
-                const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
-                C[(size_t)r * n + c] = acc[ti][tj][q];
-            }
 }
 
 // Two 64-row blocks per workgroup (TG): a hand-off per pair instead of per block; the second
@@ -1292,11 +1343,10 @@ hipError_t gba_cholesky_attributes() {
     hipError_t e = hipFuncSetAttribute((const void*)chol_diag_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)CHOL_DIAG_LDS);
     if (e == hipSuccess)
-        e = hipFuncSetAttribute((const void*)chol_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        e = hipFuncSetAttribute((const void*)chol_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)CHOL_DIAG_LDS);
     return e;
 }
-constexpr int kGbaFuseM = 96;  // chol_step_kernel for steps with at most this many block rows (config 5: every step)
 constexpr long long kGbaFuseTrail = 2500;  // trailing updates of at most this many tiles in the next step's launch
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
@@ -1326,41 +1376,56 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
         return hipGetLastError();
     }
     hipError_t e;
-    // fused steps (chol_step_kernel) once the chain, not the trailing update, bounds a step: panel
-    // workgroups wait for the diagonal block, so early steps (large trailing updates on the side
-    // stream) keep the separate launches
-    static const int fuse_m = [] {
-        const char* v = std::getenv("VIO_GBA_FUSE_M");
-        return v ? std::atoi(v) : kGbaFuseM;
+    // trailing updates of at most fuse_trail tiles (the late steps, where the cross-stream round trip of
+    // the look-ahead costs more than the update) ride in the next launch; larger ones overlap it on the
+    // side stream
+    static const long long fuse_trail = [] {
+        const char* v = std::getenv("VIO_GBA_FUSE_TRAIL");
+        return v ? std::atoll(v) : kGbaFuseTrail;
     }();
-    int* sflag = A.flags + FLAG_STRIDE * (2 * (size_t)nblk + 1);
-    if ((e = hipMemsetAsync(sflag, 0, sizeof(int) * FLAG_STRIDE * (size_t)nblk, s)) != hipSuccess) return e;
-    // trail: tiles of step k-1's trailing update (part 2) run as extra workgroups of step k's launch
-    auto step = [&](int k, int trail) {  // column k-1's update of block column k (k > 0), diagonal block k, panel k
-        const int m = nblk - k - 1;
-        if (m + 1 <= fuse_m) {
-            hipLaunchKernelGGL(chol_step_kernel, dim3(m + 1 + trail), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv,
-                               fail, sflag + FLAG_STRIDE * k, tmo, trail);
-            return;
+    // VIO_GBA_FUSE_M=0 (A/B tests): separate update / diagonal / panel launches per step instead of the
+    // chained launches
+    static const bool separate = [] {
+        const char* v = std::getenv("VIO_GBA_FUSE_M");
+        return v && std::atoi(v) == 0;
+    }();
+    if (!separate) {
+        // chained: launch k forms the panels of block column k and factors diagonal block k+1
+        // (chol_chain_kernel); column k-1's trailing update (part 3) runs inside it or beside it on the
+        // side stream, and launch k+1 follows both
+        hipLaunchKernelGGL(chol_chain_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, -1, A.Linv, fail, 0);
+        for (int k = 0; k + 1 < nblk; ++k) {
+            const int m = nblk - k - 1;  // panel block rows of column k
+            const long long tiles = k > 0 ? (long long)m * (m + 1) / 2 - 1 : 0;  // part 3 of step k-1
+            const bool side = tiles > fuse_trail;
+            if (side) {
+                if ((e = hipEventRecord(ev_panel, s)) != hipSuccess) return e;  // panel k-1 final
+                if ((e = hipStreamWaitEvent(r, ev_panel, 0)) != hipSuccess) return e;
+                hipLaunchKernelGGL(chol_syrk_kernel, dim3((unsigned)tiles), dim3(256), 0, r, A.S, n, k - 1, 3);
+                if ((e = hipEventRecord(ev_rest, r)) != hipSuccess) return e;
+            }
+            const int trail = side ? 0 : (int)tiles;
+            hipLaunchKernelGGL(chol_chain_kernel, dim3(m + trail), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv,
+                               fail, trail);
+            if (side && (e = hipStreamWaitEvent(s, ev_rest, 0)) != hipSuccess) return e;
         }
+        return hipGetLastError();
+    }
+    // separate launches: step k = column k-1's update of block column k (k > 0), diagonal block k, panel
+    // k; trail: tiles of step k-1's trailing update (part 2) before them
+    auto step = [&](int k, int trail) {
+        const int m = nblk - k - 1;
         if (trail > 0)
             hipLaunchKernelGGL(chol_syrk_kernel, dim3(trail), dim3(256), 0, s, A.S, n, k - 1, 2);
         if (k > 0) hipLaunchKernelGGL(chol_syrk_kernel, dim3(m + 1), dim3(256), 0, s, A.S, n, k - 1, 1);
         hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), CHOL_DIAG_LDS, s, A.S, n, k, A.Linv, fail);
         if (m > 0) hipLaunchKernelGGL(chol_trsm_kernel, dim3(m), dim3(256), 0, s, A.S, n, k, (const double*)A.Linv);
     };
-    // trailing updates of at most fuse_trail tiles (the late steps, where the cross-stream round trip of
-    // the look-ahead costs more than the update) ride in the next step's launch; larger ones overlap it on
-    // the side stream
-    static const long long fuse_trail = [] {
-        const char* v = std::getenv("VIO_GBA_FUSE_TRAIL");
-        return v ? std::atoll(v) : kGbaFuseTrail;
-    }();
     step(0, 0);
     for (int k = 0; k + 1 < nblk; ++k) {
         const int m = nblk - k - 1;  // trailing block rows of step k
         const long long tiles = (long long)(m - 1) * m / 2;  // its trailing update right of block column k+1
-        if (m >= 2 && tiles <= fuse_trail && m <= fuse_m) {
+        if (m >= 2 && tiles <= fuse_trail) {
             step(k + 1, (int)tiles);
             continue;
         }
