@@ -1379,79 +1379,90 @@ __global__ void __launch_bounds__(256) gftt_hist_kernel(GfArgs G) {
         if (h[b]) atomicAdd(&G.hist[b], h[b]);
 }
 
-// cut bucket: the highest buckets holding >= topk_target candidates (never more than topk_cap).
-// One workgroup: the histogram goes to LDS, suffix sums by a block scan, then the same top-down
-// walk as a sequential loop would make (first bucket from the top where the running count reaches
-// the target, or where the next nonempty bucket would overflow the buffer).
-constexpr int GC_THREADS = 1024;
-__global__ void __launch_bounds__(GC_THREADS) gftt_cut_kernel(GfArgs G) {
-    constexpr int PER = GF_BUCKETS / GC_THREADS;
-    __shared__ unsigned int suf[GF_BUCKETS + 1];  // suf[b] = sum of hist[b..]
-    __shared__ unsigned int part[GC_THREADS];
-    __shared__ int s_cut;
-    const int t = threadIdx.x;
-    // thread t owns buckets [t*PER, t*PER+PER): local suffix sums, then a scan over threads (top-down)
-    unsigned int h[PER];
+// cut bucket: the highest buckets holding >= topk_target candidates (never more than topk_cap), the
+// same top-down walk as a sequential loop would make (first bucket from the top where the running
+// count reaches the target, or where the next nonempty bucket would overflow the buffer).  Computed
+// by every workgroup of the top-K gather from the final histogram (8 KB from L2) instead of a
+// one-workgroup launch between the histogram and the gather: thread t owns buckets [8t, 8t+8), suffix
+// sums by a wave scan plus the four wave totals, the stopping bucket by a max over threads.  Returns
+// the cut; *below_empty: no candidate below it.  cs: LDS scratch of the workgroup.
+constexpr int CUT_PER = GF_BUCKETS / 256;
+struct CutShared {
+    unsigned int wtot[4], wmax[4], suf_cut;
+    int cut;
+};
+__device__ int gftt_cut_block(const GfArgs& G, CutShared& cs, unsigned int& below_empty) {
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    unsigned int h[CUT_PER];
     unsigned int loc = 0;
 #pragma unroll
-    for (int i = PER - 1; i >= 0; --i) { h[i] = G.hist[t * PER + i]; loc += h[i]; }
-    part[t] = loc;
-    __syncthreads();
-    for (int off = 1; off < GC_THREADS; off <<= 1) {  // inclusive suffix scan over threads
-        unsigned int v = t + off < GC_THREADS ? part[t + off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
+    for (int i = CUT_PER - 1; i >= 0; --i) {
+        h[i] = G.hist[t * CUT_PER + i];
+        loc += h[i];
     }
-    unsigned int run = t + 1 < GC_THREADS ? part[t + 1] : 0u;
+    unsigned int sfx = loc;  // sum of loc over lanes >= lane of the wave
 #pragma unroll
-    for (int i = PER - 1; i >= 0; --i) { run += h[i]; suf[t * PER + i] = run; }
-    if (t == 0) { suf[GF_BUCKETS] = 0; s_cut = GF_BUCKETS; }
-    __syncthreads();
-    // sequential semantics: walking b down from the top, cum = suf[b+1] before bucket b;
-    // stop (cut = b+1 ... ) at the first nonempty b with cum + c > cap (cut stays above b), or
-    // after taking b when cum + c >= target (cut = b); empty buckets extend the cut downward.
-    // The walk ends at the largest b satisfying either condition; cut = b (take) or the lowest
-    // bucket above b that was reached, which is b + 1 after empty buckets are skipped upward.
-    int cand = -1;  // largest stopping bucket and its kind
-    for (int i = PER - 1; i >= 0; --i) {
-        const int b = t * PER + i;
-        const unsigned int c = h[i];
-        if (c == 0) continue;
-        const unsigned int cum = suf[b + 1];
-        if (cum + c > G.topk_cap || cum + c >= G.topk_target) { cand = b; break; }
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned int v = (unsigned int)__shfl_down((int)sfx, off, 64);
+        if (lane + off < 64) sfx += v;
     }
-    // max over threads of the stopping bucket
-    part[t] = (unsigned int)(cand + 1);
+    if (lane == 0) cs.wtot[wid] = sfx;
     __syncthreads();
-    for (int off = GC_THREADS / 2; off > 0; off >>= 1) {
-        if (t < off) part[t] = max(part[t], part[t + off]);
-        __syncthreads();
-    }
-    if (t == 0) {
-        const int bstop = (int)part[0] - 1;
-        int cut;
-        if (bstop < 0) {
-            cut = 0;  // never stopped: the walk reaches bucket 0 (every bucket taken or empty)
-        } else {
-            const unsigned int c = G.hist[bstop];
-            const unsigned int cum = suf[bstop + 1];
-            if (cum + c > G.topk_cap) {
-                // not taken: cut = the lowest bucket above bstop reached by the walk = bstop + 1
-                // (buckets bstop+1 .. were taken or empty)
-                cut = bstop + 1;
-            } else {
-                cut = bstop;  // taken and the target is reached
+    unsigned int above = 0;  // threads of later waves
+    for (int q = wid + 1; q < 4; ++q) above += cs.wtot[q];
+    const unsigned int total = cs.wtot[0] + cs.wtot[1] + cs.wtot[2] + cs.wtot[3];  // every candidate
+    const unsigned int run0 = sfx + above - loc;  // buckets above this thread's
+    // the thread's highest stopping bucket (nonempty, cum + c over the buffer or at the target)
+    int cand = -1;
+    unsigned int cum_c = 0, c_c = 0;
+    {
+        unsigned int cum = run0;
+#pragma unroll
+        for (int i = CUT_PER - 1; i >= 0; --i) {
+            const unsigned int c = h[i];
+            if (cand < 0 && c != 0 && (cum + c > G.topk_cap || cum + c >= G.topk_target)) {
+                cand = t * CUT_PER + i;
+                cum_c = cum;
+                c_c = c;
             }
+            cum += c;
         }
-        G.cut[0] = cut;
-        G.cut[1] = suf[0] - suf[cut < GF_BUCKETS ? cut : GF_BUCKETS] == 0 ? 1 : 0;  // nothing below the cut
     }
+    unsigned int m = (unsigned int)(cand + 1);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, off, 64));
+    if (lane == 0) cs.wmax[wid] = m;
+    if (t == 0) cs.cut = 0;  // never stopped: the walk reaches bucket 0 (every bucket taken or empty)
+    __syncthreads();
+    const int bstop = (int)max(max(cs.wmax[0], cs.wmax[1]), max(cs.wmax[2], cs.wmax[3])) - 1;
+    __syncthreads();  // cs.cut = 0 before the owner's store
+    // not taken (over the buffer): the lowest bucket above bstop reached by the walk, bstop + 1;
+    // taken: the target is reached at bstop
+    if (bstop >= 0 && cand == bstop) cs.cut = cum_c + c_c > G.topk_cap ? bstop + 1 : bstop;
+    if (t == 0) cs.suf_cut = 0;
+    __syncthreads();
+    const int cut = cs.cut;
+    if (cut < GF_BUCKETS && t == cut / CUT_PER) {  // candidates at or above the cut
+        unsigned int sc = run0;
+#pragma unroll
+        for (int i = CUT_PER - 1; i >= 0; --i)
+            if (t * CUT_PER + i >= cut) sc += h[i];
+        cs.suf_cut = sc;
+    }
+    __syncthreads();
+    below_empty = total - cs.suf_cut == 0 ? 1u : 0u;
+    return cut;
 }
 
 __global__ void __launch_bounds__(256) gftt_topk_compact_kernel(GfArgs G) {
+    __shared__ CutShared cs;
+    unsigned int below_empty;
+    const unsigned int cut = (unsigned int)gftt_cut_block(G, cs, below_empty);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the selection pass
+        G.cut[0] = (int)cut;
+        G.cut[1] = (int)below_empty;
+    }
     const unsigned int n = min(*G.n_cand, G.cand_cap);
-    const unsigned int cut = (unsigned int)G.cut[0];
     const int lane = threadIdx.x & 63;
     constexpr int U = 4;  // candidate loads in flight per lane
     const unsigned int stride = gridDim.x * 256;
@@ -1864,10 +1875,15 @@ constexpr int LM_TOPK_LDS = 2048;
 __global__ void __launch_bounds__(256) gftt_lm_topk_kernel(GfArgs G) {
     __shared__ unsigned long long buf[LM_TOPK_LDS];
     __shared__ unsigned int s_n, s_base;
+    __shared__ CutShared cs;
     if (threadIdx.x == 0) s_n = 0;
-    __syncthreads();
+    unsigned int below_empty;
+    const unsigned int cut = (unsigned int)gftt_cut_block(G, cs, below_empty);  // (its barriers order s_n = 0)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the selection pass
+        G.cut[0] = (int)cut;
+        G.cut[1] = (int)below_empty;
+    }
     const float thr = lm_threshold(G);
-    const unsigned int cut = (unsigned int)G.cut[0];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_tiles = G.tiles_x * G.tiles_y;
     for (int tile = blockIdx.x * 4 + wid; tile < n_tiles; tile += gridDim.x * 4) {
@@ -2068,7 +2084,6 @@ hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, h
     hipError_t e = gftt_candidates(g, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(gftt_hist_kernel, dim3(256), dim3(256), 0, st, g);
-    hipLaunchKernelGGL(gftt_cut_kernel, dim3(1), dim3(GC_THREADS), 0, st, g);
     hipLaunchKernelGGL(gftt_topk_compact_kernel, dim3(256), dim3(256), 0, st, g);
     e = gftt_sort_topk(g, sort_tmp, sort_tmp_bytes, st);
     if (e != hipSuccess) return e;
@@ -2085,7 +2100,6 @@ hipError_t launch_gftt_after_lmax(const GfArgs& g, void* sort_tmp, size_t sort_t
     hipLaunchKernelGGL(gftt_tmax_kernel, dim3((n_tiles + 3) / 4), dim3(256), 0, st, g);
     hipLaunchKernelGGL(gftt_dirty_kernel, dim3(n_tiles * (LM_TY / LM_STRIP)), dim3(256), 0, st, g);
     hipLaunchKernelGGL(gftt_lm_hist_kernel, dim3(256), dim3(256), 0, st, g);
-    hipLaunchKernelGGL(gftt_cut_kernel, dim3(1), dim3(GC_THREADS), 0, st, g);
     hipLaunchKernelGGL(gftt_lm_topk_kernel, dim3(256), dim3(256), 0, st, g);
     hipError_t e = gftt_sort_topk(g, sort_tmp, sort_tmp_bytes, st);
     if (e != hipSuccess) return e;
