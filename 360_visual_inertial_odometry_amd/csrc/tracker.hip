@@ -604,56 +604,59 @@ __global__ void __launch_bounds__(RS_THREADS) ransac_raw_kernel(uint32_t seed, u
 }
 
 // PREP: the input compaction (ransac_prep_body) first, in the same workgroup (one launch fewer on the
-// tracker's critical path); the sampler then reads the count from LDS
+// tracker's critical path); the sampler then reads the count from LDS.  Four waves (a sixteen-wave
+// workgroup waits longer for a CU while GFTT pass 1 fills the chip from the side stream): thread t
+// tests the RS_CHUNK contiguous stream words [t RS_CHUNK, (t+1) RS_CHUNK), one block scan of the
+// per-thread accept counts places its accepted draws in stream order.
+constexpr int RS_SAMPLE_THREADS = 256;
+constexpr int RS_CHUNK = 20;
+static_assert(RS_CHUNK % 4 == 0 && RS_RAW % 4 == 0 && RS_SAMPLE_THREADS * RS_CHUNK >= RS_RAW, "sampler chunks");
 template <bool PREP>
-__global__ void __launch_bounds__(RS_THREADS) ransac_sample_kernel(RansacArgs R) {
+__global__ void __launch_bounds__(RS_SAMPLE_THREADS) ransac_sample_kernel(RansacArgs R) {
     __shared__ uint32_t acc[RS_RAW];    // accepted draws (compacted), in stream order
     __shared__ uint8_t len3[RS_RAW];    // 1: a hypothesis starting at draw p consumes exactly 3 draws
-    __shared__ int wsum[RS_THREADS / 64];
-    __shared__ int s_m, s_fallback, s_base;
-    const int n = PREP ? ransac_prep_body<RS_THREADS>(R, wsum, s_base) : *R.n_good;
+    __shared__ int wsum[RS_SAMPLE_THREADS / 64];
+    __shared__ int s_fallback, s_base;
+    const int n = PREP ? ransac_prep_body<RS_SAMPLE_THREADS>(R, wsum, s_base) : *R.n_good;
     if (PREP) __syncthreads();  // wsum is reused below
     if (n < 3 || R.iters <= 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (tid == 0) {
-        s_m = 0;
-        s_fallback = 0;
-    }
-    // the lane's tempered words of every block, loads in flight together
-    uint32_t yw[RS_BLOCKS];
+    const int w0 = tid * RS_CHUNK;
+    uint32_t yw[RS_CHUNK];  // the thread's tempered words (raw: a 256-B aligned allocation)
 #pragma unroll
-    for (int blk = 0; blk < RS_BLOCKS; ++blk) yw[blk] = tid < 624 ? R.raw[624 * blk + tid] : 0u;
-    __syncthreads();
+    for (int q = 0; q < RS_CHUNK / 4; ++q) {
+        const int w = w0 + 4 * q;
+        const uint4 v = w < RS_RAW ? *reinterpret_cast<const uint4*>(R.raw + w) : make_uint4(0u, 0u, 0u, 0u);
+        yw[4 * q] = v.x;
+        yw[4 * q + 1] = v.y;
+        yw[4 * q + 2] = v.z;
+        yw[4 * q + 3] = v.w;
+    }
     const uint32_t range = (uint32_t)n;
     const uint32_t thr = (uint32_t)(-range) % range;
+    auto accepted = [&](int u) {  // uniform_int_distribution's rejection test of word u
+        const uint32_t low = (uint32_t)((uint64_t)yw[u] * range);
+        return w0 + u < RS_RAW && !(low < range && low < thr);
+    };
+    int cnt = 0;
 #pragma unroll
-    for (int blk = 0; blk < RS_BLOCKS; ++blk) {
-        // accept test + compaction (stream order)
-        int accepted = 0;
-        uint32_t val = 0;
-        if (tid < 624) {
-            const uint32_t y = yw[blk];
-            const uint64_t prod = (uint64_t)y * range;
-            const uint32_t low = (uint32_t)prod;
-            accepted = !(low < range && low < thr);
-            val = (uint32_t)(prod >> 32);
-        }
-        const unsigned long long bal = __ballot(accepted);
-        if (lane == 0) wsum[wid] = __popcll(bal);
-        __syncthreads();
-        int off = s_m;
-        for (int q = 0; q < wid; ++q) off += wsum[q];
-        if (accepted) acc[off + __popcll(bal & ((1ull << lane) - 1ull))] = val;
-        __syncthreads();
-        if (tid == 0) {
-            int t = 0;
-            for (int q = 0; q < RS_THREADS / 64; ++q) t += wsum[q];
-            s_m += t;
-        }
-        __syncthreads();
+    for (int u = 0; u < RS_CHUNK; ++u) cnt += accepted(u) ? 1 : 0;
+    int incl = cnt;  // inclusive scan over the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
     }
-    const int M = s_m;
-    for (int p = tid; p < M; p += RS_THREADS)
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int pos = incl - cnt;
+    for (int q = 0; q < wid; ++q) pos += wsum[q];
+#pragma unroll
+    for (int u = 0; u < RS_CHUNK; ++u)
+        if (accepted(u)) acc[pos++] = (uint32_t)(((uint64_t)yw[u] * range) >> 32);
+    const int M = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+    for (int p = tid; p < M; p += RS_SAMPLE_THREADS)
         len3[p] = (p + 2 < M && acc[p] != acc[p + 1] && acc[p] != acc[p + 2] && acc[p + 1] != acc[p + 2]) ? 1 : 0;
     __syncthreads();
     if (wid == 0) {
@@ -1976,10 +1979,12 @@ hipError_t launch_ransac_raw(uint32_t seed, uint32_t* raw, hipStream_t st) {
     return hipGetLastError();
 }
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st) {
-    // the compaction stays a 4-wave workgroup of its own (a 16-wave one, the sampler's, waits longer for a
-    // CU while GFTT pass 1 fills the chip from the side stream: measured slower fused)
-    hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(RP_THREADS), 0, st, r);
-    if (gen_samples) hipLaunchKernelGGL(ransac_sample_kernel<false>, dim3(1), dim3(RS_THREADS), 0, st, r);
+    // with samples to draw: the compaction and the sampler in one 4-wave workgroup (a 16-wave one waits
+    // longer for a CU while GFTT pass 1 fills the chip from the side stream)
+    if (gen_samples)
+        hipLaunchKernelGGL(ransac_sample_kernel<true>, dim3(1), dim3(RS_SAMPLE_THREADS), 0, st, r);
+    else
+        hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(RP_THREADS), 0, st, r);
     if (r.iters > 0) hipLaunchKernelGGL(ransac_hyp_kernel, dim3((r.iters + 3) / 4), dim3(256), 0, st, r);
     hipLaunchKernelGGL(ransac_select_kernel, dim3(1), dim3(256), 0, st, r);
     return hipGetLastError();
