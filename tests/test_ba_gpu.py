@@ -566,7 +566,7 @@ ctx.close()
 def test_global_ba_solve_paths_bitwise(vio, tmp_path):
     """Every schedule of the global path gives the default's solution bits: the per-step triangular
     solves (VIO_GBA_PERSISTENT_SOLVE=0, the fallback beyond 256 blocks: every row dot reduced the same
-    way), separate update / diagonal / panel launches instead of the fused step (VIO_GBA_FUSE_M=0),
+    way), separate update / diagonal / panel launches instead of the chained ones (VIO_GBA_FUSE_M=0),
     direct launches instead of the replayed graph (VIO_GBA_GRAPH=0), every trailing update on the
     side stream (VIO_GBA_FUSE_TRAIL=0) and a threshold that puts the larger early updates on the side
     stream and the later ones inside the next step's launch within one factorisation
