@@ -1,9 +1,9 @@
 #!/bin/bash
-# tracker: bitwise GPU tests, stage times, kernel stats (tools/gpu_trk7.sh), then the HBM traffic of the
+# tracker: pipeline timeline (tools/gpu_trk_timeline.sh), then the HBM traffic of the
 # config-1 pipeline (FETCH_SIZE / WRITE_SIZE in separate passes over tools/trk_time.py)
 set -u
 tag=${1:-trk}
-bash tools/gpu_trk7.sh $tag || exit $?
+bash tools/gpu_trk_timeline.sh $tag || exit $?
 mkdir -p gpurun_out/pmc_$tag
 export TMPDIR=/tmp
 for ctr in FETCH_SIZE WRITE_SIZE; do
