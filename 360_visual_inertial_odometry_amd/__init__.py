@@ -43,7 +43,7 @@ EXPORTS = [
     "vio_window_link_mappoints", "vio_window_add_keyframe", "vio_window_triangulation_candidates",
     "vio_window_commit_triangulation", "vio_window_triangulate", "vio_window_keyframes", "vio_window_num_mappoints",
     "vio_window_mappoint", "vio_window_mappoint_observations", "vio_window_frame_mappoints", "vio_window_map_view",
-    "vio_window_apply_update",
+    "vio_window_apply_update", "vio_lie_eval",
 ]
 
 
@@ -107,6 +107,7 @@ def lib():
     L.vio_triangulate.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp]
     L.vio_triangulate_device.argtypes = [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp, vp]
     L.vio_triangulate_kernel_ms.argtypes = [vp, C.POINTER(C.c_double)]
+    L.vio_lie_eval.argtypes = [vp, C.c_int, vp, C.c_int, vp]
     L.vio_load_camera_timestamps.argtypes = [C.c_char_p, vp, C.c_int, C.POINTER(C.c_int)]
     L.vio_load_imu_csv.argtypes = [C.c_char_p, vp, C.c_int, C.POINTER(C.c_int)]
     L.erp_resize_area.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, C.c_int, C.c_int]
@@ -191,6 +192,17 @@ class Context:
     def set_ba_route(self, route):
         """vio_ctx_set_ba_route: execution route of later window solves on this context."""
         self.check(lib().vio_ctx_set_ba_route(self.h, int(route)), "vio_ctx_set_ba_route")
+
+    LIE_SO3_EXP, LIE_SE3_EXP, LIE_IMU_LOG, LIE_SO3D_EXP, LIE_SO3D_LOG = range(5)
+    _LIE_IO = {0: (3, 9), 1: (6, 12), 2: (9, 3), 3: (3, 9), 4: (9, 3)}
+
+    def lie_eval(self, op, x):
+        """vio_lie_eval: the device Lie maths of the BA factors (LIE_* ops) over the rows of x."""
+        ni, no = self._LIE_IO[int(op)]
+        a = np.ascontiguousarray(np.asarray(x, np.float64).reshape(-1, ni))
+        out = np.zeros((max(len(a), 1), no), np.float64)
+        self.check(lib().vio_lie_eval(self.h, int(op), _p(a), len(a), _p(out)), "vio_lie_eval")
+        return out[:len(a)]
 
     def ba_solve(self, problems):
         """Solve a list of BaProblem windows in one launch; returns list of result dicts."""

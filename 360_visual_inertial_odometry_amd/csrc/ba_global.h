@@ -110,6 +110,9 @@ hipError_t gba_launch_step_prep(const GbaArgs& A, double radius, double* partial
 hipError_t gba_cholesky_attributes();
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s);
 hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s);
+// workgroups of the persistent triangular solves gba_launch_solve enqueues (0: the per-step kernels), for
+// the co-residency ledger (residency.h)
+int gba_solve_persistent_wgs(const GbaArgs& A);
 hipError_t gba_launch_backsub(const GbaArgs& A, double* partial, double* out_nonfinite, hipStream_t s);
 hipError_t gba_launch_model(const GbaArgs& A, double* partial, double* out3, hipStream_t s);
 // VIBA terms (ba_kernel.hip, next to the window solver's IMU factor code)

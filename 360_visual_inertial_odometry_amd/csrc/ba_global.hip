@@ -1441,13 +1441,20 @@ hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     }
     return hipGetLastError();
 }
-hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {
-    const int n = A.nfp, nblk = n / NB;
-    static const bool per_step = [] {  // VIO_GBA_PERSISTENT_SOLVE=0: the per-step kernels (A/B tests)
+static bool gba_per_step_solve() {  // VIO_GBA_PERSISTENT_SOLVE=0: the per-step kernels (A/B tests)
+    static const bool per_step = [] {
         const char* v = std::getenv("VIO_GBA_PERSISTENT_SOLVE");
         return v && v[0] == '0';
     }();
-    if (A.flags && nblk >= 1 && nblk <= 256 && !per_step) {  // every block resident: the persistent solves
+    return per_step;
+}
+int gba_solve_persistent_wgs(const GbaArgs& A) {
+    const int nblk = A.nfp / NB;
+    return A.flags && nblk >= 1 && nblk <= 256 && !gba_per_step_solve() ? (nblk + TG - 1) / TG : 0;
+}
+hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {
+    const int n = A.nfp, nblk = n / NB;
+    if (gba_solve_persistent_wgs(A)) {  // every block resident: the persistent solves
         // y: the unset pattern (polled by the forward solve; x is reset by the forward kernel); the
         // timeout word was cleared before the Cholesky (gba_launch_cholesky)
         hipError_t e = hipMemsetAsync(A.yv, 0xff, sizeof(double) * (size_t)n, s);

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "ba_global.h"
+#include "residency.h"
 #include "ba_types.h"
 #include "ctx.h"
 
@@ -286,7 +287,11 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     auto factor_and_solve = [&]() -> hipError_t {
         if (!use_graph) {
             hipError_t e = gba_launch_cholesky(A, dfail, st);
-            return e == hipSuccess ? gba_launch_solve(A, st) : e;
+            if (e != hipSuccess) return e;
+            ResidencyGuard rg(st, gba_solve_persistent_wgs(A));  // (residency.h)
+            if ((e = rg.status()) != hipSuccess) return e;
+            e = gba_launch_solve(A, st);
+            return e == hipSuccess ? rg.commit() : e;
         }
         if (!chol_graph.g) {
             hipGraph_t g = nullptr;
@@ -300,7 +305,11 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             if (g) (void)hipGraphDestroy(g);
             if (e != hipSuccess) return e;
         }
-        return hipGraphLaunch(chol_graph.g, st);
+        // the graph ends with the persistent triangular solves: reserved for the whole replay (residency.h)
+        ResidencyGuard rg(st, gba_solve_persistent_wgs(A));
+        hipError_t e = rg.status();
+        if (e == hipSuccess) e = hipGraphLaunch(chol_graph.g, st);
+        return e == hipSuccess ? rg.commit() : e;
     };
     GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));
     GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0.data(), sizeof(double) * 3 * L, hipMemcpyHostToDevice, st));

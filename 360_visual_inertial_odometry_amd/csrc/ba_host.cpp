@@ -16,6 +16,7 @@
 
 #include "ba_types.h"
 #include "ctx.h"
+#include "residency.h"
 
 namespace vio360 {
 
@@ -29,9 +30,12 @@ const char* ba_phases_failed_launch();
 hipError_t ba_phases_prepare(const BaWin* hw, int n);
 int ba_cluster_members(const BaWin* hw, int n, int max_per_window);
 hipError_t launch_ba_cluster(const BaPools& P, int n, int C, hipStream_t stream);
+hipError_t ba_cluster_prelaunch(const BaPools& P, int n, hipStream_t stream);
 bool global_ba_applicable(const vio_ba_problem& p);
 int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out);
 size_t ba_ws_extra_doubles();
+hipError_t launch_lie_ba(int op, const double* in, double* out, int n, hipStream_t stream);
+hipError_t launch_lie_init(int op, const double* in, double* out, int n, hipStream_t stream);
 
 void set_error(vio_ctx* ctx, const std::string& msg) {
     if (ctx) ctx->last_error = msg;
@@ -509,9 +513,7 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     const char* what = "ba_window_kernel launch";
     if (cluster) {
         what = "ph_cluster_kernel";
-        if (!d.reusable) {
-            e = launch_ba_cluster(d.P, d.n, d.cluster_C, ctx->stream);
-        } else if (!d.phase_graph) {
+        if (d.reusable && !d.phase_graph) {  // the kernel alone is captured; its hand-off words are cleared per run
             hipGraph_t g = nullptr;
             e = hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal);
             if (e == hipSuccess) {
@@ -522,7 +524,15 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
             if (e == hipSuccess) e = hipGraphInstantiate(&d.phase_graph, g, nullptr, nullptr, 0);
             if (g) (void)hipGraphDestroy(g);
         }
-        if (e == hipSuccess && d.reusable) e = hipGraphLaunch(d.phase_graph, ctx->stream);
+        if (e == hipSuccess) e = ba_cluster_prelaunch(d.P, d.n, ctx->stream);
+        if (e == hipSuccess) {
+            // every member of every window resident at once, also beside other threads' persistent launches
+            ResidencyGuard rg(ctx->stream, d.cluster_C * d.n);
+            e = rg.status();
+            if (e == hipSuccess) e = d.reusable ? hipGraphLaunch(d.phase_graph, ctx->stream)
+                                                : launch_ba_cluster(d.P, d.n, d.cluster_C, ctx->stream);
+            if (e == hipSuccess) e = rg.commit();
+        }
     } else if (phases) {
         // ~70 launches per solve: a reusable batch captures them once into a graph (same arguments
         // every run) and replays it; a one-shot solve launches them directly
@@ -571,6 +581,27 @@ int vio_abi_version(void) { return VIO360_ABI_VERSION; }
 int vio_ctx_set_ba_route(vio_ctx* ctx, int route) {
     if (!ctx || route < VIO_BA_ROUTE_AUTO || route > VIO_BA_ROUTE_CLUSTER) return VIO_EINVAL;
     ctx->ba_route = route;
+    return VIO_OK;
+}
+
+int vio_lie_eval(vio_ctx* ctx, int op, const double* in, int n, double* out) {
+    static const int kIn[5] = {3, 6, 9, 3, 9}, kOut[5] = {9, 12, 3, 9, 3};
+    if (!ctx || op < VIO_LIE_SO3_EXP || op > VIO_LIE_SO3D_LOG || n < 0 || (n > 0 && (!in || !out))) return VIO_EINVAL;
+    if (n == 0) return VIO_OK;
+    const size_t bi = sizeof(double) * kIn[op] * (size_t)n, bo = sizeof(double) * kOut[op] * (size_t)n;
+    auto* d = static_cast<char*>(ctx_buffer(ctx, kSlotLie, bi + bo));
+    if (!d) {
+        set_error(ctx, "vio_lie_eval: device allocation failed");
+        return VIO_ENOMEM;
+    }
+    VIO_DEVICE(ctx);
+    double* din = reinterpret_cast<double*>(d);
+    double* dout = reinterpret_cast<double*>(d + bi);
+    VIO_HIP(ctx, hipMemcpyAsync(din, in, bi, hipMemcpyHostToDevice, ctx->stream));
+    VIO_HIP(ctx, op <= VIO_LIE_IMU_LOG ? launch_lie_ba(op, din, dout, n, ctx->stream)
+                                       : launch_lie_init(op, din, dout, n, ctx->stream));
+    VIO_HIP(ctx, hipMemcpyAsync(out, dout, bo, hipMemcpyDeviceToHost, ctx->stream));
+    VIO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return VIO_OK;
 }
 

@@ -2197,6 +2197,23 @@ hipError_t launch_ba_pack(const BaPools& P, int n, uint8_t* dst, int64_t rec_byt
     return hipGetLastError();
 }
 
+// vio_lie_eval (tests): the window factors' Lie maths, one lane per input, compiled like the factors
+__global__ void lie_ba_kernel(int op, const double* in, double* out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (op == VIO_LIE_SO3_EXP) {
+        so3_exp(in + 3 * i, out + 9 * i);
+    } else if (op == VIO_LIE_SE3_EXP) {
+        se3_exp(in + 6 * i, out + 12 * i, out + 12 * i + 9);
+    } else {
+        imu_log(in + 9 * i, out + 3 * i);
+    }
+}
+hipError_t launch_lie_ba(int op, const double* in, double* out, int n, hipStream_t stream) {
+    hipLaunchKernelGGL(lie_ba_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, op, in, out, n);
+    return hipGetLastError();
+}
+
 size_t ba_shared_bytes() { return sizeof(BaShared); }
 size_t ba_ws_extra_doubles() { return ba_ws_extra(); }
 

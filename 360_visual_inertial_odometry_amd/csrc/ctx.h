@@ -45,6 +45,8 @@ enum { kSlotRecords = 15 };
 enum { kSlotImuInit = 16 };
 // vio_mono_init_solve inputs, outputs and scratch
 enum { kSlotMonoInit = 17 };
+// vio_lie_eval inputs and outputs
+enum { kSlotLie = 18 };
 
 // Selects a device for the rest of the enclosing scope and restores the calling thread's current
 // device on exit, so a C-ABI call never leaves the caller's thread on the context's device (a process

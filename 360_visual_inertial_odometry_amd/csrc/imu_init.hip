@@ -633,7 +633,20 @@ __global__ __launch_bounds__(kThreads) void imu_init_kernel(const IiProb* __rest
     for (int k = t; k < 3 * F; k += kThreads) vel_out[p.vinit + k] = S.vel[k];
 }
 
+// vio_lie_eval (tests): SO3d::Exp with its projection and SO3d::Log, one lane per input
+__global__ void lie_init_kernel(int op, const double* in, double* out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (op == VIO_LIE_SO3D_EXP) ii_so3_exp(in + 3 * i, out + 9 * i);
+    else ii_so3d_log(in + 9 * i, out + 3 * i);
+}
+
 }  // namespace
+
+hipError_t launch_lie_init(int op, const double* in, double* out, int n, hipStream_t stream) {
+    hipLaunchKernelGGL(lie_init_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, op, in, out, n);
+    return hipGetLastError();
+}
 }  // namespace vio360
 
 using namespace vio360;

@@ -31,79 +31,96 @@ FP64_PEAK = 78.6e12  # MI355X FP64 vector (= FP64 matrix) peak, AMD spec (SURVEY
 TRACKER_PREFIXES = ("pyr_down_kernel", "lk_kernel", "ransac_", "gftt_", "disc_mask_kernel", "rocprim")
 
 
-def pmc_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/gpu_pmc.sh ->
-    tools/pmc_summary.py -> profiles/r*_pmc_traffic.json; reads corrected x2 for gfx950).  PMC counters
-    cannot be collected inside this process, so the newest committed summary of the same workload is
-    reported (None when absent)."""
+def newest_profile(suffix):
+    """The newest committed PMC summary profiles/r<round><letters>_<suffix>.json, ordered by its round
+    number and session letters (not by file-name order), with its repo-relative path and the commit it
+    was recorded at (the summary's "commit" field where the profiling script wrote one): (data, source)
+    or (None, None).  The source goes into the bench line next to every traffic figure taken from it."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
-    if not files:
+    import re
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", f"r*_{suffix}.json")):
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        if m:
+            key = (int(m.group(1)), len(m.group(2)), m.group(2))
+            if best is None or key > best[0]:
+                best = (key, f)
+    if best is None:
         return None, None
-    with open(files[-1]) as f:
-        return json.load(f)["kernels"], os.path.relpath(files[-1], ROOT)
+    with open(best[1]) as fh:
+        d = json.load(fh)
+    src = os.path.relpath(best[1], ROOT)
+    if d.get("commit"):
+        src += f"@{d['commit'][:12]}"
+    return d, src
+
+
+def traffic_fields(pair):
+    """{"traffic": bytes, "traffic_source": profile@commit} of a (bytes, source) pair."""
+    v, src = pair
+    return {"traffic": v, "traffic_source": src}
+
+
+def pmc_traffic():
+    """PMC summary of the whole bench workload (profiles/r*_pmc_traffic.json): (kernels, source)."""
+    d, src = newest_profile("pmc_traffic")
+    return (d["kernels"], src) if d else (None, None)
 
 
 def ba_traffic(args):
     """PMC HBM bytes of one 256-window x 10-iteration step of the phase route: every kernel of the
     step's graph, bytes per launch x launches per step (tools/gpu_pmc_ba.sh over tools/ba_batch_run.py
-    -> profiles/r*_pmc_traffic_ba.json; a step = one ph_setup_kernel launch)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_ba.json")))
-    if not files or args.windows != 256 or args.lm_iters != 10:
-        return None
-    with open(files[-1]) as f:
-        k = json.load(f)["kernels"]
+    -> profiles/r*_pmc_traffic_ba.json; a step = one ph_setup_kernel launch).  (bytes, source)."""
+    d, src = newest_profile("pmc_traffic_ba")
+    if not d or args.windows != 256 or args.lm_iters != 10:
+        return None, None
+    k = d["kernels"]
     if "ph_setup_kernel" not in k:
-        return None
+        return None, None
     steps = k["ph_setup_kernel"]["dispatches"]
-    return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items() if n.startswith("ph_")) / steps
+    return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items() if n.startswith("ph_")) / steps, src
 
 
 def cfg2_traffic():
     """PMC HBM bytes of one config-2 window solve (10 fixed LM iterations, one window, default route):
     every window-BA kernel's bytes per launch x launches, per solve (tools/gpu_pmc_cfg2.sh over
     tools/ba_batch_run.py -> profiles/r*_pmc_traffic_cfg2.json; a solve = one ph_cluster_kernel or
-    ph_setup_kernel launch)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_cfg2.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        k = json.load(f)["kernels"]
+    ph_setup_kernel launch).  (bytes, source)."""
+    d, src = newest_profile("pmc_traffic_cfg2")
+    if not d:
+        return None, None
+    k = d["kernels"]
     head = "ph_cluster_kernel" if "ph_cluster_kernel" in k else "ph_setup_kernel" if "ph_setup_kernel" in k else None
     if head is None:
-        return None
+        return None, None
     return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items() if n.startswith("ph_")) / \
-        k[head]["dispatches"]
+        k[head]["dispatches"], src
 
 
 def klt_traffic():
     """PMC HBM bytes of one ERP-KLT pipeline run: per-launch bytes x launches per run (lk_kernel runs once).
     Source: the newest tracker-only summary (tools/gpu_trk_pmc.sh -> profiles/r*_pmc_traffic_klt.json),
-    else the bench-wide one."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_klt.json")))
-    if files:
-        with open(files[-1]) as f:
-            k = json.load(f)["kernels"]
+    else the bench-wide one.  (bytes, source)."""
+    d, src = newest_profile("pmc_traffic_klt")
+    if d:
+        k = d["kernels"]
     else:
         k, src = pmc_traffic()
     if not k or "lk_kernel" not in k:
-        return None
+        return None, None
     runs = k["lk_kernel"]["dispatches"]
     # every kernel the pipeline launches once or more per run (rocprim: the top-K key sort); the one-off
     # kernels of the standalone GFTT that picks the bench's start points run fewer times and are left out
     return sum(v["hbm_bytes_per_launch"] * v["dispatches"] for n, v in k.items()
-               if n.startswith(TRACKER_PREFIXES) and v["dispatches"] >= runs) / runs
+               if n.startswith(TRACKER_PREFIXES) and v["dispatches"] >= runs) / runs, src
 
 
 def kernel_traffic(name):
-    """PMC HBM bytes per launch of one kernel from the committed summary (None when absent)."""
+    """PMC HBM bytes per launch of one kernel from the committed summary: (bytes, source) or (None, None)."""
     k, src = pmc_traffic()
     if not k or name not in k:
-        return None
-    return k[name]["hbm_bytes_per_launch"]
+        return None, None
+    return k[name]["hbm_bytes_per_launch"], src
 
 
 def ba_flops_per_iter(prob):
@@ -331,7 +348,7 @@ def config2_bench(vio, synth, ctx, lm_iters, cpu_seconds, want_cpu, windows=256)
         "batched": {"windows": windows, "window_iters_per_s": windows * lm_iters / wallm, "ms_per_step": wallm * 1e3},
         "iterations": res["iterations"],
         "roofline": {"bound": "mfma", "achieved": flops * lm_iters / (kms1 * 1e-3) / 1e12, "peak": FP64_PEAK / 1e12,
-                     "unit": "TFLOP/s", "frac": flops * lm_iters / (kms1 * 1e-3) / FP64_PEAK, "traffic": cfg2_traffic(),
+                     "unit": "TFLOP/s", "frac": flops * lm_iters / (kms1 * 1e-3) / FP64_PEAK, **traffic_fields(cfg2_traffic()),
                      "flops_per_iteration": flops,
                      "note": "one window: latency-bound (the window's serial LM chain); SURVEY §8d flop convention; "
                              "traffic = PMC HBM bytes of one 10-iteration solve (committed profile)"},
@@ -454,7 +471,7 @@ def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
             "peak": 8000.0,
             "unit": "GB/s",
             "frac": alg_bytes / (stage["total"] * 1e-3) / 8.0e12,
-            "traffic": klt_traffic(),
+            **traffic_fields(klt_traffic()),
             "note": "algorithmic 2 B/px (both u8 frames read once) over the whole pipeline's device time; "
                     "traffic = PMC HBM bytes of one pipeline run (all tracker kernels, committed profile)",
         },
@@ -492,14 +509,10 @@ def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
 
 def gba_traffic():
     """PMC HBM bytes of one config-5 LM iteration from the committed summary (tools/gpu_pmc_gba.sh ->
-    profiles/r*_pmc_traffic_gba.json): every kernel's bytes per launch x launches per iteration."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic_gba.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d.get("hbm_bytes_per_iteration")
+    profiles/r*_pmc_traffic_gba.json): every kernel's bytes per launch x launches per iteration.
+    (bytes, source)."""
+    d, src = newest_profile("pmc_traffic_gba")
+    return (d.get("hbm_bytes_per_iteration"), src) if d else (None, None)
 
 
 def global_ba_bench(vio, synth, ctx, lm_iters, want_cpu=False):
@@ -539,7 +552,7 @@ def global_ba_bench(vio, synth, ctx, lm_iters, want_cpu=False):
                 "incl. host assembly, allocation, upload and the final chi2 pass; fixed iterations",
         "final_cost_ratio": r["final_cost"] / r["initial_cost"],
         "roofline": {"bound": "mfma", "achieved": flops / per_iter / 1e12, "peak": FP64_PEAK / 1e12,
-                     "unit": "TFLOP/s", "frac": flops / per_iter / FP64_PEAK, "traffic": gba_traffic(),
+                     "unit": "TFLOP/s", "frac": flops / per_iter / FP64_PEAK, **traffic_fields(gba_traffic()),
                      "flops_per_iteration": flops},
         "cpu_baseline": global_cpu_baseline(vio, synth, w) if want_cpu else None,
     }
@@ -578,7 +591,7 @@ def imu_bench(vio, ctx, steps, cpu_seconds, want_cpu):
         "wall_ms_per_call": wall * 1e3,
         "note": "value over the HIP-event kernel time; wall includes the 3.7 MB sample upload and result download",
         "roofline": {"bound": "latency", "achieved": alg_bytes / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": alg_bytes / (k_ms * 1e-3) / 8.0e12, "traffic": kernel_traffic("imu_preint_kernel"),
+                     "frac": alg_bytes / (k_ms * 1e-3) / 8.0e12, **traffic_fields(kernel_traffic("imu_preint_kernel")),
                      "note": "one lane per interval: a 50-step dependent f32 chain; 2304 lanes = 36 waves"},
         "cpu_baseline": None,
     }
@@ -629,7 +642,7 @@ def tri_bench(vio, ctx, steps, want_cpu):
         "unit": "candidates/s",
         "kernel_ms": k_ms,
         "roofline": {"bound": "hbm", "achieved": alg_bytes / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": alg_bytes / (k_ms * 1e-3) / 8.0e12, "traffic": kernel_traffic("triangulate_kernel"),
+                     "frac": alg_bytes / (k_ms * 1e-3) / 8.0e12, **traffic_fields(kernel_traffic("triangulate_kernel")),
                      "note": "53 B per candidate in/out (poses L2-resident); the f64 one-sided Jacobi "
                              "(~2 kFLOP per candidate) is the actual limiter"},
         "cpu_baseline": None,
@@ -686,7 +699,7 @@ def resize_bench(vio, ctx, steps, want_cpu):
         "unit": "Mpx/s",
         "kernel_ms": k_ms,
         "roofline": {"bound": "hbm", "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": alg / (k_ms * 1e-3) / 8.0e12, "traffic": kernel_traffic("resize_area4_kernel"),
+                     "frac": alg / (k_ms * 1e-3) / 8.0e12, **traffic_fields(kernel_traffic("resize_area4_kernel")),
                      "note": "1 + 1/16 B per source pixel (read once, written at 1/16)"},
         "cpu_baseline": cpu,
     }
@@ -835,7 +848,7 @@ def main():
                 "peak": FP64_PEAK / 1e12,
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK,
-                "traffic": ba_traffic(args),
+                **traffic_fields(ba_traffic(args)),
                 "kernel": f"{head_route}-route step graph (ph_setup, ph_lin, 10 x [ph_prep, ph_schur, ph_solve, "
                           "ph_back], ph_prep, ph_post)",
                 "kernel_avg_ms": kms,

@@ -76,6 +76,22 @@ int vio_layout_check(void);
 #define VIO_BA_ROUTE_CLUSTER 3
 int vio_ctx_set_ba_route(vio_ctx* ctx, int route);
 
+/* Device Lie maths of the BA factors, evaluated for n inputs with the same device code
+   the solvers inline, for parity tests against Ceres' rotation known answers
+   (thirdparty/ceres-solver/internal/ceres/rotation_test.cc:406-589).  Rotations row-major.
+     VIO_LIE_SO3_EXP   in 3 (phi)        -> out 9   SO3d::Exp as the window factors evaluate it
+                                                    (LieUtils.cpp:203-219; no re-projection)
+     VIO_LIE_SE3_EXP   in 6 ([rho, phi]) -> out 12  SE3d::exp: R (9) | t (3) (LieUtils.cpp:305-333)
+     VIO_LIE_IMU_LOG   in 9 (R)          -> out 3   InertialFactorFixedGravity::log_SO3 (Factors.cpp:1507-1519)
+     VIO_LIE_SO3D_EXP  in 3              -> out 9   SO3d::Exp + the SO3d constructor's projection (IMU init)
+     VIO_LIE_SO3D_LOG  in 9              -> out 3   SO3d::Log with its theta ~ pi branch (LieUtils.cpp:221-273) */
+#define VIO_LIE_SO3_EXP 0
+#define VIO_LIE_SE3_EXP 1
+#define VIO_LIE_IMU_LOG 2
+#define VIO_LIE_SO3D_EXP 3
+#define VIO_LIE_SO3D_LOG 4
+int vio_lie_eval(vio_ctx* ctx, int op, const double* in, int n, double* out);
+
 /* ----------------------------------------------------------------------------------------- */
 /* Bundle adjustment / PnP                                                                    */
 

@@ -2556,3 +2556,15 @@ int oracle_imu_init(const vio_imu_init_problem* p, vio_imu_init_result* out) {
     free(sum); free(c.vel); free(c.vel_off); free(c.fac);
     return VIO_OK;
 }
+
+/* ========================================================================================= */
+/* Lie maths test entry points (tests/test_lie_kat.py: Ceres rotation_test.cc known answers)   */
+/* ========================================================================================= */
+/* SO3d::Exp incl. the SO3d constructor's projection (LieUtils.cpp:203-219, 275-288) */
+void oracle_so3_exp(const double* w, double* R) { so3_exp(w, R); }
+/* SE3d::exp (LieUtils.cpp:305-333) */
+void oracle_se3_exp(const double* xi, double* R, double* t) { se3_exp(xi, R, t); }
+/* SO3d::Log (LieUtils.cpp:221-273) */
+void oracle_so3d_log(const double* R, double* w) { so3d_log(R, w); }
+/* InertialFactorFixedGravity::log_SO3 (Factors.cpp:1507-1519) */
+void oracle_imu_log_so3(const double* R, double* w) { imu_log_so3(R, w); }

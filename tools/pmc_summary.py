@@ -7,6 +7,8 @@ as reported.  Output: JSON {kernel: {dispatches, read_bytes_per_launch, write_by
 hbm_bytes_per_launch, fetch_kb_raw, write_kb_raw}} — bench.py reads it for the roofline `traffic`.
 
 usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r1_pmc_traffic.json
+The commit the profiled tree was built from goes into the summary's "commit" field (VIO_COMMIT, else
+`git rev-parse HEAD` where a checkout exists): bench.py reports it next to the traffic figure.
 """
 import csv
 import glob
@@ -49,7 +51,16 @@ def main(src, dst):
                 continue
         out[key] = {"dispatches": n, "fetch_kb_raw": fk, "write_kb_raw": wk, "read_bytes_per_launch": rd,
                     "write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr}
+    commit = os.environ.get("VIO_COMMIT")
+    if not commit:
+        import subprocess
+        try:
+            commit = subprocess.run(["git", "rev-parse", "HEAD"], capture_output=True, text=True,
+                                    cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip() or None
+        except OSError:
+            commit = None
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/gpu_pmc.sh)",
+           "commit": commit,
            "correction": "reads = 2 x FETCH_SIZE (gfx950 half-count of wide coalesced reads), writes as reported",
            "kernels": out}
     with open(dst, "w") as f:
