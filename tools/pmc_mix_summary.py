@@ -31,7 +31,8 @@ def load(pass_dir):
 
 def main(src, dst):
     out = {}
-    for leg in ("mono", "ph", "gba"):
+    legs = sorted({os.path.basename(d)[:-3] for d in glob.glob(os.path.join(src, "*_p1"))}) or ["mono", "ph", "gba"]
+    for leg in legs:
         merged = defaultdict(dict)
         for p in ("p1", "p2"):
             for k, ctrs in load(os.path.join(src, f"{leg}_{p}")).items():
@@ -44,11 +45,15 @@ def main(src, dst):
             mfma = 512.0 * g("SQ_INSTS_VALU_MFMA_MOPS_F64", 0)
             wc = g("SQ_WAVE_CYCLES", 0) or float("nan")
             c.update({"f64_valu_flops": valu, "f64_mfma_flops": mfma,
-                      "wait_frac": g("SQ_WAIT_INST_ANY", 0) / wc, "valu_frac": g("SQ_ACTIVE_INST_VALU", 0) / wc})
+                      "wait_frac": g("SQ_WAIT_INST_ANY", 0) / wc, "valu_frac": g("SQ_ACTIVE_INST_VALU", 0) / wc,
+                      "parked_frac": g("SQ_WAIT_ANY", 0) / wc})
+            # MFMA pipe busy over the kernel's GPU-active cycles, per SIMD of the chip (256 CUs x 4)
+            if g("GRBM_GUI_ACTIVE", 0):
+                c["mfma_busy_frac_chip"] = g("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (g("GRBM_GUI_ACTIVE") * 1024.0)
             out[f"{leg}:{k}"] = dict(c)
     with open(dst, "w") as f:
-        json.dump({"source": "rocprofv3 --pmc SQ passes (tools/gpu_pmc_mix.sh)", "kernels": out}, f, indent=1,
-                  sort_keys=True)
+        json.dump({"source": "rocprofv3 --pmc SQ passes (tools/gpu_pmc_mix.sh, tools/gpu_r5_prof.sh)",
+                   "commit": os.environ.get("VIO_COMMIT"), "kernels": out}, f, indent=1, sort_keys=True)
     for k, c in sorted(out.items()):
         if c.get("SQ_WAVE_CYCLES", 0) < 1e6:
             continue
