@@ -47,9 +47,11 @@ def main(src, dst):
             c.update({"f64_valu_flops": valu, "f64_mfma_flops": mfma,
                       "wait_frac": g("SQ_WAIT_INST_ANY", 0) / wc, "valu_frac": g("SQ_ACTIVE_INST_VALU", 0) / wc,
                       "parked_frac": g("SQ_WAIT_ANY", 0) / wc})
-            # MFMA pipe busy over the kernel's GPU-active cycles, per SIMD of the chip (256 CUs x 4)
+            # MFMA pipe busy over the kernel's GPU-active cycles, per SIMD of the chip (256 CUs x 4):
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs, SQ_VALU_MFMA_BUSY_CYCLES over the 1024 SIMDs
             if g("GRBM_GUI_ACTIVE", 0):
-                c["mfma_busy_frac_chip"] = g("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (g("GRBM_GUI_ACTIVE") * 1024.0)
+                c["kernel_cycles"] = g("GRBM_GUI_ACTIVE") / 8.0
+                c["mfma_busy_frac_chip"] = g("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (c["kernel_cycles"] * 1024.0)
             out[f"{leg}:{k}"] = dict(c)
     with open(dst, "w") as f:
         json.dump({"source": "rocprofv3 --pmc SQ passes (tools/gpu_pmc_mix.sh, tools/gpu_r5_prof.sh)",
