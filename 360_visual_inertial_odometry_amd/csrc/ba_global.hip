@@ -292,6 +292,11 @@ __global__ void __launch_bounds__(GT) gba_step_obs_kernel(GbaArgs A) {
 
 // S lower triangle, one wavefront per 6x6 destination block (pa >= pb pose blocks):
 //   S[pa,pb] = [pa == pb] (s U s + D^2) - sum over co-observations Y_oa W_ob^T
+// lane (i, j) < 36 sums entry (i, j) over the block's contributions in list (landmark) order, four at a
+// time with their loads in flight.  Measured and not kept (round 5, profiles/r5_gba_schur_ab.log): 8-deep
+// batches (1.0 ms per launch against 0.55: the deeper batch's registers halve the waves in flight), 4-deep
+// batches with the tail predicated instead of serial (0.69-0.81 ms), a lane per block (36 sums per lane,
+// 16-B row loads: 1.2 ms, every load instruction touching 64 lines).
 __global__ void __launch_bounds__(GT) gba_schur_kernel(GbaArgs A) {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long long d = (long long)blockIdx.x * (GT / 64) + wid;
@@ -302,7 +307,7 @@ __global__ void __launch_bounds__(GT) gba_schur_kernel(GbaArgs A) {
     double acc = 0.0;
     const int cbeg = A.dest_ptr[d], cend = A.dest_ptr[d + 1];
     int c = cbeg;
-    for (; c + 4 <= cend; c += 4) {  // four contributions' loads in flight, summed in order
+    for (; c + 4 <= cend; c += 4) {
         double y[4][3], w[4][3];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {

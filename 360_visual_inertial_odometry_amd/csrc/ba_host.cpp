@@ -484,7 +484,7 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     }();
     d.P.imu_in_back = cluster || d.n <= imu_back_max ? 1 : 0;  // cluster: the leader, beside the walks
     static const int chol_variant = [] {
-        const char* v = std::getenv("VIO_BA_CHOL");  // experiment override: 0 chol6_solve2, 1 chol_mw_solve2, 2 chol_tile_solve2
+        const char* v = std::getenv("VIO_BA_CHOL");  // experiment override: 0 chol6_solve2, 2 chol_tile_solve2
         return v ? std::atoi(v) : 2;  // (chol_tile_solve2 where its tile geometry is instantiated, else chol6_solve2)
     }();
     d.P.chol_variant = chol_variant;

@@ -32,6 +32,18 @@ constexpr unsigned long long kWaitTicks = 200000000ull;
 __device__ __forceinline__ unsigned long long wait_clock() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ bool wait_expired(unsigned long long t0) { return wait_clock() - t0 > kWaitTicks; }
 
+// An LDS pointer the compiler must treat as an opaque register value: accesses at constant offsets from it
+// then fold into the 16-bit immediate of ds_read / ds_write.  Without it, a region placed above 64 KB of
+// LDS (the window kernels' stage area follows the 75 KB reduced matrix) has its constant addresses folded
+// into absolute values that do not fit the immediate: every access site gets an address register of its
+// own, the unrolled loops hoist them, and the cluster kernel spilled them to scratch.
+template <class T>
+__device__ __forceinline__ T* lds_base(T* p) {
+    auto q = (__attribute__((address_space(3))) T*)p;
+    asm volatile("" : "+v"(q));
+    return (T*)q;
+}
+
 // LDS writes of this wave visible to its own later reads (no workgroup barrier)
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -619,6 +631,9 @@ __device__ __forceinline__ bool chol_tile_solve2(double* A0, int n0, double* A1,
     };
     const int t = (int)threadIdx.x, lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
     const int nb0 = n0 / 6, nb1 = n1 / 6, nb = nb0 > nb1 ? nb0 : nb1;
+    A0 = lds_base(A0);
+    A1 = lds_base(A1);
+    scr = lds_base(scr);
     constexpr int soff1 = 16 * T0;                     // system 1's first row in the panel / column buffers
     double* const Pb = scr;                            // panel buffers, parity p at Pb + p * kPanelStride
     double* const E = scr + 2 * kPanelStride;          // column buffer; row kTileRows: trash
