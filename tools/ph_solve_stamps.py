@@ -29,7 +29,8 @@ names = {0: "prep U partials", 1: "prep imu", 2: "prep cost partials", 3: "prep 
          16: "solve assembly+partials", 17: "solve cholesky+solves", 18: "solve small inputs+tables",
          19: "solve pose tiles+partials", 20: "solve reductions", 21: "ctrl lane", 22: "ctrl copies",
          24: "cl imu loads", 25: "cl imu model change", 26: "cl imu factors", 27: "cl imu cost", 28: "cl imu normal eq",
-         29: "solve mode-1 head (loads)", 30: "solve mode-2 head (partials)"}
+         29: "solve mode-1 head (loads)", 30: "solve mode-2 head (partials)", 25: "solve mode-2 fail flags",
+         31: "cl member1 walk head (to back-sub)"}
 tot = sum(out[i] for i in names)
 for i, n in names.items():
     print(f"W={W} {n:28s} cycles/window/iter {out[i] / W / 11:10.0f}  ({100 * out[i] / max(tot, 1):.1f}%)")
