@@ -609,7 +609,7 @@ static std::string g_create_error;
 
 int vio_layout_check(void) {
     const uint64_t ba = ba_layout_sig(), gba = gba_layout_sig_ba_global();
-    return ba == ba_layout_sig_ba_kernel() && ba == ba_layout_sig_ba_global_host() &&
+    return ba == ba_layout_sig_ba_kernel() && ba == ba_layout_sig_ba_cluster() && ba == ba_layout_sig_ba_global_host() &&
                    gba == gba_layout_sig_ba_kernel() && gba == gba_layout_sig_ba_global_host()
                ? VIO_OK
                : VIO_EDEVICE;

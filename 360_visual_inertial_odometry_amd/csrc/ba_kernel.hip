@@ -28,8 +28,12 @@
 
 namespace vio360 {
 
+#ifndef VIO_BA_CLUSTER_TU
 uint64_t ba_layout_sig_ba_kernel() { return ba_layout_sig(); }
 uint64_t gba_layout_sig_ba_kernel() { return gba_layout_sig(); }
+#else
+uint64_t ba_layout_sig_ba_cluster() { return ba_layout_sig(); }
+#endif
 
 constexpr int NI_MAX = 3 * VI_KMAX + 6;
 // per-window workspace after ba_ws_layout(): IMU sqrt-information, imu-space H and g
@@ -70,7 +74,6 @@ struct __align__(16) BaShared {
     int posef[BA_KMAX];          // copy of BaWin::pose_f (per-lane indexed in the Schur fill)
     int pvalid[BA_KMAX];         // preint_valid
     int8_t icol[BA_KMAX][12];    // imu_col(w, k, c): imu-space index of column c of IMU factor k, or -1
-    int8_t tile_i[24], tile_j[24];  // lower 16x16 tile t -> (tile row, tile column) (ph_solve assembly)
     double Rlin[BA_KMAX][9];     // R_bw at the linearisation point (Jacobians are stored compressed)
 };
 static_assert(sizeof(BaShared) <= 160 * 1024, "BaShared exceeds the 160 KB LDS of a gfx950 CU");
@@ -164,7 +167,7 @@ __device__ inline void imu_log(const double* R, double* w) {  // Factors.cpp:150
     double f = th < 1e-6 ? 0.5 : th / (2.0 * sin(th));
     w[0] = f * v[0]; w[1] = f * v[1]; w[2] = f * v[2];
 }
-__device__ __noinline__ void imu_eval(const vio_preint& p, const double* sqi, const double* g, const double* pci,
+__device__ __forceinline__ void imu_eval_inl(const vio_preint& p, const double* sqi, const double* g, const double* pci,
                                 const double* pcj, const double* vi, const double* bg, const double* ba,
                                 const double* vj, bool want_jac, double* r, double* J) {
     const double* Rwi = pci;
@@ -269,13 +272,18 @@ __device__ __noinline__ void imu_eval(const vio_preint& p, const double* sqi, co
             J[12 * i + 6 + j] = sa;
         }
 }
+__device__ __noinline__ void imu_eval(const vio_preint& p, const double* sqi, const double* g, const double* pci,
+                                const double* pcj, const double* vi, const double* bg, const double* ba,
+                                const double* vj, bool want_jac, double* r, double* J) {
+    imu_eval_inl(p, sqi, g, pci, pcj, vi, bg, ba, vj, want_jac, r, J);
+}
 
 // imu_eval with Jacobians by one whole wave: every lane evaluates the factor's common part (bias
 // correction, raw residual, the weighted rotation residual and Jr^-1 J_Rg), lane i < 9 returns residual
 // row i in r, lane j < 12 writes Jacobian column j (J row-major 9x12, [vi | bg | ba | vj]).  Each output
 // element goes through imu_eval's operations in imu_eval's order (same values); the serial chain of
 // 486 + 81 dependent multiply-adds becomes 9 + 9 per lane.
-__device__ __noinline__ void imu_eval_wave(const vio_preint& p, const double* sqi, const double* g, const double* pci,
+__device__ __forceinline__ void imu_eval_wave_inl(const vio_preint& p, const double* sqi, const double* g, const double* pci,
                                            const double* pcj, const double* vi, const double* bg, const double* ba,
                                            const double* vj, int lane, double& r_out, double* J) {
     const double* Rwj = pcj;
@@ -402,6 +410,11 @@ __device__ __noinline__ void imu_eval_wave(const vio_preint& p, const double* sq
         }
     }
 }
+__device__ __noinline__ void imu_eval_wave(const vio_preint& p, const double* sqi, const double* g, const double* pci,
+                                           const double* pcj, const double* vi, const double* bg, const double* ba,
+                                           const double* vj, int lane, double& r_out, double* J) {
+    imu_eval_wave_inl(p, sqi, g, pci, pcj, vi, bg, ba, vj, lane, r_out, J);
+}
 
 // InertialFactorFixedGravity ctor (Factors.cpp:1310-1323): sqrt-information = chol((cov + 1e-8 I)^-1)^T,
 // identity when the inverse or its Cholesky fails.  One whole wave per factor: Gauss-Jordan with
@@ -409,7 +422,7 @@ __device__ __noinline__ void imu_eval_wave(const vio_preint& p, const double* sq
 // and multipliers broadcast by v_readlane), then the Cholesky of the inverse with lane i < 9 holding
 // row i.  Every matrix element goes through the same operations in the same order as the serial
 // elimination (oracle/ba_oracle.c), so the result is the same; nothing is dynamically indexed.
-__device__ __noinline__ void imu_sqrt_info_wave(const vio_preint& p, double* out) {
+__device__ __forceinline__ void imu_sqrt_info_wave_inl(const vio_preint& p, double* out) {
     const int lane = threadIdx.x & 63;
     const int j = lane < 18 ? lane : 17;
     double m[9];
@@ -473,6 +486,9 @@ __device__ __noinline__ void imu_sqrt_info_wave(const vio_preint& p, double* out
         for (int i = 0; i < 9; ++i)
             out[9 * i + lane] = ok ? (i <= lane ? r[i] : 0.0) : (i == lane ? 1.0 : 0.0);
     }
+}
+__device__ __noinline__ void imu_sqrt_info_wave(const vio_preint& p, double* out) {
+    imu_sqrt_info_wave_inl(p, out);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1956,6 +1972,7 @@ __device__ __forceinline__ void init_params(BaShared& sh, const WinCtx& c, bool 
     __syncthreads();
 }
 
+#ifndef VIO_BA_CLUSTER_TU  // (ba_cluster.hip: the cluster route's kernel alone)
 __global__ void __launch_bounds__(BA_THREADS, 1) ba_window_kernel(BaPools P) {
     extern __shared__ __align__(16) unsigned char smem_raw[];
     BaShared& sh = *reinterpret_cast<BaShared*>(smem_raw);
@@ -2216,6 +2233,7 @@ hipError_t launch_lie_ba(int op, const double* in, double* out, int n, hipStream
 
 size_t ba_shared_bytes() { return sizeof(BaShared); }
 size_t ba_ws_extra_doubles() { return ba_ws_extra(); }
+#endif
 
 // kernel attributes are per device: one flag per device ordinal (the caller has selected the
 // context's device).  Contexts on one device may live on different host threads (one vio_ctx per
@@ -2228,6 +2246,7 @@ static int current_device() {
 }
 static std::mutex g_attr_mutex;
 
+#ifndef VIO_BA_CLUSTER_TU
 hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream) {
     {
         static bool attr_set[kMaxDevices] = {};
@@ -2244,7 +2263,10 @@ hipError_t launch_ba_windows(const BaPools& P, int n, hipStream_t stream) {
     return hipGetLastError();
 }
 
+#endif
 }  // namespace vio360
 
 #include "ba_phases.inc"
+#ifndef VIO_BA_CLUSTER_TU
 #include "gba_imu.inc"
+#endif

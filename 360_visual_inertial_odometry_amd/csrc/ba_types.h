@@ -92,6 +92,7 @@ constexpr uint64_t ba_layout_sig() {
 // the signatures each TU was compiled with (ba_layout_sig / gba_layout_sig of ba_global.h), compared by
 // vio_layout_check
 uint64_t ba_layout_sig_ba_kernel();
+uint64_t ba_layout_sig_ba_cluster();
 uint64_t ba_layout_sig_ba_global_host();
 uint64_t gba_layout_sig_ba_kernel();
 uint64_t gba_layout_sig_ba_global_host();

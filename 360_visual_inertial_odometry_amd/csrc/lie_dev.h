@@ -53,7 +53,7 @@ __device__ __forceinline__ bool inv3(const double* a, double* o) {
 // polar factor (nearest rotation) of a near-orthonormal 3x3 by Newton's iteration
 // X <- (X + X^-T)/2, which converges quadratically to the same U V^T the reference's JacobiSVD
 // projection yields for det > 0 inputs.
-__device__ inline void polar3(const double* A, double* R) {
+__device__ __forceinline__ void polar3_inl(const double* A, double* R) {
     double X[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) X[i] = A[i];
@@ -74,6 +74,8 @@ __device__ inline void polar3(const double* A, double* R) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) R[i] = X[i];
 }
+// (the call form: the compiler decides; polar3_inl where a kernel must stay call-free)
+__device__ inline void polar3(const double* A, double* R) { polar3_inl(A, R); }
 
 // SO3d::Exp (LieUtils.cpp:203-219)
 __device__ inline void so3_exp(const double* w, double* R) {

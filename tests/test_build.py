@@ -6,7 +6,10 @@ pin the two guards against that class of fault (csrc/Makefile -MMD -MP, ba_types
 static_asserts + vio_layout_check)."""
 import os
 import re
+import struct
 import subprocess
+
+import msgpack
 
 import pytest
 
@@ -56,3 +59,61 @@ def test_touching_a_header_rebuilds_its_dependents(built, header, must):
 
 def test_translation_units_agree_on_struct_layouts(vio):
     assert vio.lib().vio_layout_check() == 0
+
+
+# ---- code-object metadata of the shipped library (no GPU needed) ----
+_BUNDLE = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _gfx950_code_objects(blob):
+    """the gfx950 ELF code objects of every (uncompressed) clang offload bundle in the library"""
+    i = 0
+    while True:
+        i = blob.find(_BUNDLE, i)
+        if i < 0:
+            return
+        n, = struct.unpack_from("<Q", blob, i + 24)
+        p = i + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", blob, p)
+            p += 24
+            triple = blob[p:p + tl].decode()
+            p += tl
+            if "gfx950" in triple:
+                yield blob[i + off:i + off + size]
+        i += len(_BUNDLE)
+
+
+def _kernel_descriptors(co):
+    """amdhsa.kernels entries of a code object's NT_AMDGPU_METADATA note (msgpack)"""
+    shoff, = struct.unpack_from("<Q", co, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", co, 0x3A)
+    for k in range(shnum):
+        sh = shoff + k * shentsize
+        typ, = struct.unpack_from("<I", co, sh + 4)
+        off, size = struct.unpack_from("<QQ", co, sh + 0x18)
+        if typ != 7:  # SHT_NOTE
+            continue
+        p = off
+        while p < off + size:
+            nsz, dsz, nt = struct.unpack_from("<III", co, p)
+            p += 12
+            name = co[p:p + nsz]
+            p += (nsz + 3) & ~3
+            desc = co[p:p + dsz]
+            p += (dsz + 3) & ~3
+            if nt == 32 and name.startswith(b"AMDGPU"):
+                yield from msgpack.unpackb(desc, raw=False)["amdhsa.kernels"]
+
+
+def test_cluster_kernel_has_no_scratch(vio):
+    """ph_cluster_kernel (the single-window route's persistent launch) keeps every value in registers or LDS:
+    its private segment is zero bytes (no spills, no call stack) and it stays within one workgroup per CU's
+    register file (512 VGPRs incl. AGPRs)"""
+    blob = open(vio.lib()._name, "rb").read()
+    found = [kd for co in _gfx950_code_objects(blob) for kd in _kernel_descriptors(co)
+             if "ph_cluster_kernel" in kd[".name"]]
+    assert len(found) == 1, [kd[".name"] for kd in found]
+    kd = found[0]
+    assert kd[".private_segment_fixed_size"] == 0, kd[".private_segment_fixed_size"]
+    assert kd[".vgpr_count"] <= 512  # the unified file: arch VGPRs + AGPRs
