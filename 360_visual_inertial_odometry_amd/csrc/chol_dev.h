@@ -15,13 +15,14 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __hiloint2double(hi, lo);
 }
 
-// 1/sqrt(p) to full double precision: hardware estimate + two Newton-Raphson steps
+// 1/sqrt(p) to full double precision: hardware estimate r0 (relative error e0 well below 2^-20) and one
+// third-order correction r0 (1 + e/2 + 3 e^2 / 8), e = 1 - p r0^2 (remaining error ~ e^3 < 2^-60): four
+// dependent operations after the estimate instead of two Newton steps' six -- it sits on the pivot chain
+// of every Cholesky here
 __device__ __forceinline__ double rsq_nr(double p) {
-    double r = __builtin_amdgcn_rsq(p);
-    const double h = 0.5 * p;
-    r = r * fma(-h * r, r, 1.5);
-    r = r * fma(-h * r, r, 1.5);
-    return r;
+    const double r = __builtin_amdgcn_rsq(p);
+    const double e = fma(-p * r, r, 1.0);
+    return fma(r * e, fma(e, 0.375, 0.5), r);
 }
 
 // Wall-clock bound of an inter-workgroup wait: s_memrealtime counts a constant 100 MHz clock, so the
@@ -531,8 +532,18 @@ struct CholTiles {
 template <int T0, int T1, int W>
 __device__ __forceinline__ void chol_tile_wave(const double* A0, int n0, const double* A1, int n1, int lda, double* A0w,
                                                double* A1w, double* Pb, double* E, double* dv, int nb0, int nb1, int nb,
-                                               int lane) {
+                                               int lane, unsigned long long* tm) {
     using G = CholTiles<T0, T1, W>;
+    // (diagnostic, tm non-null: lane 0 of wave 2 adds shader clocks of [4] part 1 + column out, [5] barrier 1,
+    // [6] part 2 + inverse, [8] barrier 2)
+    unsigned long long tlast = tm ? __builtin_amdgcn_s_memtime() : 0;
+    auto tmark = [&](int slot) {
+        if (tm && threadIdx.x == 128) {
+            const unsigned long long tt = __builtin_amdgcn_s_memtime();
+            tm[slot] += tt - tlast;
+            tlast = tt;
+        }
+    };
     constexpr int NS = G::NS > 0 ? G::NS : 1;
     double* const trash = E + kTileRows * kTilePW;
     cd4 acc[NS];
@@ -606,13 +617,17 @@ __device__ __forceinline__ void chol_tile_wave(const double* A0, int n0, const d
                 }
             }
         });
+        tmark(4);
         __syncthreads();
+        tmark(5);
         if constexpr (J > 0) {
             update(std::false_type{});
             if (J - 1 < (W ? nb1 : nb0))  // the previous diagonal block's inverse (wave 2: system 0, wave 3: system 1)
                 chol6_inv_upper((W ? A1w : A0w) + (c0 - 6) * lda + c0 - 6, lda, dv + (W ? kTileRows : 0) + c0 - 6, lane, trash);
         }
+        tmark(6);
         __syncthreads();
+        tmark(8);
     });
 }
 
@@ -643,8 +658,8 @@ __device__ __forceinline__ bool chol_tile_solve2(double* A0, int n0, double* A1,
     if (t == 0) *flag = 0;
     tmark(0);
     if (wid >= 2) {
-        if (wid == 2) chol_tile_wave<T0, T1, 0>(A0, n0, A1, n1, lda, A0, A1, Pb, E, dv, nb0, nb1, nb, lane);
-        else chol_tile_wave<T0, T1, 1>(A0, n0, A1, n1, lda, A0, A1, Pb, E, dv, nb0, nb1, nb, lane);
+        if (wid == 2) chol_tile_wave<T0, T1, 0>(A0, n0, A1, n1, lda, A0, A1, Pb, E, dv, nb0, nb1, nb, lane, tm);
+        else chol_tile_wave<T0, T1, 1>(A0, n0, A1, n1, lda, A0, A1, Pb, E, dv, nb0, nb1, nb, lane, nullptr);
     } else {
         __syncthreads();  // panels zeroed, the tiles loaded
         const int s = wid, n = s ? n1 : n0, nbs = s ? nb1 : nb0;
@@ -655,6 +670,7 @@ __device__ __forceinline__ bool chol_tile_solve2(double* A0, int n0, double* A1,
         for (int J = 0; J < nb; ++J) {
             const int c0 = 6 * J, par = J & 1;
             __syncthreads();  // block column J in E
+            tmark(9);
             // (b) diagonal block J and the panel row below it, wave s for system s
             if (J < nbs) {
                 double* const P = Pb + par * kPanelStride + (s ? soff1 : 0) * kTilePW;
@@ -676,6 +692,7 @@ __device__ __forceinline__ bool chol_tile_solve2(double* A0, int n0, double* A1,
                     for (int k = 0; k <= i; ++k, ++qq) l[qq] = dr[i][k >> 1][k & 1];
 #pragma unroll
                 for (int c = 0; c < 6; ++c) ea[c] = er[c >> 1][c & 1];
+                tmark(10);
                 double r[6];
 #pragma unroll
                 for (int c = 0; c < 6; ++c) {
@@ -694,6 +711,7 @@ __device__ __forceinline__ bool chol_tile_solve2(double* A0, int n0, double* A1,
                     for (int m = 0; m < c; ++m) ea[c] -= ea[m] * l[c * (c + 1) / 2 + m];
                     ea[c] *= r[c];
                 }
+                tmark(11);
                 // panel row (or the trash row), the previous panel's rows of this buffer zeroed (lanes < 12)
                 double* prow = live ? P + rA * kTilePW : Ptrash;
 #pragma unroll
@@ -715,7 +733,9 @@ __device__ __forceinline__ bool chol_tile_solve2(double* A0, int n0, double* A1,
                 *(lane < 36 ? A + (c0 + lane / 6) * lda + c0 + lane % 6 : trash + (lane & 7)) = lv;
                 *(lane < 6 ? inv + c0 + lane : trash + (lane & 7)) = pick_d(r, lane);
             }
+            tmark(12);
             __syncthreads();  // panel J in P
+            tmark(13);
         }
         if (bad && lane == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }

@@ -11,10 +11,184 @@
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../360_visual_inertial_odometry_amd/csrc/chol_dev.h"
 
 using namespace vio360;
+
+namespace vio360 {
+// (measured here, not shipped: in the window kernels it was no faster and gave the cluster kernel scratch)
+// One system of chol_tile_solve1w, factored by ONE wave with no workgroup barrier: the T (T + 1) / 2 lower
+// 16x16 tiles of the system (rows incl. the right-hand-side row n, padded to 16 T) stay in this wave's
+// registers as v_mfma_f64_16x16x4_f64 accumulators for the whole factorisation.  Block step J (c0 = 6 J, a
+// compile-time index): the tiles holding block column J write it (rows >= c0) to the column buffer E; every
+// lane factors the 6x6 diagonal block in registers and solves its panel row (lane l: row c0 + 6 + l, the rhs
+// row included) into the panel buffer P (rows c0 .. c0 + 5, the previous panel's, zeroed); L goes to A, 1 /
+// L[c][c] to dv; then every tile that panel J can still change takes C -= P P^T (two k-steps, panel columns
+// 6, 7 zero).  Only wave-local LDS ordering between the steps (wave_lds_sync).  Per tile the panels are applied
+// in the order of chol_tile_solve2 (and by the same MFMAs), the diagonal blocks and panel rows are the same
+// operations: the same bits.  Returns nonzero (every lane) on a non-positive pivot.
+template <int T>
+__device__ __forceinline__ int chol_wave_tiles(double* A, int n, int lda, double* P, double* E, double* trash, double* dv,
+                                               int lane) {
+    constexpr int NS = T * (T + 1) / 2;
+    constexpr int NBMAX = (16 * T) / 6 + 1;
+    const int nb = n / 6;
+    cd4 acc[NS];
+    auto ta = [](int q) { int gg = q, r = 0; while (gg > r) { gg -= r + 1; ++r; } return r; };
+    static_for<NS>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        constexpr int a = ta(q), b = q - a * (a + 1) / 2;
+        const int col = 16 * b + (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = 16 * a + (lane >> 4) + 4 * i;
+            const bool in = row <= n && col <= row && col < n;
+            const double v = A[(in ? row : 0) * lda + (in ? col : 0)];
+            acc[q][i] = in ? v : 0.0;
+        }
+    });
+    int bad = 0;
+    static_for<NBMAX>([&](auto JJ) {
+        constexpr int J = decltype(JJ)::value, c0 = 6 * J;
+        if (J >= nb) return;  // uniform
+        // block column J out of the tiles holding it (others: the trash row)
+        static_for<NS>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            constexpr int a = ta(q), b = q - a * (a + 1) / 2, c16 = 16 * b, r16 = 16 * a;
+            if constexpr (c16 <= c0 + 5 && c16 + 15 >= c0 && r16 + 15 >= c0) {
+                const int col = c16 + (lane & 15);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = r16 + (lane >> 4) + 4 * i;
+                    const bool in = col >= c0 && col < c0 + 6 && row >= c0 && row <= n;
+                    *(in ? E + row * kTilePW + col - c0 : trash + (lane & 7)) = acc[q][i];
+                }
+            }
+        });
+        wave_lds_sync();
+        const int rA = c0 + 6 + lane;
+        const bool live = rA <= n;
+        cd2 dr[6][3], er[3];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) dr[i][p] = *reinterpret_cast<const cd2*>(E + (c0 + i) * kTilePW + 2 * p);
+        const double* erow = E + (live ? rA : n) * kTilePW;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) er[p] = *reinterpret_cast<const cd2*>(erow + 2 * p);
+        double l[21], ea[6], r[6];
+#pragma unroll
+        for (int i = 0, qq = 0; i < 6; ++i)
+#pragma unroll
+            for (int k = 0; k <= i; ++k, ++qq) l[qq] = dr[i][k >> 1][k & 1];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) ea[c] = er[c >> 1][c & 1];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            const double piv = l[c * (c + 1) / 2 + c];
+            bad |= !(piv > 0.0);
+            r[c] = rsq_nr(piv);
+            l[c * (c + 1) / 2 + c] = piv * r[c];
+#pragma unroll
+            for (int i = c + 1; i < 6; ++i) l[i * (i + 1) / 2 + c] *= r[c];
+#pragma unroll
+            for (int i = c + 1; i < 6; ++i)
+#pragma unroll
+                for (int k = c + 1; k <= i; ++k) l[i * (i + 1) / 2 + k] -= l[i * (i + 1) / 2 + c] * l[k * (k + 1) / 2 + c];
+#pragma unroll
+            for (int m = 0; m < c; ++m) ea[c] -= ea[m] * l[c * (c + 1) / 2 + m];
+            ea[c] *= r[c];
+        }
+        // panel row (or the trash row); the previous panel's rows c0 .. c0 + 5 zeroed (lanes < 6)
+        double* prow = live ? P + rA * kTilePW : trash;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<cd2*>(prow + 2 * p) = cd2{ea[2 * p], ea[2 * p + 1]};
+        double* zrow = (lane < 6 && J > 0) ? P + (c0 + lane) * kTilePW : trash;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<cd2*>(zrow + 2 * p) = cd2{0.0, 0.0};
+        // L: the panel row, the diagonal block (lane u < 36: entry (u / 6, u % 6), zeros above), 1 / L[c][c]
+        double* arow = live ? A + rA * lda + c0 : trash;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) arow[c] = ea[c];
+        double full[36];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) full[6 * i + k] = k <= i ? l[i * (i + 1) / 2 + k] : 0.0;
+        const double lv = pick_d(full, lane);
+        *(lane < 36 ? A + (c0 + lane / 6) * lda + c0 + lane % 6 : trash + (lane & 7)) = lv;
+        *(lane < 6 ? dv + c0 + lane : trash + (lane & 7)) = pick_d(r, lane);
+        wave_lds_sync();
+        // C -= P P^T on the tiles panel J can still change (rows and columns >= c0 + 6)
+        double av[NS][2], bv[NS][2];
+        static_for<NS>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            constexpr int a = ta(q), b = q - a * (a + 1) / 2;
+            if constexpr (16 * a + 15 >= c0 + 6 && 16 * b + 15 >= c0 + 6) {
+#pragma unroll
+                for (int kh = 0; kh < 2; ++kh) {
+                    av[q][kh] = -P[(16 * a + (lane & 15)) * kTilePW + 4 * kh + (lane >> 4)];
+                    bv[q][kh] = P[(16 * b + (lane & 15)) * kTilePW + 4 * kh + (lane >> 4)];
+                }
+            }
+        });
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+            static_for<NS>([&](auto Q) {
+                constexpr int q = decltype(Q)::value;
+                constexpr int a = ta(q), b = q - a * (a + 1) / 2;
+                if constexpr (16 * a + 15 >= c0 + 6 && 16 * b + 15 >= c0 + 6)
+                    acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[q][kh], bv[q][kh], acc[q], 0, 0, 0);
+            });
+    });
+    return bad;
+}
+
+// chol_tile_solve2's systems, each factored by one wave alone (chol_wave_tiles: wave 0 system 0, wave 1 system
+// 1, no barrier inside the factorisation); then the diagonal blocks' inverses over all four waves and the
+// blocked backward substitution as chol_tile_solve2.  Same arguments, scratch and bits.
+template <int T0, int T1>
+__device__ __forceinline__ bool chol_tile_solve1w(double* A0, int n0, double* A1, int n1, int lda, double* x0, double* x1,
+                                                  double* scr, int* flag) {
+    static_assert(T0 <= 4 && T1 <= 4 && T0 + T1 <= kTileRows / 16, "chol_tile_solve1w: one panel row per lane");
+    const int t = (int)threadIdx.x, lane = t & 63, wid = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int nb0 = n0 / 6, nb1 = n1 / 6;
+    A0 = lds_base(A0);
+    A1 = lds_base(A1);
+    scr = lds_base(scr);
+    double* const Pb = scr;                            // system s's panel at Pb + s * kPanelStride
+    double* const E = scr + 2 * kPanelStride;          // column buffer (system 1 from row 16 T0); row kTileRows: trash
+    double* const trash = E + kTileRows * kTilePW;
+    double* const dv = E + (kTileRows + 1) * kTilePW;  // 1 / L[c][c]: system 0 at dv, system 1 at dv + kTileRows
+    for (int e = t; e < 2 * kPanelStride; e += 256) Pb[e] = 0.0;
+    if (t == 0) *flag = 0;
+    __syncthreads();
+    int bad = 0;
+    if (wid == 0 && nb0 > 0) bad = chol_wave_tiles<T0>(A0, n0, lda, Pb, E, trash, dv, lane);
+    else if constexpr (T1 > 0) {
+        if (wid == 1 && nb1 > 0) bad = chol_wave_tiles<T1>(A1, n1, lda, Pb + kPanelStride, E + 16 * T0 * kTilePW, trash,
+                                                           dv + kTileRows, lane);
+    }
+    if (bad && lane == 0) __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+    if (*flag) return false;
+    // the diagonal blocks' inverses (chol6_inv_upper), block j of both systems' list by wave j % 4
+    for (int j = wid; j < nb0 + nb1; j += 4) {
+        const bool s1 = j >= nb0;
+        const int jj = s1 ? j - nb0 : j;
+        chol6_inv_upper((s1 ? A1 : A0) + 6 * jj * lda + 6 * jj, lda, dv + (s1 ? kTileRows : 0) + 6 * jj, lane, trash);
+    }
+    __syncthreads();
+    if (wid == 0 && nb0 > 0) chol6_backward_blk(A0, lda, n0, dv, x0, lane);
+    else if (wid == 1 && nb1 > 0) chol6_backward_blk(A1, lda, n1, dv + kTileRows, x1, lane);
+    __syncthreads();
+    return true;
+}
+
+}  // namespace vio360
+
 
 constexpr int LD = 97;  // ph_solve's s_ld(90)
 
@@ -146,6 +320,10 @@ __global__ void __launch_bounds__(256, 1) probe(const double* gA, const double* 
             chol_tile_solve2<4, 0>(S, n0, A1, 0, LD, xs[0], xs[1], &Lb[0][0], &flag, tsum);
         } else if (V == 6) {
             chol_tile_solve2<3, 0>(A1, n1, S, 0, LD, xs[1], xs[0], &Lb[0][0], &flag, tsum);
+        } else if (V == 7) {
+            chol_tile_solve1w<4, 3>(S, n0, A1, n1, LD, xs[0], xs[1], &Lb[0][0], &flag);
+        } else if (V == 8) {
+            chol_tile_solve1w<4, 0>(S, n0, A1, 0, LD, xs[0], xs[1], &Lb[0][0], &flag);
         }
         const unsigned long long t1 = __builtin_amdgcn_s_memtime();
         tot += t1 - t0;
@@ -156,15 +334,14 @@ __global__ void __launch_bounds__(256, 1) probe(const double* gA, const double* 
         gx[64 + threadIdx.x] = xs[1][threadIdx.x];
     }
     if (threadIdx.x == 0) *cyc = tot / reps;
-    if (V == 4 && threadIdx.x == 0)
-        printf("   V4 phases per solve: set-up %llu  factor %llu  -- %llu  backward %llu\n", tsum[0] / reps, tsum[1] / reps,
-               tsum[2] / reps, tsum[3] / reps);
-    if (V == 4 && threadIdx.x == 0)
-        printf("   V4 tile wave: (a1) %llu  barrier1 %llu  (a2) %llu  inverse %llu  barrier2 %llu\n", tsum[4] / reps,
-               tsum[5] / reps, tsum[6] / reps, tsum[7] / reps, tsum[8] / reps);
-    if (V == 4 && threadIdx.x == 0)
-        printf("   V4 diag wave: wait %llu  loads %llu  factor+panel %llu  stores %llu\n", tsum[9] / reps, tsum[10] / reps,
-               tsum[11] / reps, tsum[12] / reps);
+    if (V >= 4 && V <= 6 && threadIdx.x == 0) {
+        printf("   V%d phases per solve: set-up %llu  factor tail %llu  backward %llu\n", V, tsum[0] / reps, tsum[1] / reps,
+               tsum[3] / reps);
+        printf("   V%d tile wave 2: part1+col %llu  barrier1 %llu  part2+inverse %llu  barrier2 %llu\n", V, tsum[4] / reps,
+               tsum[5] / reps, tsum[6] / reps, tsum[8] / reps);
+        printf("   V%d diag wave 0: wait E %llu  load issue %llu  factor+panel %llu  stores %llu  barrier %llu\n", V,
+               tsum[9] / reps, tsum[10] / reps, tsum[11] / reps, tsum[12] / reps, tsum[13] / reps);
+    }
 }
 
 static void make_spd(int n, double* A /* (n+1) x 64, lower + rhs row */, unsigned seed) {
@@ -204,11 +381,13 @@ int main() {
     hipMalloc(&dc, 8);
     hipMemcpy(dA, A, sizeof(A), hipMemcpyHostToDevice);
     hipMemcpy(dB, B, sizeof(B), hipMemcpyHostToDevice);
-    void (*fns[7])(const double*, const double*, int, int, int, double*, unsigned long long*) = {
-        probe<0>, probe<1>, probe<2>, probe<3>, probe<4>, probe<5>, probe<6>};
-    const char* names[7] = {"chol6_solve2 54", "chol6_solve2 54+36", "chol_mw 4x16 54", "chol_mw 3x18 54 + 1x40 36",
-                            "chol_tile_solve2 54+36", "chol_tile_solve2 54", "chol_tile_solve2 36"};
-    for (int v = 0; v < 7; ++v) {
+    void (*fns[9])(const double*, const double*, int, int, int, double*, unsigned long long*) = {
+        probe<0>, probe<1>, probe<2>, probe<3>, probe<4>, probe<5>, probe<6>, probe<7>, probe<8>};
+    const char* names[9] = {"chol6_solve2 54", "chol6_solve2 54+36", "chol_mw 4x16 54", "chol_mw 3x18 54 + 1x40 36",
+                            "chol_tile_solve2 54+36", "chol_tile_solve2 54", "chol_tile_solve2 36",
+                            "chol_tile_solve1w 54+36", "chol_tile_solve1w 54"};
+    static double xall[9][128];
+    for (int v = 0; v < 9; ++v) {
         for (int rep = 0; rep < 2; ++rep) {
             hipLaunchKernelGGL(fns[v], dim3(1), dim3(256), 0, 0, dA, dB, n0, n1, reps, dx, dc);
             if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
@@ -217,8 +396,16 @@ int main() {
         double x[128];
         hipMemcpy(&cyc, dc, 8, hipMemcpyDeviceToHost);
         hipMemcpy(x, dx, sizeof(x), hipMemcpyDeviceToHost);
-        const double r0 = v == 6 ? 0.0 : resid(n0, A, x), r1 = (v == 1 || v == 3 || v == 4 || v == 6) ? resid(n1, B, x + 64) : 0.0;
-        printf("V%d %-28s cycles/solve %7llu  resid %.2e %.2e\n", v, names[v], cyc, r0, r1);
+        const double r0 = v == 6 ? 0.0 : resid(n0, A, x), r1 = (v == 1 || v == 3 || v == 4 || v == 6 || v == 7) ? resid(n1, B, x + 64) : 0.0;
+        for (int i = 0; i < 128; ++i) xall[v][i] = x[i];
+        int same = -1;
+        if (v == 7 || v == 8) {
+            same = 1;
+            for (int i = 0; i < (v == 7 ? 128 : 54); ++i)
+                if ((i < 54 || (i >= 64 && i < 100)) && memcmp(&x[i], &xall[v - 3][i], 8) != 0) same = 0;
+        }
+        printf("V%d %-28s cycles/solve %7llu  resid %.2e %.2e%s\n", v, names[v], cyc, r0, r1,
+               same < 0 ? "" : same ? "  bitwise = tile_solve2" : "  DIFFERS from tile_solve2");
     }
     return 0;
 }
