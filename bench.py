@@ -115,6 +115,25 @@ def klt_traffic():
                if n.startswith(TRACKER_PREFIXES) and v["dispatches"] >= runs) / runs, src
 
 
+def sq_mix(route_leg="ph256"):
+    """SQ-counter mix of the window-BA step kernels from the newest committed summary
+    (tools/gpu_r5_prof.sh -> profiles/r*_pmc_mix.json): per kernel its MFMA-pipe busy share of the chip's
+    SIMD cycles while it runs, VALU-issue share and dependency-wait share of its wave cycles.  The dominant
+    kernel of the step by time is ph_back (no MFMA work); ph_schur holds the step's MFMA work.
+    ({kernel: {...}}, source) or (None, None)."""
+    d, src = newest_profile("pmc_mix")
+    if not d:
+        return None, None
+    out = {}
+    for k, v in d["kernels"].items():
+        leg, _, name = k.partition(":")
+        if leg != route_leg or not name.startswith("ph_"):
+            continue
+        out[name] = {"mfma_busy_frac": v.get("mfma_busy_frac_chip"), "valu_frac": v.get("valu_frac"),
+                     "wait_frac": v.get("wait_frac"), "dispatches": v.get("dispatches")}
+    return (out or None), src
+
+
 def kernel_traffic(name):
     """PMC HBM bytes per launch of one kernel from the committed summary: (bytes, source) or (None, None)."""
     k, src = pmc_traffic()
@@ -785,6 +804,15 @@ def main():
 
     c4 = None if args.no_config4 else config4_strong(vio, synth, ctx, dist, rank, world, args.steps, args.warmup,
                                                        args.lm_iters)
+    mix, mix_src = sq_mix()
+    mix_note = ""
+    if mix:
+        def _busy(name):
+            v = next((m for k, m in mix.items() if k.startswith(name)), None)
+            return v["mfma_busy_frac"] if v and v.get("mfma_busy_frac") is not None else float("nan")
+        mix_note = (f"; MFMA pipe busy (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES over the chip's SIMD cycles, {mix_src}): "
+                    f"dominant kernel ph_back {_busy('ph_back_kernel'):.3f} (no MFMA work: the walk is VALU / memory "
+                    f"bound), ph_schur {_busy('ph_schur_kernel'):.3f}, ph_solve {_busy('ph_solve_kernel'):.3f}")
     out = None
     if rank == 0:
         # single-window latency (config 3 exactly, one window per launch) for the >=50x CPU target
@@ -856,7 +884,9 @@ def main():
                 "flops_per_launch": flops_iter * args.lm_iters,
                 "note": "FP64 (vector = matrix peak on MI355X); flops by the SURVEY §8d convention; achieved = "
                         "flops of one step / HIP-event time of the step's graph on the batch stream; traffic = "
-                        "PMC HBM bytes of all the step's kernels",
+                        "PMC HBM bytes of all the step's kernels" + mix_note,
+                "sq_mix": mix,
+                "sq_mix_source": mix_src,
             },
             "single_window": {
                 "config": "config 3 (one window per launch)",
