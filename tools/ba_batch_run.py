@@ -1,6 +1,6 @@
 """Diagnostic: one config-4 shard (W config-3 VIO windows, 10 fixed LM iterations) solved S times on a
 resident batch; prints the average HIP-event time per launch.  Route: VIO_BA_PHASES=1 /
-VIO_BA_MONOLITHIC=1 in the environment.  Used under rocprofv3 for per-kernel statistics.
+VIO_BA_MONOLITHIC=1 / VIO_BA_ROUTE=cluster in the environment.  Used under rocprofv3 for per-kernel statistics.
 BA_CFG=2: config-2 windows (visual-only RunLocalBA, 10 KF x 200 landmarks) instead."""
 import importlib
 import os
@@ -16,6 +16,8 @@ synth = importlib.import_module("360_visual_inertial_odometry_amd.synth")
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 ctx = vio.Context(0)
+if os.environ.get("VIO_BA_ROUTE") == "cluster":  # force the cluster route (experiment)
+    ctx.set_ba_route(ctx.ROUTE_CLUSTER)
 if os.environ.get("BA_CFG") == "2":
     probs = [vio.BaProblem(synth.config2(synth.SEED + i), variant=vio.VIO_BA_LOCAL, max_iterations=10,
                            fixed_iterations=1) for i in range(W)]
