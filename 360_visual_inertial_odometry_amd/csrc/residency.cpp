@@ -33,6 +33,9 @@ void prune(Ledger& L) {
     size_t k = 0;
     for (size_t i = 0; i < L.live.size(); ++i) {
         const hipError_t q = hipEventQuery(L.live[i].done);
+        // (the status is consumed here: it must not stay behind as this thread's last HIP error, where a
+        // later hipGetLastError -- ours after a launch, or the caller's -- would report it)
+        if (q != hipSuccess) (void)hipGetLastError();
         if (q == hipErrorNotReady) L.live[k++] = L.live[i];
         else L.spare.push_back(L.live[i].done);
     }
