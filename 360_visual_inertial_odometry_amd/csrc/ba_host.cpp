@@ -476,11 +476,12 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     const bool cluster = any_other && d.cluster_C > 0;
     const bool phases = !cluster && any_other && !force_monolithic(ctx, d);
     d.P.route = phases || cluster ? 1 : 0;
-    // IMU candidate terms beside the back-substitution walk for small batches (a single window's serial
-    // path is then shorter); in ph_solve for larger ones (ph_back keeps 4 waves per SIMD, no scratch)
+    // IMU candidate terms beside the back-substitution walk (ph_back_x's extra workgroup) up to 64 windows
+    // (a window's serial path is then shorter: 32 windows 1.436 -> 1.342 ms, 64 windows 1.677 -> 1.633 ms,
+    // profiles/r5_imu_back_sweep.log); in ph_solve for larger batches (256 windows: 3.04 against 3.17 ms)
     static const int imu_back_max = [] {
         const char* v = std::getenv("VIO_BA_IMU_BACK_MAX");  // experiment override
-        return v ? std::atoi(v) : 8;
+        return v ? std::atoi(v) : 64;
     }();
     d.P.imu_in_back = cluster || d.n <= imu_back_max ? 1 : 0;  // cluster: the leader, beside the walks
     static const int chol_variant = [] {
