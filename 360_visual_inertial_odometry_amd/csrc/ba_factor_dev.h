@@ -216,6 +216,48 @@ __device__ __forceinline__ int factor_eval_ap(const double* pc, const double* Rc
     return 0;
 }
 
+// factor_eval_ap in two parts: the residual (returns 1 on a PnP evaluation failure); `tail` says whether the
+// Jacobian tail applies (factor_ap_tail at the camera-frame point P, |P| = L, 1 / L = iL), which the caller
+// runs when it needs A / Pb -- after its loss, so that A / Pb are not live across it (the same operations
+// as factor_eval_ap, hence the same values)
+__device__ __forceinline__ int factor_eval_res(const double* pc, const double* Pw, double uo, double vo, double cols,
+                                               double rows, const double* Lw, bool outlier, bool is_pnp, double* r,
+                                               double* P, double& L, double& iL, bool& tail) {
+    tail = false;
+    if (outlier) {
+        r[0] = 640.0; r[1] = 480.0;
+        return 0;
+    }
+    const double* Rcw = pc + 24;
+    const double* tcw = pc + 33;
+    m3vec(Rcw, Pw, P);
+    P[0] += tcw[0]; P[1] += tcw[1]; P[2] += tcw[2];
+    const double x = P[0], y = P[1], z = P[2];
+    L = nrm3(P);
+    if (L < 1e-10) {
+        if (is_pnp) return 1;
+        r[0] = 640.0; r[1] = 360.0;
+        return 0;
+    }
+    constexpr double inv2pi = 1.0 / (2.0 * M_PI), invpi = 1.0 / M_PI;
+    iL = 1.0 / L;
+    double theta = atan2(x, z);
+    double phi = -asin(y * iL);
+    double u = cols * (0.5 + theta * inv2pi);
+    double v = rows * (0.5 - phi * invpi);
+    double du = uo - u, dv = vo - v;
+    if (du > cols / 2.0) du -= cols;
+    else if (du < -cols / 2.0) du += cols;
+    if (fabs(du) > 100.0 || fabs(dv) > 100.0) {
+        r[0] = 100.0; r[1] = 100.0;
+        return 0;
+    }
+    r[0] = Lw[0] * du;
+    r[1] = Lw[2] * du + Lw[3] * dv;
+    tail = true;
+    return 0;
+}
+
 // The compressed Jacobian of factor_eval_ap at a point whose residual was linearised with Jacobian scale asc
 // (the Huber / Corrector scale, 0 when the Jacobian was zero: outlier, degenerate or out-of-range residual):
 // A = asc Jw R_cb_raw and Pb, recomputed from the point and the pose cache at the linearisation point (pcl:

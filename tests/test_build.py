@@ -117,3 +117,20 @@ def test_cluster_kernel_has_no_scratch(vio):
     kd = found[0]
     assert kd[".private_segment_fixed_size"] == 0, kd[".private_segment_fixed_size"]
     assert kd[".vgpr_count"] <= 512  # the unified file: arch VGPRs + AGPRs
+
+
+def test_wide_phase_kernels_have_no_scratch(vio):
+    """the phase route's per-window kernels that run one workgroup per window across the chip (ph_prep,
+    ph_back, ph_solve) and the global-BA diagonal-chain kernels touch no scratch: a workgroup's first
+    private-segment access cost ph_prep ≈ 25 k cycles per window at 256 windows (profiles/r5s_*)"""
+    blob = open(vio.lib()._name, "rb").read()
+    want = ("ph_prep_kernel", "ph_back_kernel", "ph_back_x_kernel", "ph_solve_kernel", "chol_diag_kernel",
+            "chol_chain_kernel")
+    found = {}
+    for co in _gfx950_code_objects(blob):
+        for kd in _kernel_descriptors(co):
+            for w in want:
+                if w + "E" in kd[".name"]:
+                    found[w] = kd[".private_segment_fixed_size"]
+    assert set(found) == set(want), found
+    assert all(v == 0 for v in found.values()), found
