@@ -389,7 +389,9 @@ constexpr size_t CHOL_DIAG_LDS = sizeof(double) * (2 * NB * TLD + 4 * 256 + 256 
 // factor the 64x64 block held in T (lower part, row stride TLD) in place into L and build X = L^-1
 // (X zeroed by the caller); LB / LT / P: scratch as laid out by diag_lds_layout.  Returns nonzero
 // (the same in every thread) when a pivot is not positive.
-__device__ __forceinline__ int diag_block_lds(double* T, double* X, double* LB, double* LT, double* P, int& bad_s) {
+// (a call: inlined into chol_diag_kernel / chol_chain_kernel it removes their 12-B stack but costs the chained
+// Cholesky ≈ 5 % per LM iteration, profiles/r5s_gba_inline_ab.log -- those launches are one workgroup wide)
+__device__ int diag_block_lds(double* T, double* X, double* LB, double* LT, double* P, int& bad_s) {
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int r16 = lane & 15, kk = lane >> 4;
     constexpr int NT = NB / 16;

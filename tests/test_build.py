@@ -121,11 +121,11 @@ def test_cluster_kernel_has_no_scratch(vio):
 
 def test_wide_phase_kernels_have_no_scratch(vio):
     """the phase route's per-window kernels that run one workgroup per window across the chip (ph_prep,
-    ph_back, ph_solve) and the global-BA diagonal-chain kernels touch no scratch: a workgroup's first
-    private-segment access cost ph_prep ≈ 25 k cycles per window at 256 windows (profiles/r5s_*)"""
+    ph_back, ph_solve) touch no scratch: a workgroup's first private-segment access cost ph_prep ≈ 25 k
+    cycles per window at 256 windows (profiles/r5s_*).  (The global solver's one-workgroup diagonal
+    launches keep their call and its 12-B stack: inlined they were 5 % slower, profiles/r5s_gba_inline_ab.log.)"""
     blob = open(vio.lib()._name, "rb").read()
-    want = ("ph_prep_kernel", "ph_back_kernel", "ph_back_x_kernel", "ph_solve_kernel", "chol_diag_kernel",
-            "chol_chain_kernel")
+    want = ("ph_prep_kernel", "ph_back_kernel", "ph_back_x_kernel", "ph_solve_kernel")
     found = {}
     for co in _gfx950_code_objects(blob):
         for kd in _kernel_descriptors(co):
