@@ -213,6 +213,12 @@ class Context:
         self.check(lib().vio_ba_solve_batched(self.h, P, O, n), "vio_ba_solve_batched")
         return [o.result() for o in outs]
 
+    def ba_solve_call(self, problems, trace_cap=256):
+        """vio_ba_solve_batched with its problem / output structs marshalled once: call() is one C-ABI call
+        (pack + upload + solve + download, as a C++ host makes it per keyframe), results() converts the
+        outputs of the last call."""
+        return BaSolveCall(self, problems, trace_cap)
+
     # ---- IMU initialisation ----
     def imu_init(self, problems):
         """vio_imu_init_solve: Optimizer::OptimizeIMUInit for a list of abi.ImuInitProblem in one
@@ -606,6 +612,28 @@ class Frontend:
             self.close()
         except Exception:
             pass
+
+
+class BaSolveCall:
+    """One vio_ba_solve_batched call over fixed problems, its ctypes structs built once (Context.ba_solve_call)."""
+
+    def __init__(self, ctx, problems, trace_cap=256):
+        self.ctx = ctx
+        self.problems = problems
+        n = len(problems)
+        self._P = (abi.VioBaProblem * n)(*[p.c for p in problems])
+        self._outs = [BaOutput(p.K, p.L, p.N, trace_cap) for p in problems]
+        self._O = (abi.VioBaOutput * n)(*[o.c for o in self._outs])
+        self._n = n
+        self._fn = lib().vio_ba_solve_batched
+
+    def __call__(self):
+        rc = self._fn(self.ctx.h, self._P, self._O, self._n)
+        if rc != 0:
+            self.ctx.check(rc, "vio_ba_solve_batched")
+
+    def results(self):
+        return [o.result() for o in self._outs]
 
 
 class BaBatch:

@@ -56,27 +56,56 @@ void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes) {
     if (ctx->bufs[slot]) (void)hipFree(ctx->bufs[slot]);
     ctx->bufs[slot] = nullptr;
     ctx->caps[slot] = 0;
-    size_t cap = std::max<size_t>(bytes, 256);
+    // 25 % headroom: per-keyframe solves grow and shrink by a few landmarks from call to call
+    size_t cap = std::max<size_t>(bytes + bytes / 4, 256);
     if (hipMalloc(&ctx->bufs[slot], cap) != hipSuccess) return nullptr;
     ctx->caps[slot] = cap;
     return ctx->bufs[slot];
 }
+void* ctx_host_buffer(vio_ctx* ctx, int slot, size_t bytes) {
+    if ((int)ctx->hbufs.size() <= slot) {
+        ctx->hbufs.resize(slot + 1, nullptr);
+        ctx->hcaps.resize(slot + 1, 0);
+    }
+    if (ctx->hcaps[slot] >= bytes && ctx->hbufs[slot]) return ctx->hbufs[slot];
+    DeviceScope dev_scope(ctx->device);
+    if (dev_scope.err != hipSuccess) return nullptr;
+    if (ctx->hbufs[slot]) {
+        (void)hipStreamSynchronize(ctx->stream);  // no copy from / into the old buffer is in flight
+        (void)hipHostFree(ctx->hbufs[slot]);
+    }
+    ctx->hbufs[slot] = nullptr;
+    ctx->hcaps[slot] = 0;
+    size_t cap = std::max<size_t>(bytes + bytes / 4, 4096);
+    if (hipHostMalloc(&ctx->hbufs[slot], cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    ctx->hcaps[slot] = cap;
+    return ctx->hbufs[slot];
+}
 
 namespace {
 
-// host image of a packed batch
-struct Packed {
-    std::vector<BaWin> win;
-    std::vector<double> pose_raw, lm_xyz0, vel0;
-    std::vector<uint8_t> kf_const, lm_var, lm_marg, preint_valid;
-    std::vector<int32_t> lm_ptr, obs_kf, obs_lm, kf_ptr, kf_obs;
-    std::vector<float> obs_uv;
-    std::vector<vio_preint> preint;
-    std::vector<std::vector<int32_t>> perm;  // per window: sorted position -> original obs index
-    int64_t ws_total = 0, out_total = 0, N_total = 0, L_total = 0, tr_total = 0;
+// A batch lives in ONE device allocation, in three regions: the inputs (filled on the host into one staging
+// buffer and sent with one host-to-device copy), the outputs the host reads back (one device-to-host copy,
+// the cluster route's error words included) and the workspace.  Byte offsets, 256-B aligned.
+struct BaRegions {
+    size_t win, pose_raw, kf_const, lm_xyz0, lm_var, lm_marg, lm_ptr, obs_kf, obs_lm, obs_uv, kf_ptr, kf_obs, preint,
+        preint_valid, vel0, obs_perm, in_bytes;
+    size_t i32, sum, out, trace, u8, bad, csync, out_begin, out_bytes;
+    size_t ws, total;
 };
 
-int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
+// host side of a packed batch: the window descriptors (grid extents, result scatter) and the pool totals
+struct Packed {
+    std::vector<BaWin> win;
+    int64_t ws_total = 0, out_total = 0, tr_total = 0;
+    int64_t N_total = 0, L_total = 0, K_total = 0, lmptr_total = 0, kfptr_total = 0;
+    BaRegions R{};
+};
+
+// Checks one problem and appends its descriptor: Ceres' problem reduction (constant blocks and residual
+// blocks on constant blocks only leave the problem, program.cc:305-400) and the Schur ordering of the
+// surviving blocks, plus the window's offsets into the pools.  The arrays are written by fill_window.
+int analyze_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk, std::vector<uint32_t>& scratch) {
     const int K = p.num_kf, L = p.num_lm, N = p.num_obs;
     if (K <= 0 || L < 0 || N < 0) { set_error(ctx, "invalid sizes"); return VIO_EINVAL; }
     if (p.variant < VIO_BA_LOCAL || p.variant > VIO_PNP) { set_error(ctx, "unknown variant"); return VIO_EINVAL; }
@@ -90,22 +119,23 @@ int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
     }
     if (vi && (!p.preint || !p.preint_valid || !p.vel)) { set_error(ctx, "VIBA needs preint/preint_valid/vel"); return VIO_EINVAL; }
     if (p.max_iterations < 0) { set_error(ctx, "max_iterations < 0"); return VIO_EINVAL; }
+    // range check, and one observation per (keyframe, landmark) -- MapPoint::AddObservation keeps one per
+    // frame -- through a keyframe bit mask per landmark (K <= 16)
+    scratch.assign((size_t)L, 0u);
+    std::vector<uint8_t> pose_used(K, 0), vel_used(K, 0);
     for (int o = 0; o < N; ++o) {
-        if (p.obs_kf[o] < 0 || p.obs_kf[o] >= K || p.obs_lm[o] < 0 || p.obs_lm[o] >= L) {
+        const int k = p.obs_kf[o], l = p.obs_lm[o];
+        if (k < 0 || k >= K || l < 0 || l >= L) {
             set_error(ctx, "observation index out of range");
             return VIO_EINVAL;
         }
-    }
-    // one observation per (keyframe, landmark): MapPoint::AddObservation keeps one per frame
-    {
-        std::vector<int64_t> key(N);
-        for (int o = 0; o < N; ++o) key[o] = (int64_t)p.obs_lm[o] * K + p.obs_kf[o];
-        std::sort(key.begin(), key.end());
-        for (int o = 1; o < N; ++o)
-            if (key[o] == key[o - 1]) {
-                set_error(ctx, "duplicate (keyframe, landmark) observation");
-                return VIO_EINVAL;
-            }
+        const uint32_t bit = 1u << k;
+        if (scratch[l] & bit) {
+            set_error(ctx, "duplicate (keyframe, landmark) observation");
+            return VIO_EINVAL;
+        }
+        scratch[l] |= bit;
+        if (!p.kf_const[k]) pose_used[k] = 1;
     }
     BaWin w;
     std::memset(&w, 0, sizeof w);
@@ -126,14 +156,7 @@ int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
     }
     if (vi) for (int i = 0; i < 3; ++i) { w.gravity[i] = p.gravity[i]; w.bg0[i] = p.bg[i]; w.ba0[i] = p.ba[i]; }
     // reduced problem: which blocks are free and used
-    std::vector<uint8_t> pose_used(K, 0), lm_used(L, 0), vel_used(K, 0);
     bool bias_used = false;
-    for (int o = 0; o < N; ++o) {
-        int k = p.obs_kf[o], l = p.obs_lm[o];
-        bool kvar = !p.kf_const[k], lvar = !pnp && !p.lm_const[l];
-        if (kvar) pose_used[k] = 1;
-        if (lvar) lm_used[l] = 1;
-    }
     if (vi) {
         for (int k = 1; k < K; ++k) {
             if (!p.preint_valid[k]) continue;
@@ -143,10 +166,10 @@ int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
             if (!p.kf_const[k]) pose_used[k] = 1;
         }
     }
-    int off = 0, P = 0;
+    int off = 0;
     for (int k = 0; k < BA_KMAX; ++k) { w.pose_f[k] = -1; w.vel_f[k] = -1; }
     for (int k = 0; k < K; ++k)
-        if (pose_used[k]) { w.pose_f[k] = off; off += 6; P++; }
+        if (pose_used[k]) { w.pose_f[k] = off; off += 6; }
     w.np = off;
     for (int k = 0; k < K; ++k)
         if (vel_used[k]) { w.vel_f[k] = off; off += 3; }
@@ -160,12 +183,12 @@ int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
     w.npad = 16 * w.T;
     w.n_imu = 0;
     if (vi) for (int k = 1; k < K; ++k) w.n_imu += p.preint_valid[k] ? 1 : 0;
-    // offsets
-    w.o_pose = (int64_t)pk.kf_const.size();
-    w.o_lm = (int64_t)pk.lm_var.size();
-    w.o_lmptr = (int64_t)pk.lm_ptr.size();
-    w.o_obs = (int64_t)pk.obs_kf.size();
-    w.o_kfptr = (int64_t)pk.kf_ptr.size();
+    // offsets into the pools
+    w.o_pose = pk.K_total;
+    w.o_lm = pk.L_total;
+    w.o_lmptr = pk.lmptr_total;
+    w.o_obs = pk.N_total;
+    w.o_kfptr = pk.kfptr_total;
     w.o_ws = pk.ws_total;
     w.o_out = pk.out_total;
     w.o_tr = pk.tr_total;
@@ -175,66 +198,117 @@ int pack_window(vio_ctx* ctx, const vio_ba_problem& p, Packed& pk) {
     pk.ws_total += WL.total + (int64_t)ba_ws_extra_doubles() + (int64_t)ba_phase_doubles(K, L, N, w.T);
     pk.ws_total = (pk.ws_total + 31) & ~(int64_t)31;
     pk.out_total += ba_out_layout(K, L, N).total;
-    // poses
-    for (int k = 0; k < K; ++k) {
-        for (int i = 0; i < 9; ++i) pk.pose_raw.push_back(p.T_wb_init[k].R[i]);
-        for (int i = 0; i < 3; ++i) pk.pose_raw.push_back(p.T_wb_init[k].t[i]);
-        for (int i = 0; i < 9; ++i) pk.pose_raw.push_back(p.T_cb[k].R[i]);
-        for (int i = 0; i < 3; ++i) pk.pose_raw.push_back(p.T_cb[k].t[i]);
-        pk.kf_const.push_back(p.kf_const[k] ? 1 : 0);
-        if (vi) {
-            pk.preint.push_back(p.preint[k]);
-            pk.preint_valid.push_back(k >= 1 && p.preint_valid[k] ? 1 : 0);
-            for (int i = 0; i < 3; ++i) pk.vel0.push_back(p.vel[3 * k + i]);
-        } else {
-            vio_preint z;
-            std::memset(&z, 0, sizeof z);
-            pk.preint.push_back(z);
-            pk.preint_valid.push_back(0);
-            for (int i = 0; i < 3; ++i) pk.vel0.push_back(0.0);
-        }
-    }
-    // landmarks
-    const uint8_t* marg = pnp ? p.lm_const : p.lm_marg;
-    for (int l = 0; l < L; ++l) {
-        for (int i = 0; i < 3; ++i) pk.lm_xyz0.push_back(p.lm_xyz[3 * l + i]);
-        pk.lm_var.push_back(lm_used[l]);
-        pk.lm_marg.push_back(marg ? (marg[l] ? 1 : 0) : 0);
-    }
-    // observations sorted by landmark (stable)
-    std::vector<int32_t> perm(N);
-    for (int o = 0; o < N; ++o) perm[o] = o;
-    std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return p.obs_lm[a] < p.obs_lm[b]; });
-    std::vector<int32_t> lptr(L + 1, 0);
-    for (int o = 0; o < N; ++o) lptr[p.obs_lm[o] + 1]++;
-    for (int l = 0; l < L; ++l) lptr[l + 1] += lptr[l];
-    pk.lm_ptr.insert(pk.lm_ptr.end(), lptr.begin(), lptr.end());
-    for (int q = 0; q < N; ++q) {
-        int o = perm[q];
-        pk.obs_kf.push_back(p.obs_kf[o]);
-        pk.obs_lm.push_back(p.obs_lm[o]);
-        pk.obs_uv.push_back(p.obs_uv[2 * o]);
-        pk.obs_uv.push_back(p.obs_uv[2 * o + 1]);
-    }
-    std::vector<int32_t> kptr(K + 1, 0);
-    for (int q = 0; q < N; ++q) kptr[p.obs_kf[perm[q]] + 1]++;
-    for (int k = 0; k < K; ++k) kptr[k + 1] += kptr[k];
-    std::vector<int32_t> fill(K, 0), kobs(N);
-    for (int q = 0; q < N; ++q) {
-        int k = p.obs_kf[perm[q]];
-        kobs[kptr[k] + fill[k]++] = q;
-    }
-    pk.kf_ptr.insert(pk.kf_ptr.end(), kptr.begin(), kptr.end());
-    pk.kf_obs.insert(pk.kf_obs.end(), kobs.begin(), kobs.end());
-    pk.perm.push_back(std::move(perm));
-    pk.win.push_back(w);
-    pk.N_total += N;
+    pk.K_total += K;
     pk.L_total += L;
+    pk.N_total += N;
+    pk.lmptr_total += L + 1;
+    pk.kfptr_total += K + 1;
+    pk.win.push_back(w);
     return VIO_OK;
 }
 
-template <class T>
-size_t bytes_of(const std::vector<T>& v) { return v.size() * sizeof(T); }
+void layout_regions(Packed& pk, int n, bool cluster) {
+    BaRegions& R = pk.R;
+    size_t o = 0;
+    auto take = [&o](size_t bytes) {
+        const size_t at = o;
+        o = (o + std::max<size_t>(bytes, 16) + 255) & ~(size_t)255;
+        return at;
+    };
+    R.win = take(sizeof(BaWin) * (size_t)n);
+    R.pose_raw = take(sizeof(double) * 24 * (size_t)pk.K_total);
+    R.kf_const = take((size_t)pk.K_total);
+    R.lm_xyz0 = take(sizeof(double) * 3 * (size_t)pk.L_total);
+    R.lm_var = take((size_t)pk.L_total);
+    R.lm_marg = take((size_t)pk.L_total);
+    R.lm_ptr = take(sizeof(int32_t) * (size_t)pk.lmptr_total);
+    R.obs_kf = take(sizeof(int32_t) * (size_t)pk.N_total);
+    R.obs_lm = take(sizeof(int32_t) * (size_t)pk.N_total);
+    R.obs_uv = take(sizeof(float) * 2 * (size_t)pk.N_total);
+    R.kf_ptr = take(sizeof(int32_t) * (size_t)pk.kfptr_total);
+    R.kf_obs = take(sizeof(int32_t) * (size_t)pk.N_total);
+    R.preint = take(sizeof(vio_preint) * (size_t)pk.K_total);
+    R.preint_valid = take((size_t)pk.K_total);
+    R.vel0 = take(sizeof(double) * 3 * (size_t)pk.K_total);
+    R.obs_perm = take(sizeof(int32_t) * (size_t)pk.N_total);
+    R.in_bytes = o;
+    R.out_begin = o;
+    R.i32 = take(sizeof(int32_t) * SI_COUNT * (size_t)n);
+    R.sum = take(sizeof(double) * SD_COUNT * (size_t)n);
+    R.out = take(sizeof(double) * (size_t)pk.out_total);
+    R.trace = take(sizeof(vio_ba_iteration) * (size_t)pk.tr_total);
+    R.u8 = take((size_t)pk.N_total);
+    R.bad = take((size_t)pk.L_total);
+    R.csync = cluster ? take(sizeof(int) * PH_SYNC_INTS * (size_t)n) : 0;
+    R.out_bytes = o - R.out_begin;
+    R.ws = take(sizeof(double) * (size_t)pk.ws_total);
+    R.total = o;
+}
+
+// Writes window w's arrays into the input staging image (base = byte 0 of the inputs region): poses,
+// landmarks, observations in landmark order (a counting sort, stable: the caller's order within a landmark)
+// with their CSR, the per-keyframe observation lists, and the sorted position -> caller's index map.
+void fill_window(const vio_ba_problem& p, const BaWin& w, const BaRegions& R, uint8_t* base, std::vector<int32_t>& fillv) {
+    const int K = w.K, L = w.L, N = w.N;
+    const bool vi = w.is_vi, pnp = w.is_pnp;
+    double* pose_raw = reinterpret_cast<double*>(base + R.pose_raw) + 24 * w.o_pose;
+    uint8_t* kf_const = base + R.kf_const + w.o_pose;
+    vio_preint* preint = reinterpret_cast<vio_preint*>(base + R.preint) + w.o_pose;
+    uint8_t* preint_valid = base + R.preint_valid + w.o_pose;
+    double* vel0 = reinterpret_cast<double*>(base + R.vel0) + 3 * w.o_pose;
+    for (int k = 0; k < K; ++k) {
+        double* q = pose_raw + 24 * k;
+        std::memcpy(q, p.T_wb_init[k].R, 9 * sizeof(double));
+        std::memcpy(q + 9, p.T_wb_init[k].t, 3 * sizeof(double));
+        std::memcpy(q + 12, p.T_cb[k].R, 9 * sizeof(double));
+        std::memcpy(q + 21, p.T_cb[k].t, 3 * sizeof(double));
+        kf_const[k] = p.kf_const[k] ? 1 : 0;
+        if (vi) {
+            preint[k] = p.preint[k];
+            preint_valid[k] = k >= 1 && p.preint_valid[k] ? 1 : 0;
+            for (int i = 0; i < 3; ++i) vel0[3 * k + i] = p.vel[3 * k + i];
+        } else {
+            std::memset(&preint[k], 0, sizeof(vio_preint));
+            preint_valid[k] = 0;
+            for (int i = 0; i < 3; ++i) vel0[3 * k + i] = 0.0;
+        }
+    }
+    // landmark CSR (counts, then the exclusive scan)
+    int32_t* lptr = reinterpret_cast<int32_t*>(base + R.lm_ptr) + w.o_lmptr;
+    std::fill(lptr, lptr + L + 1, 0);
+    for (int o = 0; o < N; ++o) lptr[p.obs_lm[o] + 1]++;
+    for (int l = 0; l < L; ++l) lptr[l + 1] += lptr[l];
+    if (L > 0) std::memcpy(reinterpret_cast<double*>(base + R.lm_xyz0) + 3 * w.o_lm, p.lm_xyz, sizeof(double) * 3 * L);
+    uint8_t* lm_var = base + R.lm_var + w.o_lm;
+    uint8_t* lm_marg = base + R.lm_marg + w.o_lm;
+    const uint8_t* marg = pnp ? p.lm_const : p.lm_marg;
+    for (int l = 0; l < L; ++l) {
+        // a landmark is a free parameter when it is not constant and some observation uses it
+        lm_var[l] = !pnp && !p.lm_const[l] && lptr[l + 1] > lptr[l] ? 1 : 0;
+        lm_marg[l] = marg ? (marg[l] ? 1 : 0) : 0;
+    }
+    // observations sorted by landmark, stable
+    int32_t* perm = reinterpret_cast<int32_t*>(base + R.obs_perm) + w.o_obs;
+    fillv.assign(lptr, lptr + L);
+    for (int o = 0; o < N; ++o) perm[fillv[p.obs_lm[o]]++] = o;
+    int32_t* obs_kf = reinterpret_cast<int32_t*>(base + R.obs_kf) + w.o_obs;
+    int32_t* obs_lm = reinterpret_cast<int32_t*>(base + R.obs_lm) + w.o_obs;
+    float* obs_uv = reinterpret_cast<float*>(base + R.obs_uv) + 2 * w.o_obs;
+    int32_t* kptr = reinterpret_cast<int32_t*>(base + R.kf_ptr) + w.o_kfptr;
+    std::fill(kptr, kptr + K + 1, 0);
+    for (int q = 0; q < N; ++q) {
+        const int o = perm[q];
+        obs_kf[q] = p.obs_kf[o];
+        obs_lm[q] = p.obs_lm[o];
+        obs_uv[2 * q] = p.obs_uv[2 * o];
+        obs_uv[2 * q + 1] = p.obs_uv[2 * o + 1];
+        kptr[obs_kf[q] + 1]++;
+    }
+    for (int k = 0; k < K; ++k) kptr[k + 1] += kptr[k];
+    int32_t* kobs = reinterpret_cast<int32_t*>(base + R.kf_obs) + w.o_obs;
+    fillv.assign(kptr, kptr + K);
+    for (int q = 0; q < N; ++q) kobs[fillv[obs_kf[q]]++] = q;
+}
 
 }  // namespace
 
@@ -242,8 +316,10 @@ size_t bytes_of(const std::vector<T>& v) { return v.size() * sizeof(T); }
 struct BaDevice {
     int n = 0;
     Packed pk;
-    // device allocations (owned)
-    std::vector<void*> allocs;
+    void* mem = nullptr;                  // the batch's allocation (owned: vio_ba_batch); one-shot solves use
+                                          // the context's arena
+    std::vector<uint8_t> stage_own;       // vio_ba_batch: the input image (kept: set_preint, result scatter)
+    uint8_t* stage = nullptr;             // the input image the batch was uploaded from
     BaPools P{};
     void* prof_buf = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -255,7 +331,6 @@ struct BaDevice {
     double ms_sum = 0.0;
     int ms_count = 0;
     bool timing_pending = false;
-    std::vector<int32_t> perm_host;
 };
 
 static bool env_flag(const char* name) {
@@ -274,94 +349,98 @@ static bool cluster_wanted(const vio_ctx* ctx, int n) {
     return n <= kClusterMaxWindows;
 }
 
-static int upload_batch(vio_ctx* ctx, BaDevice& d) {
-    Packed& pk = d.pk;
-    auto up = [&](const void* src, size_t bytes, void** dst) -> int {
-        size_t b = std::max<size_t>(bytes, 16);
-        void* p = nullptr;
-        VIO_HIP(ctx, hipMalloc(&p, b));
-        d.allocs.push_back(p);
-        if (bytes) VIO_HIP(ctx, hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, ctx->stream));
-        *dst = p;
-        return VIO_OK;
-    };
-    void* ptr;
-    int rc;
-#define UP(vec, field, type)                                                  \
-    if ((rc = up(vec.data(), bytes_of(vec), &ptr)) != VIO_OK) return rc;      \
-    d.P.field = (type)ptr;
-    // landmark chunks per Schur split-k group (phase route): a full config-4 shard (>= 256 windows)
-    // fills the chip with 2 groups per window and halves ph_solve's partial sums; smaller batches keep
-    // more, shorter groups (latency): 3 below 64 windows, 5 up to 255 (sweep of 2/3/4/5/10 at 1..256
-    // windows, profiles/r4e_gs_sweep.log); the cluster route: one chunk per group, the group's member owns
-    // its landmarks
+// internal status of a cluster launch whose bounded hand-off wait expired (the caller falls back to the
+// phase route; VIO_EDEVICE if that fails too)
+constexpr int kClusterTimeout = 1000;
+
+// Packs problems[0..n) and uploads them: descriptors, route choice, one device allocation (the batch's own,
+// or the context's grow-only arena for a one-shot solve), the input image filled on the host (a vector for
+// a reusable batch, the context's pinned staging buffer for a one-shot solve) and one host-to-device copy.
+// landmark chunks per Schur split-k group (phase route): a full config-4 shard (>= 256 windows) fills the
+// chip with 2 groups per window and halves ph_solve's partial sums; smaller batches keep more, shorter
+// groups (latency): 3 below 64 windows, 5 up to 255 (sweep of 2/3/4/5/10 at 1..256 windows,
+// profiles/r4e_gs_sweep.log); the cluster route: one chunk per group, the group's member owns its landmarks
+static int schur_group_size(int n, bool cluster) {
     const char* gse = std::getenv("VIO_BA_SCHUR_GS");  // experiment override
+    return cluster ? 1 : gse ? std::max(1, std::atoi(gse)) : n >= 256 ? 10 : n >= 64 ? 5 : 3;
+}
+
+static int pack_upload(vio_ctx* ctx, BaDevice& d, const vio_ba_problem* probs, int n, bool allow_cluster) {
+    Packed& pk = d.pk;
+    d.n = n;
+    pk.win.reserve(n);
+    std::vector<uint32_t> scratch;
+    for (int i = 0; i < n; ++i)
+        if (int rc = analyze_window(ctx, probs[i], pk, scratch)) return rc;
     static const int cmax = [] {
         const char* v = std::getenv("VIO_BA_CLUSTER_C");  // experiment override: members per window
         return v ? std::atoi(v) : 0;
     }();
     // (an explicitly requested cluster route takes whatever members fit: no minimum per landmark chunk)
     const int cm = cmax > 0 ? cmax : ctx->ba_route == VIO_BA_ROUTE_CLUSTER ? (1 << 20) : 0;
-    d.cluster_C = cluster_wanted(ctx, d.n) ? ba_cluster_members(pk.win.data(), d.n, cm) : 0;
-    const int gs = d.cluster_C ? 1 : gse ? std::max(1, std::atoi(gse)) : pk.win.size() >= 256 ? 10 : pk.win.size() >= 64 ? 5 : 3;
+    d.cluster_C = allow_cluster && cluster_wanted(ctx, n) ? ba_cluster_members(pk.win.data(), n, cm) : 0;
+    const int gs = schur_group_size(n, d.cluster_C > 0);
     for (BaWin& w : pk.win) w.gs = gs;
-    UP(pk.win, win, const BaWin*);
-    UP(pk.pose_raw, pose_raw, const double*);
-    UP(pk.kf_const, kf_const, const uint8_t*);
-    UP(pk.lm_xyz0, lm_xyz0, const double*);
-    UP(pk.lm_var, lm_var, const uint8_t*);
-    UP(pk.lm_marg, lm_marg, const uint8_t*);
-    UP(pk.lm_ptr, lm_ptr, const int32_t*);
-    UP(pk.obs_kf, obs_kf, const int32_t*);
-    UP(pk.obs_lm, obs_lm, const int32_t*);
-    UP(pk.obs_uv, obs_uv, const float*);
-    UP(pk.kf_ptr, kf_ptr, const int32_t*);
-    UP(pk.kf_obs, kf_obs, const int32_t*);
-    UP(pk.preint, preint, const vio_preint*);
-    UP(pk.preint_valid, preint_valid, const uint8_t*);
-    UP(pk.vel0, vel0, const double*);
-#undef UP
-    {   // sorted position -> caller's observation index, all windows back to back (result records)
-        std::vector<int32_t> perm;
-        perm.reserve(pk.N_total);
-        for (const auto& p : pk.perm) perm.insert(perm.end(), p.begin(), p.end());
-        if ((rc = up(perm.data(), bytes_of(perm), &ptr)) != VIO_OK) return rc;
-        d.P.obs_perm = (const int32_t*)ptr;
-        d.perm_host = std::move(perm);  // kept alive for the async upload
+    layout_regions(pk, n, d.cluster_C > 0);
+    const BaRegions& R = pk.R;
+    uint8_t* dev = nullptr;
+    if (d.reusable) {
+        {
+            DeviceScope dev_scope(ctx->device);
+            VIO_HIP(ctx, dev_scope.err);
+            VIO_HIP(ctx, hipMalloc(&d.mem, R.total));
+        }
+        dev = static_cast<uint8_t*>(d.mem);
+        d.stage_own.resize(R.in_bytes);
+        d.stage = d.stage_own.data();
+    } else {
+        dev = static_cast<uint8_t*>(ctx_buffer(ctx, kSlotBaSolve, R.total));
+        d.stage = static_cast<uint8_t*>(ctx_host_buffer(ctx, kHostSlotBaIn, R.in_bytes));
+        if (!dev || !d.stage) {
+            set_error(ctx, "vio_ba_solve: device or pinned host allocation failed");
+            return VIO_ENOMEM;
+        }
     }
-    auto alloc = [&](size_t bytes, void** dst) -> int {
-        void* p = nullptr;
-        VIO_HIP(ctx, hipMalloc(&p, std::max<size_t>(bytes, 16)));
-        d.allocs.push_back(p);
-        *dst = p;
-        return VIO_OK;
-    };
-    if ((rc = alloc(sizeof(double) * pk.ws_total, &ptr)) != VIO_OK) return rc;
-    d.P.ws = (double*)ptr;
-    if ((rc = alloc(sizeof(double) * pk.out_total, &ptr)) != VIO_OK) return rc;
-    d.P.out = (double*)ptr;
-    if ((rc = alloc(pk.N_total, &ptr)) != VIO_OK) return rc;
-    d.P.out_u8 = (uint8_t*)ptr;
-    if ((rc = alloc(pk.L_total, &ptr)) != VIO_OK) return rc;
-    d.P.out_bad = (uint8_t*)ptr;
-    if ((rc = alloc(sizeof(int32_t) * SI_COUNT * d.n, &ptr)) != VIO_OK) return rc;
-    d.P.out_i32 = (int32_t*)ptr;
-    if ((rc = alloc(sizeof(double) * SD_COUNT * d.n, &ptr)) != VIO_OK) return rc;
-    d.P.out_sum = (double*)ptr;
-    if ((rc = alloc(sizeof(vio_ba_iteration) * pk.tr_total, &ptr)) != VIO_OK) return rc;
-    d.P.out_trace = (vio_ba_iteration*)ptr;
-    if (d.cluster_C) {
-        if ((rc = alloc(sizeof(int) * PH_SYNC_INTS * (size_t)d.n, &ptr)) != VIO_OK) return rc;
-        d.P.csync = (int*)ptr;
+    std::memcpy(d.stage + R.win, pk.win.data(), sizeof(BaWin) * (size_t)n);
+    std::vector<int32_t> fillv;
+    for (int i = 0; i < n; ++i) fill_window(probs[i], pk.win[i], R, d.stage, fillv);
+    BaPools& P = d.P;
+    P.win = reinterpret_cast<const BaWin*>(dev + R.win);
+    P.pose_raw = reinterpret_cast<const double*>(dev + R.pose_raw);
+    P.kf_const = dev + R.kf_const;
+    P.lm_xyz0 = reinterpret_cast<const double*>(dev + R.lm_xyz0);
+    P.lm_var = dev + R.lm_var;
+    P.lm_marg = dev + R.lm_marg;
+    P.lm_ptr = reinterpret_cast<const int32_t*>(dev + R.lm_ptr);
+    P.obs_kf = reinterpret_cast<const int32_t*>(dev + R.obs_kf);
+    P.obs_lm = reinterpret_cast<const int32_t*>(dev + R.obs_lm);
+    P.obs_uv = reinterpret_cast<const float*>(dev + R.obs_uv);
+    P.kf_ptr = reinterpret_cast<const int32_t*>(dev + R.kf_ptr);
+    P.kf_obs = reinterpret_cast<const int32_t*>(dev + R.kf_obs);
+    P.preint = reinterpret_cast<const vio_preint*>(dev + R.preint);
+    P.preint_valid = dev + R.preint_valid;
+    P.vel0 = reinterpret_cast<const double*>(dev + R.vel0);
+    P.obs_perm = reinterpret_cast<const int32_t*>(dev + R.obs_perm);
+    P.out_i32 = reinterpret_cast<int32_t*>(dev + R.i32);
+    P.out_sum = reinterpret_cast<double*>(dev + R.sum);
+    P.out = reinterpret_cast<double*>(dev + R.out);
+    P.out_trace = reinterpret_cast<vio_ba_iteration*>(dev + R.trace);
+    P.out_u8 = dev + R.u8;
+    P.out_bad = dev + R.bad;
+    P.csync = d.cluster_C ? reinterpret_cast<int*>(dev + R.csync) : nullptr;
+    P.ws = reinterpret_cast<double*>(dev + R.ws);
+    VIO_DEVICE(ctx);
+    VIO_HIP(ctx, hipMemcpyAsync(dev, d.stage, R.in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (d.reusable) {
+        VIO_HIP(ctx, hipEventCreate(&d.ev0));
+        VIO_HIP(ctx, hipEventCreate(&d.ev1));
     }
-    VIO_HIP(ctx, hipEventCreate(&d.ev0));
-    VIO_HIP(ctx, hipEventCreate(&d.ev1));
     return VIO_OK;
 }
 
 static void free_batch(BaDevice& d) {
-    for (void* p : d.allocs) (void)hipFree(p);
-    d.allocs.clear();
+    if (d.mem) (void)hipFree(d.mem);
+    d.mem = nullptr;
     if (d.prof_buf) (void)hipFree(d.prof_buf);
     d.prof_buf = nullptr;
     if (d.ev0) (void)hipEventDestroy(d.ev0);
@@ -375,56 +454,73 @@ static void free_batch(BaDevice& d) {
         if (ev) (void)hipEventDestroy(ev), ev = nullptr;
 }
 
-// the cluster route's per-window error words (a bounded hand-off wait that expired): VIO_EDEVICE
+// the cluster route's per-window error words (a bounded hand-off wait that expired), from a host image of
+// the hand-off state
+static bool cluster_timed_out(const BaDevice& d, const int* sync) {
+    for (int i = 0; i < d.n; ++i)
+        if (sync[(size_t)PH_SYNC_INTS * i + PH_SYNC_ERR]) return true;
+    return false;
+}
 static int check_cluster(vio_ctx* ctx, BaDevice& d) {
     if (!d.cluster_C || !d.P.csync) return VIO_OK;
     std::vector<int> sync((size_t)PH_SYNC_INTS * d.n);
     VIO_HIP(ctx, hipMemcpyAsync(sync.data(), d.P.csync, sizeof(int) * sync.size(), hipMemcpyDeviceToHost, ctx->stream));
     VIO_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    for (int i = 0; i < d.n; ++i)
-        if (sync[(size_t)PH_SYNC_INTS * i + 192]) {
-            set_error(ctx, "cluster route: a hand-off wait timed out (workgroups not co-resident?)");
-            return VIO_EDEVICE;
-        }
+    if (cluster_timed_out(d, sync.data())) {
+        set_error(ctx, "cluster route: a hand-off wait timed out (workgroups not co-resident?)");
+        return kClusterTimeout;
+    }
     return VIO_OK;
 }
 
-static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
-    Packed& pk = d.pk;
-    if (int rc = check_cluster(ctx, d)) return rc;
-    std::vector<double> out(pk.out_total);
-    std::vector<uint8_t> u8(pk.N_total), bad(pk.L_total);
-    std::vector<int32_t> si(SI_COUNT * d.n);
-    std::vector<double> sd(SD_COUNT * d.n);
-    bool want_trace = false;
-    for (int i = 0; i < d.n; ++i) want_trace |= outs[i].trace != nullptr && outs[i].trace_cap > 0;
-    std::vector<vio_ba_iteration> tr(want_trace ? pk.tr_total : 0);
-    if (want_trace)
-        VIO_HIP(ctx, hipMemcpyAsync(tr.data(), d.P.out_trace, sizeof(vio_ba_iteration) * tr.size(),
-                                    hipMemcpyDeviceToHost, ctx->stream));
-    VIO_HIP(ctx, hipMemcpyAsync(out.data(), d.P.out, sizeof(double) * out.size(), hipMemcpyDeviceToHost, ctx->stream));
-    VIO_HIP(ctx, hipMemcpyAsync(u8.data(), d.P.out_u8, u8.size(), hipMemcpyDeviceToHost, ctx->stream));
-    VIO_HIP(ctx, hipMemcpyAsync(bad.data(), d.P.out_bad, bad.size(), hipMemcpyDeviceToHost, ctx->stream));
-    VIO_HIP(ctx, hipMemcpyAsync(si.data(), d.P.out_i32, sizeof(int32_t) * si.size(), hipMemcpyDeviceToHost, ctx->stream));
-    VIO_HIP(ctx, hipMemcpyAsync(sd.data(), d.P.out_sum, sizeof(double) * sd.size(), hipMemcpyDeviceToHost, ctx->stream));
+// Fetches the outputs region (one device-to-host copy into the context's pinned staging buffer; the cluster
+// route's error words ride along) and waits for it.  kClusterTimeout when a cluster hand-off wait expired.
+static int fetch_outputs(vio_ctx* ctx, BaDevice& d, const uint8_t** img) {
+    const BaRegions& R = d.pk.R;
+    auto* h = static_cast<uint8_t*>(ctx_host_buffer(ctx, kHostSlotBaOut, R.out_bytes));
+    if (!h) {
+        set_error(ctx, "BA download: pinned host allocation failed");
+        return VIO_ENOMEM;
+    }
+    const uint8_t* dev = reinterpret_cast<const uint8_t*>(d.P.out_i32) - R.i32;  // the region's device base
+    VIO_HIP(ctx, hipMemcpyAsync(h, dev + R.out_begin, R.out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     VIO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *img = h - R.out_begin;  // indexable with the region offsets
+    if (d.cluster_C && cluster_timed_out(d, reinterpret_cast<const int*>(*img + R.csync))) {
+        set_error(ctx, "cluster route: a hand-off wait timed out (workgroups not co-resident?)");
+        return kClusterTimeout;
+    }
+    return VIO_OK;
+}
+
+// scatters the fetched outputs into the callers' buffers (observations back in the caller's order)
+static void scatter_outputs(const BaDevice& d, const uint8_t* img, vio_ba_output* outs) {
+    const Packed& pk = d.pk;
+    const BaRegions& R = pk.R;
+    const double* out = reinterpret_cast<const double*>(img + R.out);
+    const uint8_t* u8 = img + R.u8;
+    const uint8_t* bad = img + R.bad;
+    const int32_t* si = reinterpret_cast<const int32_t*>(img + R.i32);
+    const double* sd = reinterpret_cast<const double*>(img + R.sum);
+    const vio_ba_iteration* tr = reinterpret_cast<const vio_ba_iteration*>(img + R.trace);
+    const int32_t* perm_all = reinterpret_cast<const int32_t*>(d.stage + R.obs_perm);
     for (int i = 0; i < d.n; ++i) {
         const BaWin& w = pk.win[i];
         vio_ba_output& o = outs[i];
         BaOutLayout OL = ba_out_layout(w.K, w.L, w.N);
-        const double* ob = out.data() + w.o_out;
+        const double* ob = out + w.o_out;
         if (o.T_wb)
             for (int k = 0; k < w.K; ++k) {
                 std::memcpy(o.T_wb[k].R, ob + OL.T_wb + 12 * k, 9 * sizeof(double));
                 std::memcpy(o.T_wb[k].t, ob + OL.T_wb + 12 * k + 9, 3 * sizeof(double));
             }
         if (o.lm_xyz) std::memcpy(o.lm_xyz, ob + OL.lm, sizeof(double) * 3 * w.L);
-        const std::vector<int32_t>& perm = pk.perm[i];
-        for (int q = 0; q < w.N; ++q) {
-            if (o.obs_chi2) o.obs_chi2[perm[q]] = ob[OL.chi2 + q];
-            if (o.obs_outlier) o.obs_outlier[perm[q]] = u8[w.o_obs + q];
-        }
-        if (o.lm_bad) std::memcpy(o.lm_bad, bad.data() + w.o_lm, w.L);
+        const int32_t* perm = perm_all + w.o_obs;
+        if (o.obs_chi2)
+            for (int q = 0; q < w.N; ++q) o.obs_chi2[perm[q]] = ob[OL.chi2 + q];
+        if (o.obs_outlier)
+            for (int q = 0; q < w.N; ++q) o.obs_outlier[perm[q]] = u8[w.o_obs + q];
+        if (o.lm_bad) std::memcpy(o.lm_bad, bad + w.o_lm, w.L);
         if (w.is_vi) {
             if (o.vel) std::memcpy(o.vel, ob + OL.vel, sizeof(double) * 3 * w.K);
             if (o.bg) std::memcpy(o.bg, ob + OL.bias, sizeof(double) * 3);
@@ -433,8 +529,8 @@ static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
         if (o.summary) {
             vio_ba_summary& s = *o.summary;
             std::memset(&s, 0, sizeof s);
-            const int32_t* a = si.data() + SI_COUNT * i;
-            const double* b = sd.data() + SD_COUNT * i;
+            const int32_t* a = si + SI_COUNT * i;
+            const double* b = sd + SD_COUNT * i;
             s.success = a[SI_SUCCESS];
             s.termination = a[SI_TERM];
             s.iterations = a[SI_ITERS];
@@ -452,6 +548,12 @@ static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
             for (int q = 0; q < n_it; ++q) o.trace[q] = tr[w.o_tr + q];
         }
     }
+}
+
+static int download_batch(vio_ctx* ctx, BaDevice& d, vio_ba_output* outs) {
+    const uint8_t* img = nullptr;
+    if (int rc = fetch_outputs(ctx, d, &img)) return rc;
+    scatter_outputs(d, img, outs);
     return VIO_OK;
 }
 
@@ -566,6 +668,37 @@ static int launch(vio_ctx* ctx, BaDevice& d, bool timed) {
     return VIO_OK;
 }
 
+static int solve_one_shot(vio_ctx* ctx, const vio_ba_problem* probs, vio_ba_output* outs, int n, bool allow_cluster) {
+    BaDevice d;
+    d.reusable = false;
+    int rc = pack_upload(ctx, d, probs, n, allow_cluster);
+    if (rc == VIO_OK) rc = launch(ctx, d, false);
+    if (rc == VIO_OK) rc = download_batch(ctx, d, outs);
+    if (rc != VIO_OK) (void)hipStreamSynchronize(ctx->stream);  // the arena may be reused or freed next
+    free_batch(d);
+    return rc;
+}
+
+// A reusable batch whose last cluster run timed out moves to the phase route for good: the descriptors get
+// the phase route's Schur group size, the captured cluster graph goes, and the batch runs again (its inputs
+// are untouched: every run starts from them).  The caller then reads the phase route's results.
+static int batch_fall_back(vio_ctx* ctx, BaDevice& d) {
+    d.cluster_C = 0;
+    d.P.csync = nullptr;
+    const int gs = schur_group_size(d.n, false);
+    for (BaWin& w : d.pk.win) w.gs = gs;
+    std::memcpy(d.stage + d.pk.R.win, d.pk.win.data(), sizeof(BaWin) * (size_t)d.n);
+    VIO_DEVICE(ctx);
+    VIO_HIP(ctx, hipMemcpyAsync((void*)d.P.win, d.stage + d.pk.R.win, sizeof(BaWin) * (size_t)d.n,
+                                hipMemcpyHostToDevice, ctx->stream));
+    if (d.phase_graph) (void)hipGraphExecDestroy(d.phase_graph);
+    d.phase_graph = nullptr;
+    d.timing_pending = false;  // (the timed-out run's time is not a solve's)
+    if (int rc = launch(ctx, d, false)) return rc;
+    VIO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return VIO_OK;
+}
+
 }  // namespace vio360
 
 using namespace vio360;
@@ -652,8 +785,11 @@ int vio_ctx_create(int device, vio_ctx** out) {
 void vio_ctx_destroy(vio_ctx* ctx) {
     if (!ctx) return;
     DeviceScope _vio_dev_scope(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
     for (void* p : ctx->bufs)
         if (p) (void)hipFree(p);
+    for (void* p : ctx->hbufs)
+        if (p) (void)hipHostFree(p);
     for (hipEvent_t e : ctx->imu_ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->tri_ev)
@@ -676,14 +812,14 @@ int vio_ba_batch_create(vio_ctx* ctx, const vio_ba_problem* probs, int n, vio_ba
     DeviceScope _vio_dev_scope(ctx->device);
     vio_ba_batch* b = new vio_ba_batch();
     b->ctx = ctx;
-    b->dev.n = n;
     b->dev.reusable = true;
-    for (int i = 0; i < n; ++i) {
-        int rc = pack_window(ctx, probs[i], b->dev.pk);
-        if (rc != VIO_OK) { delete b; return rc; }
+    int rc = pack_upload(ctx, b->dev, probs, n, true);
+    if (rc != VIO_OK) {
+        (void)hipStreamSynchronize(ctx->stream);
+        free_batch(b->dev);
+        delete b;
+        return rc;
     }
-    int rc = upload_batch(ctx, b->dev);
-    if (rc != VIO_OK) { free_batch(b->dev); delete b; return rc; }
     *out = b;
     return VIO_OK;
 }
@@ -706,8 +842,8 @@ int vio_ba_batch_run(vio_ba_batch* b) {
 int vio_ba_batch_set_preint(vio_ba_batch* b, const vio_preint* src, int count, int on_device) {
     if (!b || (count > 0 && !src)) return VIO_EINVAL;
     vio_ctx* ctx = b->ctx;
-    Packed& pk = b->dev.pk;
-    if (count != (int)pk.preint.size()) {
+    const Packed& pk = b->dev.pk;
+    if (count != (int)pk.K_total) {
         set_error(ctx, "vio_ba_batch_set_preint: count must be the batch's total keyframe count");
         return VIO_EINVAL;
     }
@@ -717,8 +853,9 @@ int vio_ba_batch_set_preint(vio_ba_batch* b, const vio_preint* src, int count, i
     if (on_device) {
         VIO_HIP(ctx, hipMemcpyAsync((void*)b->dev.P.preint, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
     } else {
-        std::memcpy(pk.preint.data(), src, bytes);  // the staging copy outlives the async upload
-        VIO_HIP(ctx, hipMemcpyAsync((void*)b->dev.P.preint, pk.preint.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+        uint8_t* stage = b->dev.stage + pk.R.preint;  // the batch's input image outlives the async upload
+        std::memcpy(stage, src, bytes);
+        VIO_HIP(ctx, hipMemcpyAsync((void*)b->dev.P.preint, stage, bytes, hipMemcpyHostToDevice, ctx->stream));
     }
     return VIO_OK;
 }
@@ -727,13 +864,17 @@ int vio_ba_batch_sync(vio_ba_batch* b) {
     if (!b) return VIO_EINVAL;
     VIO_DEVICE(b->ctx);
     VIO_HIP(b->ctx, hipStreamSynchronize(b->ctx->stream));
-    return check_cluster(b->ctx, b->dev);
+    int rc = check_cluster(b->ctx, b->dev);
+    if (rc == kClusterTimeout) rc = batch_fall_back(b->ctx, b->dev);
+    return rc;
 }
 
 int vio_ba_batch_download(vio_ba_batch* b, vio_ba_output* outs) {
     if (!b || !outs) return VIO_EINVAL;
     VIO_DEVICE(b->ctx);
-    return download_batch(b->ctx, b->dev, outs);
+    int rc = download_batch(b->ctx, b->dev, outs);
+    if (rc == kClusterTimeout && (rc = batch_fall_back(b->ctx, b->dev)) == VIO_OK) rc = download_batch(b->ctx, b->dev, outs);
+    return rc == kClusterTimeout ? VIO_EDEVICE : rc;
 }
 
 int vio_ba_batch_kernel_ms(vio_ba_batch* b, double* avg_ms, int* count) {
@@ -893,13 +1034,13 @@ int vio_ba_solve_batched(vio_ctx* ctx, const vio_ba_problem* probs, vio_ba_outpu
         }
         return VIO_OK;
     }
-    vio_ba_batch* b = nullptr;
-    int rc = vio_ba_batch_create(ctx, probs, n, &b);
-    if (rc != VIO_OK) return rc;
-    rc = launch(ctx, b->dev, false);
-    if (rc == VIO_OK) rc = download_batch(ctx, b->dev, outs);
-    vio_ba_batch_destroy(b);
-    return rc;
+    // one-shot solve (once per keyframe in the reference: Estimator.cpp:763-790 -> RunLocalBA / RunVIBA):
+    // the context's grow-only device arena and pinned staging buffers, one host-to-device copy of the
+    // packed inputs, one device-to-host copy of the outputs region -- no allocation once the arena fits.
+    // A cluster launch whose hand-off wait expired is solved again on the phase route.
+    int rc = solve_one_shot(ctx, probs, outs, n, true);
+    if (rc == kClusterTimeout) rc = solve_one_shot(ctx, probs, outs, n, false);
+    return rc == kClusterTimeout ? VIO_EDEVICE : rc;
 }
 
 int vio_ba_solve(vio_ctx* ctx, const vio_ba_problem* prob, vio_ba_output* out) {

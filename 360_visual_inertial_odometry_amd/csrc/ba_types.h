@@ -17,6 +17,7 @@ constexpr int BA_NF_MAX = 96;    // reduced (Schur) system size bound: 6*15 pose
 constexpr int BA_STAGE = 3392;   // doubles of LDS for the Schur k-panels (chunk depth derived per tile count)
 constexpr int BA_GCOL = 256;     // max k rows per Schur chunk
 constexpr int PH_SYNC_INTS = 512; // cluster route: ints of hand-off state per window (2 KB)
+constexpr int PH_SYNC_ERR = 192;  // ... of which the window's error word (a bounded hand-off wait expired)
 
 // per-window descriptor (host-packed, read-only on device)
 struct BaWin {

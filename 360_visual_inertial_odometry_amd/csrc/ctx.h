@@ -14,6 +14,9 @@ struct vio_ctx {
     // grow-only device buffers keyed by slot
     std::vector<void*> bufs;
     std::vector<size_t> caps;
+    // grow-only pinned host staging buffers keyed by slot
+    std::vector<void*> hbufs;
+    std::vector<size_t> hcaps;
     // IMU preintegration kernel timing (created on first use)
     hipEvent_t imu_ev[2] = {nullptr, nullptr};
     float imu_ms = -1.f;
@@ -33,6 +36,8 @@ void set_error(vio_ctx* ctx, const std::string& msg);
 int hip_fail(vio_ctx* ctx, hipError_t e, const char* what);
 // device buffer of at least `bytes` for slot `slot` (contents undefined); nullptr on failure
 void* ctx_buffer(vio_ctx* ctx, int slot, size_t bytes);
+// pinned host buffer of at least `bytes` for slot `slot` (contents undefined); nullptr on failure
+void* ctx_host_buffer(vio_ctx* ctx, int slot, size_t bytes);
 // scratch slots owned by vio_imu_preintegrate
 enum { kSlotImuData = 8, kSlotImuIntervals = 9, kSlotImuOut = 10 };
 // scratch slots owned by vio_triangulate
@@ -47,6 +52,10 @@ enum { kSlotImuInit = 16 };
 enum { kSlotMonoInit = 17 };
 // vio_lie_eval inputs and outputs
 enum { kSlotLie = 18 };
+// the one-shot window solves' arena (vio_ba_solve[_batched]: inputs, outputs, workspace)
+enum { kSlotBaSolve = 19 };
+// pinned host slots: the one-shot solves' input image and every BA download's outputs image
+enum { kHostSlotBaIn = 0, kHostSlotBaOut = 1 };
 
 // Selects a device for the rest of the enclosing scope and restores the calling thread's current
 // device on exit, so a C-ABI call never leaves the caller's thread on the context's device (a process

@@ -337,6 +337,25 @@ def time_batch(batch, reps, warmup=3):
     return wall, kms
 
 
+def time_solve_call(vio, ctx, probs, reps):
+    """Wall time per vio_ba_solve_batched call on host problems (pack + one upload + solve + one download +
+    scatter into the caller's buffers), the ctypes structs built once as a C++ host holds its windows; and
+    per Python-level Context.ba_solve (which also marshals the structs and converts the results)."""
+    call = ctx.ba_solve_call(probs)
+    for _ in range(3):
+        call()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    c_call = (time.perf_counter() - t0) / reps
+    ctx.ba_solve(probs)
+    t0 = time.perf_counter()
+    for _ in range(max(reps // 5, 3)):
+        ctx.ba_solve(probs)
+    py_call = (time.perf_counter() - t0) / max(reps // 5, 3)
+    return c_call, py_call
+
+
 def config2_bench(vio, synth, ctx, lm_iters, cpu_seconds, want_cpu, windows=256):
     """Config 2 (BASELINE.json configs[1]): visual-only sliding-window BA, 10 KF x 200 landmarks, 2,000
     ERP observations, RunLocalBA semantics (Optimizer.cpp:726-966; first keyframe constant).  Single
@@ -349,11 +368,7 @@ def config2_bench(vio, synth, ctx, lm_iters, cpu_seconds, want_cpu, windows=256)
     wall1, kms1 = time_batch(one, 20)
     res = one.download()[0]
     one.close()
-    ctx.ba_solve(probs[:1])
-    t0 = time.perf_counter()
-    for _ in range(20):
-        ctx.ba_solve(probs[:1])
-    xfer = (time.perf_counter() - t0) / 20
+    xfer, _ = time_solve_call(vio, ctx, probs[:1], 50)
     many = vio.BaBatch(ctx, probs)
     wallm, kmsm = time_batch(many, 10)
     many.close()
@@ -832,11 +847,7 @@ def main():
         one.close()
         # the same window through vio_ba_solve: host problem in, host result out (upload + solve +
         # download per call, SURVEY §8d's single-window definition)
-        ctx.ba_solve(probs[:1])
-        t1 = time.perf_counter()
-        for _ in range(n1):
-            ctx.ba_solve(probs[:1])
-        single_xfer_wall = (time.perf_counter() - t1) / n1
+        single_xfer_wall, single_py_wall = time_solve_call(vio, ctx, probs[:1], n1)
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(vio, synth, args.lm_iters, args.cpu_seconds)
         gba = None if args.no_global else global_ba_bench(vio, synth, ctx, args.lm_iters,
                                                            not args.no_cpu_baseline and world == 1)
@@ -892,6 +903,8 @@ def main():
                 "config": "config 3 (one window per launch)",
                 "iters_per_s_wall": single_ips,
                 "iters_per_s_with_transfer": args.lm_iters / single_xfer_wall,
+                "ms_per_solve_call": single_xfer_wall * 1e3,
+                "iters_per_s_python_call": args.lm_iters / single_py_wall,
                 "kernel_ms": single_kms,
                 "route": single_route,
                 "workgroups": single_wg,
@@ -899,9 +912,11 @@ def main():
                 "vs_cpu_4t": (single_ips / cpu["single_window_threads"]["4"]) if cpu else None,
                 "vs_cpu_4t_with_transfer": (args.lm_iters / single_xfer_wall / cpu["single_window_threads"]["4"])
                 if cpu else None,
-                "note": "resident = BaBatch re-run on device-resident inputs; with_transfer = vio_ba_solve "
-                        "(pack + upload + solve + download) per call; CPU = the oracle on one window at 1 / 4 "
-                        "threads inside the solve",
+                "note": "resident = BaBatch re-run on device-resident inputs; with_transfer = one "
+                        "vio_ba_solve_batched C-ABI call per solve on host buffers (pack + one pinned upload + solve "
+                        "+ one pinned download + scatter; the call's structs built once, as a C++ host holds its "
+                        "windows); python_call = Context.ba_solve (ctypes marshalling and result dicts included); "
+                        "CPU = the oracle on one window at 1 / 4 threads inside the solve",
             },
             "sustained": sustained,
             "cpu_baseline": cpu,

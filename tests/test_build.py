@@ -9,7 +9,6 @@ import re
 import struct
 import subprocess
 
-import msgpack
 
 import pytest
 
@@ -84,6 +83,11 @@ def _gfx950_code_objects(blob):
         i += len(_BUNDLE)
 
 
+
+def _msgpack():
+    """msgpack (the code-object metadata format) -- only the code-object tests need it: skipped without it"""
+    return pytest.importorskip("msgpack")
+
 def _kernel_descriptors(co):
     """amdhsa.kernels entries of a code object's NT_AMDGPU_METADATA note (msgpack)"""
     shoff, = struct.unpack_from("<Q", co, 0x28)
@@ -103,7 +107,7 @@ def _kernel_descriptors(co):
             desc = co[p:p + dsz]
             p += (dsz + 3) & ~3
             if nt == 32 and name.startswith(b"AMDGPU"):
-                yield from msgpack.unpackb(desc, raw=False)["amdhsa.kernels"]
+                yield from _msgpack().unpackb(desc, raw=False)["amdhsa.kernels"]
 
 
 def test_cluster_kernel_has_no_scratch(vio):
