@@ -97,8 +97,9 @@ constexpr uint64_t gba_layout_sig() {
            (uint64_t)offsetof(GbaArgs, is_vi) << 16 | (uint64_t)offsetof(GbaArgs, Himu);
 }
 
-// the word a timed-out inter-workgroup wait of the Cholesky / triangular solves sets (cleared at the start
-// of every gba_launch_cholesky); nonzero after a step means a device fault, not a failed factorisation
+// the word a timed-out inter-workgroup wait of the Cholesky / triangular solves sets (cleared by
+// gba_reset_timeout before every factorisation, outside the captured graph); nonzero after a step means a
+// device fault, not a failed factorisation
 inline int* gba_timeout_word(const GbaArgs& A) { return A.flags ? A.flags + 32 * 2 * (size_t)(A.nfp / 64) : nullptr; }
 
 hipError_t gba_launch_setup(const GbaArgs& A, hipStream_t s);
@@ -108,6 +109,7 @@ hipError_t gba_launch_eval(const GbaArgs& A, const double* xp, const double* xl,
 hipError_t gba_launch_linearise(const GbaArgs& A, int first, double* partial, double* out_gmax, hipStream_t s);
 hipError_t gba_launch_step_prep(const GbaArgs& A, double radius, double* partial, double* out_bad, hipStream_t s);
 hipError_t gba_cholesky_attributes();
+hipError_t gba_reset_timeout(const GbaArgs& A, hipStream_t s);
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s);
 hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s);
 // workgroups of the persistent triangular solves gba_launch_solve enqueues (0: the per-step kernels), for

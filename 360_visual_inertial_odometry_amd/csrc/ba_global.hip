@@ -1355,19 +1355,19 @@ hipError_t gba_cholesky_attributes() {
     return e;
 }
 constexpr long long kGbaFuseTrail = 2500;  // trailing updates of at most this many tiles in the next step's launch
+hipError_t gba_reset_timeout(const GbaArgs& A, hipStream_t s) {
+    int* tmo = gba_timeout_word(A);
+    if (!tmo) return hipSuccess;
+    // (VIO_GBA_TEST_TIMEOUT=1: the word starts set, as after a timed-out wait -- the host's device-error
+    // path, exercised by tests/test_ba_gpu.py::test_wait_timeouts_report_device_errors)
+    static std::atomic<int> test_tmo{[] {
+        const char* v = std::getenv("VIO_GBA_TEST_TIMEOUT");
+        return v && v[0] == '1' ? 1 : 0;
+    }()};  // one-shot: the first factorisation of the process only
+    return hipMemsetAsync(tmo, test_tmo.exchange(0) ? 1 : 0, sizeof(int), s);
+}
 hipError_t gba_launch_cholesky(const GbaArgs& A, int* fail, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
-    int* tmo = A.flags ? A.flags + FLAG_STRIDE * 2 * (size_t)nblk : nullptr;  // timeout word of the Cholesky + solves
-    if (tmo) {
-        // (VIO_GBA_TEST_TIMEOUT=1: the word starts set, as after a timed-out wait -- the host's device-error
-        // path, exercised by tests/test_ba_gpu.py::test_wait_timeouts_report_device_errors)
-        static std::atomic<int> test_tmo{[] {
-            const char* v = std::getenv("VIO_GBA_TEST_TIMEOUT");
-            return v && v[0] == '1' ? 1 : 0;
-        }()};  // one-shot: the first factorisation of the process only
-        const hipError_t e0 = hipMemsetAsync(tmo, test_tmo.exchange(0) ? 1 : 0, sizeof(int), s);
-        if (e0 != hipSuccess) return e0;
-    }
     hipStream_t r = A.side;
     hipEvent_t ev_panel = A.ev[0], ev_rest = A.ev[1];
     if (!r || !ev_panel || !ev_rest) {  // no side stream: the plain schedule
@@ -1463,7 +1463,7 @@ hipError_t gba_launch_solve(const GbaArgs& A, hipStream_t s) {
     const int n = A.nfp, nblk = n / NB;
     if (gba_solve_persistent_wgs(A)) {  // every block resident: the persistent solves
         // y: the unset pattern (polled by the forward solve; x is reset by the forward kernel); the
-        // timeout word was cleared before the Cholesky (gba_launch_cholesky)
+        // timeout word was cleared before the Cholesky (gba_reset_timeout)
         hipError_t e = hipMemsetAsync(A.yv, 0xff, sizeof(double) * (size_t)n, s);
         if (e != hipSuccess) return e;
         const unsigned g = (unsigned)((nblk + TG - 1) / TG);

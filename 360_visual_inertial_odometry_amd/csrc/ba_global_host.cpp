@@ -24,40 +24,32 @@ uint64_t gba_layout_sig_ba_global_host() { return gba_layout_sig(); }
 
 namespace {
 
-struct DevBufs {
-    std::vector<void*> ptrs;
-    vio_ctx* ctx;
-    ~DevBufs() {
-        for (void* p : ptrs) (void)hipFree(p);
-    }
-    template <class T>
-    int alloc(T** p, size_t n) {
-        void* q = nullptr;
-        if (hipMalloc(&q, std::max<size_t>(n * sizeof(T), 64)) != hipSuccess) {
-            set_error(ctx, "hipMalloc failed (global BA)");
-            return VIO_ENOMEM;
-        }
-        ptrs.push_back(q);
-        *p = (T*)q;
-        return VIO_OK;
-    }
-    template <class T>
-    int upload(T** p, const std::vector<T>& v) {
-        int rc = alloc(p, v.size());
-        if (rc) return rc;
-        if (!v.empty() && hipMemcpy((void*)*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) {
-            set_error(ctx, "hipMemcpy failed (global BA)");
-            return VIO_EDEVICE;
-        }
-        return VIO_OK;
-    }
-};
-
 #define GBA_CHECK(expr)                                            \
     do {                                                           \
         hipError_t _e = (expr);                                    \
         if (_e != hipSuccess) return hip_fail(ctx, _e, #expr);     \
     } while (0)
+
+// the per-context state that outlives a global solve: the Cholesky's look-ahead stream and events, and the
+// captured Cholesky + triangular-solve graph with the device arguments it was captured with
+struct GbaCache {
+    hipStream_t side = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    hipGraphExec_t graph = nullptr;
+    unsigned char key[sizeof(GbaArgs)] = {};
+    int* key_fail = nullptr;
+    ~GbaCache() {
+        if (graph) (void)hipGraphExecDestroy(graph);
+        if (side) (void)hipStreamDestroy(side);
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
+GbaCache& gba_cache(vio_ctx* ctx) {
+    if (!ctx->gba_cache) ctx->gba_cache = std::make_shared<GbaCache>();
+    return *static_cast<GbaCache*>(ctx->gba_cache.get());
+}
 
 }  // namespace
 
@@ -81,23 +73,31 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             set_error(ctx, "observation index out of range");
             return VIO_EINVAL;
         }
+    // landmark CSR and the landmark-sorted order (a counting sort, stable: the caller's order within a
+    // landmark); one observation per (keyframe, landmark): a keyframe stamp per landmark, O(N + K)
+    std::vector<int> lm_ptr(L + 1, 0), perm(N);
+    for (int o = 0; o < N; ++o) lm_ptr[p.obs_lm[o] + 1]++;
+    for (int l = 0; l < L; ++l) lm_ptr[l + 1] += lm_ptr[l];
     {
-        std::vector<int64_t> key(N);
-        for (int o = 0; o < N; ++o) key[o] = (int64_t)p.obs_lm[o] * K + p.obs_kf[o];
-        std::sort(key.begin(), key.end());
-        for (int o = 1; o < N; ++o)
-            if (key[o] == key[o - 1]) { set_error(ctx, "duplicate (keyframe, landmark) observation"); return VIO_EINVAL; }
+        std::vector<int> fill(lm_ptr.begin(), lm_ptr.end() - 1);
+        for (int o = 0; o < N; ++o) perm[fill[p.obs_lm[o]]++] = o;
+        std::vector<int> stamp(K, -1);
+        for (int l = 0; l < L; ++l)
+            for (int q = lm_ptr[l]; q < lm_ptr[l + 1]; ++q) {
+                const int k = p.obs_kf[perm[q]];
+                if (stamp[k] == l) { set_error(ctx, "duplicate (keyframe, landmark) observation"); return VIO_EINVAL; }
+                stamp[k] = l;
+            }
     }
     DeviceScope _vio_dev_scope(ctx->device);
+    GBA_CHECK(_vio_dev_scope.err);
     hipStream_t st = ctx->stream;
     // ---- reduced problem (Ceres RemoveFixedBlocks; points are the e-blocks) ----
-    std::vector<uint8_t> pose_used(K, 0), lm_used(L, 0), active(N, 0);
+    std::vector<uint8_t> pose_used(K, 0), lm_used(L, 0);
     for (int o = 0; o < N; ++o) {
         int k = p.obs_kf[o], l = p.obs_lm[o];
-        bool kv = !p.kf_const[k], lv = !p.lm_const[l];
-        if (kv) pose_used[k] = 1;
-        if (lv) lm_used[l] = 1;
-        active[o] = kv || lv;
+        if (!p.kf_const[k]) pose_used[k] = 1;
+        if (!p.lm_const[l]) lm_used[l] = 1;
     }
     // VIBA: an IMU factor k (preint_valid[k]) brings velocities k-1, k, the biases and its two poses in
     // (RunVIBA: velocities and biases are never constant; Optimizer.cpp:493-636)
@@ -126,75 +126,193 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     const int nfp = std::max(64, (nf + 63) / 64 * 64);
     int n_free = nf;
     for (int l = 0; l < L; ++l) n_free += 3 * lm_used[l];
-    // landmark-sorted observations
-    std::vector<int> perm(N);
-    for (int o = 0; o < N; ++o) perm[o] = o;
-    std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return p.obs_lm[a] < p.obs_lm[b]; });
-    std::vector<int> lm_ptr(L + 1, 0), okf(N), olm(N), kf_ptr(K + 1, 0), kf_obs(N);
-    std::vector<float> ouv(2 * (size_t)N);
-    for (int o = 0; o < N; ++o) lm_ptr[p.obs_lm[o] + 1]++;
-    for (int l = 0; l < L; ++l) lm_ptr[l + 1] += lm_ptr[l];
-    for (int q = 0; q < N; ++q) {
-        int o = perm[q];
-        okf[q] = p.obs_kf[o]; olm[q] = p.obs_lm[o];
-        ouv[2 * q] = p.obs_uv[2 * o]; ouv[2 * q + 1] = p.obs_uv[2 * o + 1];
-        kf_ptr[okf[q] + 1]++;
-    }
-    for (int k = 0; k < K; ++k) kf_ptr[k + 1] += kf_ptr[k];
-    {
-        std::vector<int> fill(K, 0);
-        for (int q = 0; q < N; ++q) kf_obs[kf_ptr[okf[q]] + fill[okf[q]]++] = q;
-    }
-    // Schur contributions by destination block (pa >= pb), landmark order inside a destination
+    // Schur contributions by destination block (pa >= pb), landmark order inside a destination: counts
     const long long n_dest = (long long)P * (P + 1) / 2;
-    std::vector<int> dest_cnt(n_dest + 1, 0);
     auto dest_of = [](int a, int b) { return (long long)a * (a + 1) / 2 + b; };
+    // (pose block of every landmark-sorted observation, -1 for a constant pose: the pair loops below read it
+    // contiguously)
+    std::vector<int> blk(N);
+    for (int q = 0; q < N; ++q) {
+        const int f = pose_f[p.obs_kf[perm[q]]];
+        blk[q] = f < 0 ? -1 : f / 6;
+    }
+    std::vector<int> dest_cnt(n_dest + 1, 0);
     for (int l = 0; l < L; ++l) {
         if (!lm_used[l]) continue;
         for (int qa = lm_ptr[l]; qa < lm_ptr[l + 1]; ++qa) {
-            int fa = pose_f[okf[qa]];
-            if (fa < 0) continue;
+            const int a = blk[qa];
+            if (a < 0) continue;
+            int* row = &dest_cnt[dest_of(a, 0) + 1];
             for (int qb = lm_ptr[l]; qb < lm_ptr[l + 1]; ++qb) {
-                int fb = pose_f[okf[qb]];
-                if (fb < 0 || fb > fa) continue;
-                dest_cnt[dest_of(fa / 6, fb / 6) + 1]++;
+                const int b = blk[qb];
+                if (b >= 0 && b <= a) row[b]++;
             }
         }
     }
     for (long long d = 0; d < n_dest; ++d) dest_cnt[d + 1] += dest_cnt[d];
     const long long n_contrib = dest_cnt[n_dest];
     if (n_contrib > INT32_MAX) { set_error(ctx, "too many Schur contributions"); return VIO_ENOSYS; }
-    std::vector<int> ca(n_contrib), cb(n_contrib), dfill(dest_cnt.begin(), dest_cnt.end() - 1);
-    for (int l = 0; l < L; ++l) {
-        if (!lm_used[l]) continue;
-        for (int qa = lm_ptr[l]; qa < lm_ptr[l + 1]; ++qa) {
-            int fa = pose_f[okf[qa]];
-            if (fa < 0) continue;
-            for (int qb = lm_ptr[l]; qb < lm_ptr[l + 1]; ++qb) {
-                int fb = pose_f[okf[qb]];
-                if (fb < 0 || fb > fa) continue;
-                int pos = dfill[dest_of(fa / 6, fb / 6)]++;
-                ca[pos] = qa; cb[pos] = qb;
+
+    // ---- one device arena per context (grow-only): inputs | outputs | state and scratch ----
+    // The inputs are written straight into the context's pinned staging buffer and go up in ONE copy; the
+    // outputs (pose cache, landmarks, chi2 / outlier / bad flags, velocities, biases) are adjacent and come
+    // back in ONE copy.
+    const size_t Ns = std::max(N, 1), Ls = std::max(L, 1);
+    size_t off = 0;
+    auto take = [&off](size_t bytes) {
+        const size_t at = off;
+        off = (off + std::max<size_t>(bytes, 64) + 255) & ~(size_t)255;
+        return at;
+    };
+    struct { size_t pose_raw, pose_f, pob, lm_used, lm_marg, lm_ptr, okf, olm, ouv, kf_ptr, kf_obs, dest_a, dest_b,
+                    dptr, ca, cb, xl0, pre, pv, vel_f, v0, b0; } I{};
+    I.pose_raw = take(sizeof(double) * 24 * K);
+    I.pose_f = take(sizeof(int) * K);
+    I.pob = take(sizeof(int) * (size_t)P);
+    I.lm_used = take(L);
+    I.lm_marg = take(L);
+    I.lm_ptr = take(sizeof(int) * (size_t)(L + 1));
+    I.okf = take(sizeof(int) * Ns);
+    I.olm = take(sizeof(int) * Ns);
+    I.ouv = take(sizeof(float) * 2 * Ns);
+    I.kf_ptr = take(sizeof(int) * (size_t)(K + 1));
+    I.kf_obs = take(sizeof(int) * Ns);
+    I.dest_a = take(sizeof(int) * (size_t)n_dest);
+    I.dest_b = take(sizeof(int) * (size_t)n_dest);
+    I.dptr = take(sizeof(int) * (size_t)(n_dest + 1));
+    I.ca = take(sizeof(int) * (size_t)n_contrib);
+    I.cb = take(sizeof(int) * (size_t)n_contrib);
+    I.xl0 = take(sizeof(double) * 3 * Ls);
+    if (vi) {
+        I.pre = take(sizeof(vio_preint) * K);
+        I.pv = take(K);
+        I.vel_f = take(sizeof(int) * K);
+        I.v0 = take(sizeof(double) * 3 * K);
+        I.b0 = take(sizeof(double) * 6);
+    }
+    const size_t in_bytes = off;
+    struct { size_t pc, x_lm, chi2, outl, bad, x_vel, x_bias, end; } O{};
+    O.pc = take(sizeof(double) * 36 * K);
+    O.x_lm = take(sizeof(double) * 3 * Ls);
+    O.chi2 = take(sizeof(double) * Ns);
+    O.outl = take(Ns);
+    O.bad = take(Ls);
+    O.x_vel = take(sizeof(double) * 3 * K);
+    O.x_bias = take(sizeof(double) * 6);
+    O.end = off;
+    const size_t nblk_max = (std::max<size_t>({Ns, Ls, 6 * (size_t)K, (size_t)nfp}) + 255) / 256 + 8;
+    struct { size_t pinit, x_pose, c_pose, c_lm, r, jp, jl, V, gl, sl, Vi, yl, U, gf, colsq_f, sf, Df, bf, yv, xf, Wo,
+                    Yo, S, Linv, partial, scal, dfail, flags, c_vel, c_bias, sqi, imuJ, imur, imu_cost, Himu; } W{};
+    W.pinit = take(sizeof(double) * 24 * K);
+    W.x_pose = take(sizeof(double) * 6 * K);
+    W.c_pose = take(sizeof(double) * 6 * K);
+    W.c_lm = take(sizeof(double) * 3 * Ls);
+    W.r = take(sizeof(double) * 2 * Ns);
+    W.jp = take(sizeof(double) * 12 * Ns);
+    W.jl = take(sizeof(double) * 6 * Ns);
+    W.V = take(sizeof(double) * 6 * Ls);
+    W.gl = take(sizeof(double) * 3 * Ls);
+    W.sl = take(sizeof(double) * 3 * Ls);
+    W.Vi = take(sizeof(double) * 6 * Ls);
+    W.yl = take(sizeof(double) * 3 * Ls);
+    W.U = take(sizeof(double) * 27 * K);
+    W.gf = take(sizeof(double) * nfp);
+    W.colsq_f = take(sizeof(double) * nfp);
+    W.sf = take(sizeof(double) * nfp);
+    W.Df = take(sizeof(double) * nfp);
+    W.bf = take(sizeof(double) * nfp);
+    W.yv = take(sizeof(double) * nfp);
+    W.xf = take(sizeof(double) * nfp);
+    W.Wo = take(sizeof(double) * 18 * Ns);
+    W.Yo = take(sizeof(double) * 18 * Ns);
+    W.S = take(sizeof(double) * (size_t)nfp * nfp);
+    W.Linv = take(sizeof(double) * (size_t)nfp * 64);
+    W.partial = take(sizeof(double) * (3 * nblk_max + 3 * (size_t)K));
+    W.scal = take(sizeof(double) * 32);
+    W.dfail = take(sizeof(int) * 4);
+    W.flags = take(sizeof(int) * 32 * (3 * ((size_t)nfp / 64) + 1));
+    if (vi) {
+        W.c_vel = take(sizeof(double) * 3 * K);
+        W.c_bias = take(sizeof(double) * 6);
+        W.sqi = take(sizeof(double) * 81 * K);
+        W.imuJ = take(sizeof(double) * 108 * K);
+        W.imur = take(sizeof(double) * 9 * K);
+        W.imu_cost = take(sizeof(double) * K);
+        W.Himu = take(sizeof(double) * ((size_t)ni * ni + ni));
+    }
+    const size_t total = off;
+    auto* dev = static_cast<uint8_t*>(ctx_buffer(ctx, kSlotGbaSolve, total));
+    auto* hs = static_cast<uint8_t*>(ctx_host_buffer(ctx, kHostSlotGba, std::max(in_bytes, O.end - O.pc)));
+    if (!dev || !hs) {
+        set_error(ctx, "global BA: device arena or pinned staging allocation failed");
+        return VIO_ENOMEM;
+    }
+    // ---- the input image, written in place ----
+    {
+        auto* pose_raw = reinterpret_cast<double*>(hs + I.pose_raw);
+        for (int k = 0; k < K; ++k) {
+            std::memcpy(pose_raw + 24 * k, p.T_wb_init[k].R, 9 * sizeof(double));
+            std::memcpy(pose_raw + 24 * k + 9, p.T_wb_init[k].t, 3 * sizeof(double));
+            std::memcpy(pose_raw + 24 * k + 12, p.T_cb[k].R, 9 * sizeof(double));
+            std::memcpy(pose_raw + 24 * k + 21, p.T_cb[k].t, 3 * sizeof(double));
+        }
+        std::memcpy(hs + I.pose_f, pose_f.data(), sizeof(int) * K);
+        if (P) std::memcpy(hs + I.pob, pose_of_block.data(), sizeof(int) * P);
+        if (L) std::memcpy(hs + I.lm_used, lm_used.data(), L);
+        for (int l = 0; l < L; ++l) hs[I.lm_marg + l] = p.lm_marg ? (p.lm_marg[l] != 0) : 0;
+        std::memcpy(hs + I.lm_ptr, lm_ptr.data(), sizeof(int) * (L + 1));
+        auto* okf = reinterpret_cast<int*>(hs + I.okf);
+        auto* olm = reinterpret_cast<int*>(hs + I.olm);
+        auto* ouv = reinterpret_cast<float*>(hs + I.ouv);
+        auto* kf_ptr = reinterpret_cast<int*>(hs + I.kf_ptr);
+        std::fill(kf_ptr, kf_ptr + K + 1, 0);
+        for (int q = 0; q < N; ++q) {
+            const int o = perm[q];
+            okf[q] = p.obs_kf[o];
+            olm[q] = p.obs_lm[o];
+            ouv[2 * q] = p.obs_uv[2 * o];
+            ouv[2 * q + 1] = p.obs_uv[2 * o + 1];
+            kf_ptr[okf[q] + 1]++;
+        }
+        for (int k = 0; k < K; ++k) kf_ptr[k + 1] += kf_ptr[k];
+        auto* kf_obs = reinterpret_cast<int*>(hs + I.kf_obs);
+        std::vector<int> fill(kf_ptr, kf_ptr + K);
+        for (int q = 0; q < N; ++q) kf_obs[fill[okf[q]]++] = q;
+        auto* dest_a = reinterpret_cast<int*>(hs + I.dest_a);
+        auto* dest_b = reinterpret_cast<int*>(hs + I.dest_b);
+        for (int a = 0; a < P; ++a)
+            for (int b = 0; b <= a; ++b) { dest_a[dest_of(a, b)] = a; dest_b[dest_of(a, b)] = b; }
+        std::memcpy(hs + I.dptr, dest_cnt.data(), sizeof(int) * (size_t)(n_dest + 1));
+        auto* ca = reinterpret_cast<int*>(hs + I.ca);
+        auto* cb = reinterpret_cast<int*>(hs + I.cb);
+        std::vector<int> dfill(dest_cnt.begin(), dest_cnt.end() - 1);
+        for (int l = 0; l < L; ++l) {
+            if (!lm_used[l]) continue;
+            for (int qa = lm_ptr[l]; qa < lm_ptr[l + 1]; ++qa) {
+                const int a = blk[qa];
+                if (a < 0) continue;
+                int* row = &dfill[dest_of(a, 0)];
+                for (int qb = lm_ptr[l]; qb < lm_ptr[l + 1]; ++qb) {
+                    const int b = blk[qb];
+                    if (b < 0 || b > a) continue;
+                    const int pos = row[b]++;
+                    ca[pos] = qa; cb[pos] = qb;
+                }
             }
         }
+        if (L) std::memcpy(hs + I.xl0, p.lm_xyz, sizeof(double) * 3 * L);
+        if (vi) {
+            std::memcpy(hs + I.pre, p.preint, sizeof(vio_preint) * K);
+            std::memcpy(hs + I.pv, p.preint_valid, K);
+            std::memcpy(hs + I.vel_f, vel_f.data(), sizeof(int) * K);
+            std::memcpy(hs + I.v0, p.vel, sizeof(double) * 3 * K);
+            auto* b0 = reinterpret_cast<double*>(hs + I.b0);
+            for (int i = 0; i < 3; ++i) { b0[i] = p.bg[i]; b0[3 + i] = p.ba[i]; }
+        }
     }
-    std::vector<int> dest_a(n_dest), dest_b(n_dest);
-    for (int a = 0; a < P; ++a)
-        for (int b = 0; b <= a; ++b) { dest_a[dest_of(a, b)] = a; dest_b[dest_of(a, b)] = b; }
-    std::vector<double> pose_raw(24 * (size_t)K), xl0(3 * (size_t)L);
-    for (int k = 0; k < K; ++k) {
-        std::memcpy(&pose_raw[24 * k], p.T_wb_init[k].R, 9 * sizeof(double));
-        std::memcpy(&pose_raw[24 * k + 9], p.T_wb_init[k].t, 3 * sizeof(double));
-        std::memcpy(&pose_raw[24 * k + 12], p.T_cb[k].R, 9 * sizeof(double));
-        std::memcpy(&pose_raw[24 * k + 21], p.T_cb[k].t, 3 * sizeof(double));
-    }
-    std::memcpy(xl0.data(), p.lm_xyz, sizeof(double) * 3 * L);
-    std::vector<uint8_t> lm_marg(L, 0);
-    for (int l = 0; l < L; ++l) lm_marg[l] = p.lm_marg ? (p.lm_marg[l] != 0) : 0;
+    GBA_CHECK(hipMemcpyAsync(dev, hs, in_bytes, hipMemcpyHostToDevice, st));
 
     // ---- device state ----
-    DevBufs B;
-    B.ctx = ctx;
     GbaArgs A;
     std::memset(&A, 0, sizeof A);
     A.K = K; A.L = L; A.N = N; A.P = P; A.nf = nf; A.nfp = nfp;
@@ -207,70 +325,49 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
         double l00 = std::sqrt(p.info[0]), l10 = p.info[2] / l00, t = p.info[3] - l10 * l10;
         if (t > 0) { A.Lw[0] = l00; A.Lw[2] = l10; A.Lw[3] = std::sqrt(t); }
     }
-    int rc;
-    const double* c_pose_raw; const int *c_pose_f, *c_pob, *c_lm_ptr, *c_okf, *c_olm, *c_kf_ptr, *c_kf_obs;
-    const int *c_da, *c_db, *c_dp, *c_ca, *c_cb; const uint8_t *c_lv, *c_lmarg; const float* c_uv;
-    std::vector<int> dptr(dest_cnt.begin(), dest_cnt.end());
-    if ((rc = B.upload((double**)&c_pose_raw, pose_raw)) || (rc = B.upload((int**)&c_pose_f, pose_f)) ||
-        (rc = B.upload((int**)&c_pob, pose_of_block)) || (rc = B.upload((uint8_t**)&c_lv, lm_used)) ||
-        (rc = B.upload((uint8_t**)&c_lmarg, lm_marg)) || (rc = B.upload((int**)&c_lm_ptr, lm_ptr)) ||
-        (rc = B.upload((int**)&c_okf, okf)) || (rc = B.upload((int**)&c_olm, olm)) ||
-        (rc = B.upload((float**)&c_uv, ouv)) || (rc = B.upload((int**)&c_kf_ptr, kf_ptr)) ||
-        (rc = B.upload((int**)&c_kf_obs, kf_obs)) || (rc = B.upload((int**)&c_da, dest_a)) ||
-        (rc = B.upload((int**)&c_db, dest_b)) || (rc = B.upload((int**)&c_dp, dptr)) ||
-        (rc = B.upload((int**)&c_ca, ca)) || (rc = B.upload((int**)&c_cb, cb)))
-        return rc;
-    A.pose_raw = c_pose_raw; A.pose_f = c_pose_f; A.pose_of_block = c_pob; A.lm_var = c_lv; A.lm_marg = c_lmarg;
-    A.lm_ptr = c_lm_ptr; A.obs_kf = c_okf; A.obs_lm = c_olm; A.obs_uv = c_uv; A.kf_ptr = c_kf_ptr; A.kf_obs = c_kf_obs;
-    A.n_dest = n_dest; A.dest_a = c_da; A.dest_b = c_db; A.dest_ptr = c_dp; A.contrib_a = c_ca; A.contrib_b = c_cb;
-    const size_t Ns = std::max(N, 1), Ls = std::max(L, 1);
-    if ((rc = B.alloc(&A.pinit, 24 * (size_t)K)) || (rc = B.alloc(&A.pc, 36 * (size_t)K)) ||
-        (rc = B.alloc(&A.x_pose, 6 * (size_t)K)) || (rc = B.alloc(&A.x_lm, 3 * Ls)) ||
-        (rc = B.alloc(&A.c_pose, 6 * (size_t)K)) || (rc = B.alloc(&A.c_lm, 3 * Ls)) ||
-        (rc = B.alloc(&A.r, 2 * Ns)) || (rc = B.alloc(&A.jp, 12 * Ns)) || (rc = B.alloc(&A.jl, 6 * Ns)) ||
-        (rc = B.alloc(&A.V, 6 * Ls)) || (rc = B.alloc(&A.gl, 3 * Ls)) || (rc = B.alloc(&A.sl, 3 * Ls)) ||
-        (rc = B.alloc(&A.Vi, 6 * Ls)) || (rc = B.alloc(&A.yl, 3 * Ls)) || (rc = B.alloc(&A.U, 27 * (size_t)K)) ||
-        (rc = B.alloc(&A.gf, nfp)) || (rc = B.alloc(&A.colsq_f, nfp)) || (rc = B.alloc(&A.sf, nfp)) ||
-        (rc = B.alloc(&A.Df, nfp)) || (rc = B.alloc(&A.bf, nfp)) || (rc = B.alloc(&A.yv, nfp)) ||
-        (rc = B.alloc(&A.xf, nfp)) || (rc = B.alloc(&A.Wo, 18 * Ns)) || (rc = B.alloc(&A.Yo, 18 * Ns)) ||
-        (rc = B.alloc(&A.S, (size_t)nfp * nfp)) || (rc = B.alloc(&A.Linv, (size_t)nfp * 64)))
-        return rc;
-    const size_t nblk_max = (std::max<size_t>({Ns, Ls, 6 * (size_t)K, (size_t)nfp}) + 255) / 256 + 8;
-    double* partial;
-    double* scal;  // [0] cost [1] gmax [2] bad [3] nonfinite [4..6] model/step/xnorm [7] cand cost [8..10] post
-    int* dfail;
-    uint8_t *d_outl, *d_bad;
-    double* d_chi2;
+    auto at = [dev](size_t o) { return static_cast<void*>(dev + o); };
+    A.pose_raw = (const double*)at(I.pose_raw); A.pose_f = (const int*)at(I.pose_f);
+    A.pose_of_block = (const int*)at(I.pob); A.lm_var = (const uint8_t*)at(I.lm_used);
+    A.lm_marg = (const uint8_t*)at(I.lm_marg); A.lm_ptr = (const int*)at(I.lm_ptr);
+    A.obs_kf = (const int*)at(I.okf); A.obs_lm = (const int*)at(I.olm); A.obs_uv = (const float*)at(I.ouv);
+    A.kf_ptr = (const int*)at(I.kf_ptr); A.kf_obs = (const int*)at(I.kf_obs);
+    A.n_dest = n_dest; A.dest_a = (const int*)at(I.dest_a); A.dest_b = (const int*)at(I.dest_b);
+    A.dest_ptr = (const int*)at(I.dptr); A.contrib_a = (const int*)at(I.ca); A.contrib_b = (const int*)at(I.cb);
+    A.pc = (double*)at(O.pc); A.x_lm = (double*)at(O.x_lm);
+    A.pinit = (double*)at(W.pinit); A.x_pose = (double*)at(W.x_pose); A.c_pose = (double*)at(W.c_pose);
+    A.c_lm = (double*)at(W.c_lm); A.r = (double*)at(W.r); A.jp = (double*)at(W.jp); A.jl = (double*)at(W.jl);
+    A.V = (double*)at(W.V); A.gl = (double*)at(W.gl); A.sl = (double*)at(W.sl); A.Vi = (double*)at(W.Vi);
+    A.yl = (double*)at(W.yl); A.U = (double*)at(W.U); A.gf = (double*)at(W.gf); A.colsq_f = (double*)at(W.colsq_f);
+    A.sf = (double*)at(W.sf); A.Df = (double*)at(W.Df); A.bf = (double*)at(W.bf); A.yv = (double*)at(W.yv);
+    A.xf = (double*)at(W.xf); A.Wo = (double*)at(W.Wo); A.Yo = (double*)at(W.Yo); A.S = (double*)at(W.S);
+    A.Linv = (double*)at(W.Linv); A.flags = (int*)at(W.flags);
+    double* partial = (double*)at(W.partial);
+    double* scal = (double*)at(W.scal);  // [0] cost [1] gmax [2] bad [3] nonfinite [4..6] model/step/xnorm [7] cand cost [8..10] post
+    int* dfail = (int*)at(W.dfail);
+    double* d_chi2 = (double*)at(O.chi2);
+    uint8_t* d_outl = (uint8_t*)at(O.outl);
+    uint8_t* d_bad = (uint8_t*)at(O.bad);
+    const double* xl0 = (const double*)at(I.xl0);
     if (vi) {
-        const vio_preint* c_pre; const uint8_t* c_pv; const int* c_vf;
-        std::vector<vio_preint> pre(p.preint, p.preint + K);
-        std::vector<uint8_t> pv(p.preint_valid, p.preint_valid + K);
-        std::vector<double> v0(p.vel, p.vel + 3 * (size_t)K), b0(6);
-        for (int i = 0; i < 3; ++i) { b0[i] = p.bg[i]; b0[3 + i] = p.ba[i]; }
-        if ((rc = B.upload((vio_preint**)&c_pre, pre)) || (rc = B.upload((uint8_t**)&c_pv, pv)) ||
-            (rc = B.upload((int**)&c_vf, vel_f)) || (rc = B.upload(&A.x_vel, v0)) || (rc = B.upload(&A.x_bias, b0)) ||
-            (rc = B.alloc(&A.c_vel, 3 * (size_t)K)) || (rc = B.alloc(&A.c_bias, 6)) || (rc = B.alloc(&A.sqi, 81 * (size_t)K)) ||
-            (rc = B.alloc(&A.imuJ, 108 * (size_t)K)) || (rc = B.alloc(&A.imur, 9 * (size_t)K)) ||
-            (rc = B.alloc(&A.imu_cost, (size_t)K)) || (rc = B.alloc(&A.Himu, (size_t)ni * ni + ni)))
-            return rc;
-        A.preint = c_pre; A.preint_valid = c_pv; A.vel_f = c_vf;
+        A.preint = (const vio_preint*)at(I.pre); A.preint_valid = (const uint8_t*)at(I.pv); A.vel_f = (const int*)at(I.vel_f);
+        A.x_vel = (double*)at(O.x_vel); A.x_bias = (double*)at(O.x_bias);
+        A.c_vel = (double*)at(W.c_vel); A.c_bias = (double*)at(W.c_bias); A.sqi = (double*)at(W.sqi);
+        A.imuJ = (double*)at(W.imuJ); A.imur = (double*)at(W.imur); A.imu_cost = (double*)at(W.imu_cost);
+        A.Himu = (double*)at(W.Himu);
+        GBA_CHECK(hipMemcpyAsync(A.x_vel, at(I.v0), sizeof(double) * 3 * K, hipMemcpyDeviceToDevice, st));
+        GBA_CHECK(hipMemcpyAsync(A.x_bias, at(I.b0), sizeof(double) * 6, hipMemcpyDeviceToDevice, st));
     }
-    if ((rc = B.alloc(&partial, 3 * nblk_max + 3 * (size_t)K)) || (rc = B.alloc(&scal, 32)) ||
-        (rc = B.alloc(&dfail, 4)) || (rc = B.alloc(&A.flags, 32 * (3 * ((size_t)nfp / 64) + 1))) || (rc = B.alloc(&d_outl, Ns)) || (rc = B.alloc(&d_bad, Ls)) ||
-        (rc = B.alloc(&d_chi2, Ns)))
-        return rc;
-    // look-ahead stream + events of the Cholesky (released with the solve)
-    struct SideGuard {
-        GbaArgs* a;
-        ~SideGuard() {
-            if (a->side) (void)hipStreamDestroy(a->side);
-            for (hipEvent_t& e : a->ev)
-                if (e) (void)hipEventDestroy(e);
-        }
-    } side_guard{&A};
-    if (hipStreamCreateWithFlags(&A.side, hipStreamNonBlocking) != hipSuccess) A.side = nullptr;
-    for (hipEvent_t& e : A.ev)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    int rc;
+    // look-ahead stream, its events and the captured Cholesky + triangular-solve graph: kept per context and
+    // replayed while the solve's device arguments repeat (the arena makes them repeat for problems of the
+    // same shape: a call then captures nothing)
+    GbaCache& G = gba_cache(ctx);
+    if (!G.side && hipStreamCreateWithFlags(&G.side, hipStreamNonBlocking) != hipSuccess) G.side = nullptr;
+    for (hipEvent_t& e : G.ev)
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    A.side = G.side;
+    A.ev[0] = G.ev[0];
+    A.ev[1] = G.ev[1];
     GBA_CHECK(gba_cholesky_attributes());
     // the Cholesky + triangular solves of a step are the same launches every LM iteration: captured
     // once (fork / join of the look-ahead stream included) and replayed as one graph
@@ -278,12 +375,6 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
         const char* v = std::getenv("VIO_GBA_GRAPH");
         return !(v && v[0] == '0');
     }();
-    struct GraphGuard {
-        hipGraphExec_t g = nullptr;
-        ~GraphGuard() {
-            if (g) (void)hipGraphExecDestroy(g);
-        }
-    } chol_graph;
     auto factor_and_solve = [&]() -> hipError_t {
         if (!use_graph) {
             hipError_t e = gba_launch_cholesky(A, dfail, st);
@@ -293,7 +384,9 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             e = gba_launch_solve(A, st);
             return e == hipSuccess ? rg.commit() : e;
         }
-        if (!chol_graph.g) {
+        if (!G.graph || std::memcmp(G.key, &A, sizeof A) != 0 || G.key_fail != dfail) {
+            if (G.graph) (void)hipGraphExecDestroy(G.graph);
+            G.graph = nullptr;
             hipGraph_t g = nullptr;
             hipError_t e = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
             if (e != hipSuccess) return e;
@@ -301,18 +394,23 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             if (el == hipSuccess) el = gba_launch_solve(A, st);
             e = hipStreamEndCapture(st, &g);
             if (el != hipSuccess) e = el;
-            if (e == hipSuccess) e = hipGraphInstantiate(&chol_graph.g, g, nullptr, nullptr, 0);
+            if (e == hipSuccess) e = hipGraphInstantiate(&G.graph, g, nullptr, nullptr, 0);
             if (g) (void)hipGraphDestroy(g);
-            if (e != hipSuccess) return e;
+            if (e != hipSuccess) {
+                G.graph = nullptr;
+                return e;
+            }
+            std::memcpy(G.key, &A, sizeof A);
+            G.key_fail = dfail;
         }
         // the graph ends with the persistent triangular solves: reserved for the whole replay (residency.h)
         ResidencyGuard rg(st, gba_solve_persistent_wgs(A));
         hipError_t e = rg.status();
-        if (e == hipSuccess) e = hipGraphLaunch(chol_graph.g, st);
+        if (e == hipSuccess) e = hipGraphLaunch(G.graph, st);
         return e == hipSuccess ? rg.commit() : e;
     };
     GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));
-    GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0.data(), sizeof(double) * 3 * L, hipMemcpyHostToDevice, st));
+    GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0, sizeof(double) * 3 * L, hipMemcpyDeviceToDevice, st));
     GBA_CHECK(gba_launch_setup(A, st));
     if (vi) GBA_CHECK(gba_imu_launch_setup(A, st));
     // scal slots of the VIBA terms: [11] IMU cost at x, [12] IMU gradient max-norm, [13..15] IMU model change /
@@ -387,6 +485,7 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
             it.iteration = iteration;
             // ComputeTrustRegionStep + candidate cost, one batch of kernels, one readback
             GBA_CHECK(hipMemsetAsync(dfail, 0, sizeof(int), st));
+            GBA_CHECK(gba_reset_timeout(A, st));
             GBA_CHECK(gba_launch_step_prep(A, radius, partial, scal + 2, st));
             if (vi) GBA_CHECK(gba_imu_launch_system(A, st));
             GBA_CHECK(factor_and_solve());
@@ -460,40 +559,38 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
         }
         if (termination == VIO_TERM_FAILURE) {  // Ceres leaves the user's parameters untouched
             GBA_CHECK(hipMemsetAsync(A.x_pose, 0, sizeof(double) * 6 * K, st));
-            GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0.data(), sizeof(double) * 3 * L, hipMemcpyHostToDevice, st));
+            GBA_CHECK(hipMemcpyAsync(A.x_lm, xl0, sizeof(double) * 3 * L, hipMemcpyDeviceToDevice, st));
             if (vi) {
-                std::vector<double> b0(6);
-                for (int i = 0; i < 3; ++i) { b0[i] = p.bg[i]; b0[3 + i] = p.ba[i]; }
-                GBA_CHECK(hipMemcpy(A.x_vel, p.vel, sizeof(double) * 3 * K, hipMemcpyHostToDevice));
-                GBA_CHECK(hipMemcpy(A.x_bias, b0.data(), sizeof(double) * 6, hipMemcpyHostToDevice));
+                GBA_CHECK(hipMemcpyAsync(A.x_vel, at(I.v0), sizeof(double) * 3 * K, hipMemcpyDeviceToDevice, st));
+                GBA_CHECK(hipMemcpyAsync(A.x_bias, at(I.b0), sizeof(double) * 6, hipMemcpyDeviceToDevice, st));
             }
         }
     }
-    // ---- chi^2 / outliers / bad landmarks, outputs ----
+    // ---- chi^2 / outliers / bad landmarks, outputs (one copy of the outputs region) ----
     GBA_CHECK(gba_launch_post(A, d_chi2, d_outl, d_bad, partial, scal + 8, st));
-    if ((rc = read(h, 8, 3))) return rc;
-    std::vector<double> pc(36 * (size_t)K), xl(3 * Ls), chi2(Ns);
-    std::vector<uint8_t> outl(Ns), bad(Ls);
-    GBA_CHECK(hipMemcpy(pc.data(), A.pc, sizeof(double) * 36 * K, hipMemcpyDeviceToHost));
-    GBA_CHECK(hipMemcpy(xl.data(), A.x_lm, sizeof(double) * 3 * Ls, hipMemcpyDeviceToHost));
-    GBA_CHECK(hipMemcpy(chi2.data(), d_chi2, sizeof(double) * Ns, hipMemcpyDeviceToHost));
-    GBA_CHECK(hipMemcpy(outl.data(), d_outl, Ns, hipMemcpyDeviceToHost));
-    GBA_CHECK(hipMemcpy(bad.data(), d_bad, Ls, hipMemcpyDeviceToHost));
+    GBA_CHECK(hipMemcpyAsync(hs, dev + O.pc, O.end - O.pc, hipMemcpyDeviceToHost, st));
+    if ((rc = read(h, 8, 3))) return rc;  // (waits for the outputs copy too: same stream)
+    auto img = [&](size_t o) { return hs + (o - O.pc); };
+    const double* pc = reinterpret_cast<const double*>(img(O.pc));
+    const double* xl = reinterpret_cast<const double*>(img(O.x_lm));
+    const double* chi2 = reinterpret_cast<const double*>(img(O.chi2));
+    const uint8_t* outl = img(O.outl);
+    const uint8_t* bad = img(O.bad);
     if (out->T_wb)
         for (int k = 0; k < K; ++k) {
             std::memcpy(out->T_wb[k].R, &pc[36 * k], 9 * sizeof(double));
             std::memcpy(out->T_wb[k].t, &pc[36 * k + 9], 3 * sizeof(double));
         }
-    if (out->lm_xyz) std::memcpy(out->lm_xyz, xl.data(), sizeof(double) * 3 * L);
-    for (int q = 0; q < N; ++q) {
-        if (out->obs_chi2) out->obs_chi2[perm[q]] = chi2[q];
-        if (out->obs_outlier) out->obs_outlier[perm[q]] = outl[q];
-    }
-    if (out->lm_bad) std::memcpy(out->lm_bad, bad.data(), L);
+    if (out->lm_xyz && L) std::memcpy(out->lm_xyz, xl, sizeof(double) * 3 * L);
+    if (out->obs_chi2)
+        for (int q = 0; q < N; ++q) out->obs_chi2[perm[q]] = chi2[q];
+    if (out->obs_outlier)
+        for (int q = 0; q < N; ++q) out->obs_outlier[perm[q]] = outl[q];
+    if (out->lm_bad && L) std::memcpy(out->lm_bad, bad, L);
     if (vi) {
-        double xb[6];
-        if (out->vel) GBA_CHECK(hipMemcpy(out->vel, A.x_vel, sizeof(double) * 3 * K, hipMemcpyDeviceToHost));
-        GBA_CHECK(hipMemcpy(xb, A.x_bias, sizeof xb, hipMemcpyDeviceToHost));
+        const double* xv = reinterpret_cast<const double*>(img(O.x_vel));
+        const double* xb = reinterpret_cast<const double*>(img(O.x_bias));
+        if (out->vel) std::memcpy(out->vel, xv, sizeof(double) * 3 * K);
         if (out->bg) std::memcpy(out->bg, xb, 3 * sizeof(double));
         if (out->ba) std::memcpy(out->ba, xb + 3, 3 * sizeof(double));
     }

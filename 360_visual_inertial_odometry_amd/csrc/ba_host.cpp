@@ -786,6 +786,7 @@ void vio_ctx_destroy(vio_ctx* ctx) {
     if (!ctx) return;
     DeviceScope _vio_dev_scope(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    ctx->gba_cache.reset();  // its graph / side stream before the buffers and the stream
     for (void* p : ctx->bufs)
         if (p) (void)hipFree(p);
     for (void* p : ctx->hbufs)

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -28,6 +29,8 @@ struct vio_ctx {
     hipEvent_t init_ev[2] = {nullptr, nullptr};
     // window-BA execution route (vio_ctx_set_ba_route)
     int ba_route = VIO_BA_ROUTE_AUTO;
+    // global-BA state kept between solves (ba_global_host.cpp GbaCache: look-ahead stream, captured graph)
+    std::shared_ptr<void> gba_cache;
 };
 
 namespace vio360 {
@@ -54,8 +57,10 @@ enum { kSlotMonoInit = 17 };
 enum { kSlotLie = 18 };
 // the one-shot window solves' arena (vio_ba_solve[_batched]: inputs, outputs, workspace)
 enum { kSlotBaSolve = 19 };
+// the global BA solves' arena (inputs, outputs, the dense reduced system and the rest of the state)
+enum { kSlotGbaSolve = 20 };
 // pinned host slots: the one-shot solves' input image and every BA download's outputs image
-enum { kHostSlotBaIn = 0, kHostSlotBaOut = 1 };
+enum { kHostSlotBaIn = 0, kHostSlotBaOut = 1, kHostSlotGba = 2 };
 
 // Selects a device for the rest of the enclosing scope and restores the calling thread's current
 // device on exit, so a C-ABI call never leaves the caller's thread on the context's device (a process

@@ -542,6 +542,33 @@ def test_global_ba_fixed_iterations(vio, synth, gpu_ctx):
     assert_parity(o, g, p.c.chi2_threshold, iters_tol=0)
 
 
+def test_global_ba_arena_reuse_bitwise(vio, synth):
+    """The global path keeps its device arena, pinned staging buffer, look-ahead stream and the captured
+    Cholesky + triangular-solve graph in the context between solves (the graph is replayed while the solve's
+    device arguments repeat).  Solves of different shapes in a row -- visual, VI, a larger visual problem and
+    the first again -- each equal that problem solved alone on a fresh context, bit for bit."""
+    probs = [vio.BaProblem(synth.make_global(K=64, L=3000, k_per=8, seed=8), variant=vio.VIO_BA_FULL,
+                           max_iterations=6, fixed_iterations=1),
+             vio.BaProblem(synth.make_window(K=16, L=200, seed=56, imu=True, all_visible=False),
+                           variant=vio.VIO_BA_VI, max_iterations=6, fixed_iterations=1),
+             vio.BaProblem(synth.make_global(K=120, L=6000, k_per=10, seed=31), variant=vio.VIO_BA_FULL,
+                           max_iterations=6, fixed_iterations=1)]
+    ref = []
+    for p in probs:
+        c = vio.Context(0)
+        ref.append(c.ba_solve([p])[0])
+        c.close()
+    ctx = vio.Context(0)
+    try:
+        for i in (0, 1, 2, 0, 2):
+            g = ctx.ba_solve([probs[i]])[0]
+            for key in ("T_wb", "lm_xyz", "obs_chi2", "obs_outlier", "lm_bad", "vel", "bg", "ba"):
+                assert np.array_equal(g[key], ref[i][key]), (i, key)
+            assert g["final_cost"] == ref[i]["final_cost"] and g["iterations"] == ref[i]["iterations"]
+    finally:
+        ctx.close()
+
+
 def test_config5_full_size_properties(vio, synth, gpu_ctx):
     """Config 5 (1000 KF x 50k landmarks, dense 5994^2 reduced system) at full size: converges,
     improves on the ground truth, bitwise reproducible."""
