@@ -60,7 +60,7 @@ struct GbaArgs {
     double* Wo;               // [N][18]
     double* Yo;               // [N][18]
     double* S;                // [nfp][nfp]
-    double* Linv;             // [nfp/64][64][64]
+    double* Linv;             // [nfp/64 + 2][64][64]: the inverse diagonal blocks + the chained Cholesky's scratch
     hipStream_t side;         // look-ahead stream of the Cholesky (nullptr: plain schedule)
     hipEvent_t ev[2];
     int* flags;               // [32 (3 nfp/64 + 1)] triangular-solve flags, one per 128 B (+ timeout word), Cholesky step flags

@@ -796,8 +796,12 @@ __device__ __forceinline__ void flag_publish(int* f) {
 // bitwise the three-launch schedule.  Workgroups past m (trail > 0: `trail` of them) apply step k-1's
 // trailing update right of block column k+1 (part 3 of step k-1, its tiles in order): disjoint from
 // block columns k and k+1 and from S_dd, after panel k-1 (the previous launch) and before launch k+1,
-// so the look-ahead needs no second stream for it.  Dynamic LDS: CHOL_DIAG_LDS bytes.  fail: set by a
-// non-positive pivot; later launches then do nothing (the host rejects the step).
+// so the look-ahead needs no second stream for it.  Workgroup 1 (the owner of L_{k+2,k}) also forms column k's
+// product L_{k+2,k} L_{k+2,k}^T for the next launch's diagonal block into a scratch block (Linv past its nblk
+// inverses, two blocks by parity): the next workgroup 0 subtracts it where it formed it itself before, so its
+// chain holds three 64^3 products instead of four -- same operands, same code, same bits.  Dynamic LDS:
+// CHOL_DIAG_LDS bytes.  fail: set by a non-positive pivot; later launches then do nothing (the host rejects
+// the step).  Linv: nblk + 2 blocks.
 __global__ void __launch_bounds__(256) chol_chain_kernel(double* S, int n, int k, double* Linv, int* fail, int trail) {
     extern __shared__ double dyn[];
     double (*As)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(dyn);
@@ -816,10 +820,14 @@ __global__ void __launch_bounds__(256) chol_chain_kernel(double* S, int n, int k
     constexpr int PER = NB * NB / 256;
     // every global load of the workgroup first: the panel block, the diagonal block (workgroup 0),
     // column k-1's operand blocks, L_kk^-1
-    double cv[2][2][4], dv[2][2][4], va[PER], vb[PER], vl[PER];
+    double cv[2][2][4], dv[2][2][4], pv[2][2][4], va[PER], vb[PER], vl[PER];
     const int i = k + 1 + (int)blockIdx.x;
     double* C = S + (size_t)i * NB * n + (size_t)k * NB;
     double* D = S + (size_t)d * NB * n + (size_t)d * NB;
+    // column k-1's product for S_dd, L_{d,k-1} L_{d,k-1}^T: formed by workgroup 1 of the previous launch (the
+    // owner of L_{d,k-1}) into the scratch block of d's parity -- off this workgroup's chain
+    double* const P2 = Linv + (size_t)nblk * NB * NB;  // two 64x64 scratch blocks past the inverses
+    const double* P2d = P2 + (size_t)(d & 1) * NB * NB;
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -829,6 +837,7 @@ __global__ void __launch_bounds__(256) chol_chain_kernel(double* S, int n, int k
                 const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
                 cv[ti][tj][q] = k >= 0 ? C[(size_t)r * n + c] : 0.0;
                 dv[ti][tj][q] = lead && c <= r ? D[(size_t)r * n + c] : 0.0;
+                pv[ti][tj][q] = lead && k > 0 && c <= r ? P2d[r * NB + c] : 0.0;
             }
     if (k > 0) {
         const double* Aik = S + (size_t)i * NB * n + (size_t)(k - 1) * NB;
@@ -877,12 +886,16 @@ __global__ void __launch_bounds__(256) chol_chain_kernel(double* S, int n, int k
         __syncthreads();
         tile_product(acc);
         sub(cv, acc, false);
-        if (lead) {
-            __syncthreads();
-            to_lds(Bs, va);
-            __syncthreads();
-            tile_product(acc);
-            sub(dv, acc, true);
+        if (lead) {  // S_dd -= L_{d,k-1} L_{d,k-1}^T (the previous launch's product, same operands and code)
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                        if (c <= r) dv[ti][tj][q] = dv[ti][tj][q] - pv[ti][tj][q];
+                    }
         }
         __syncthreads();  // every wave is done with As / Bs
     }
@@ -908,6 +921,35 @@ __global__ void __launch_bounds__(256) chol_chain_kernel(double* S, int n, int k
                     const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
                     C[(size_t)r * n + c] = acc[ti][tj][q];
                 }
+        if (blockIdx.x == 1) {
+            // the next launch's column-k product for its diagonal block d + 1 = k + 2: L_{k+2,k} L_{k+2,k}^T from
+            // the panel block just formed, exactly as workgroup 0 would form it (the same LDS operands)
+            __syncthreads();
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                        As[r][c] = acc[ti][tj][q];
+                        Bs[r][c] = acc[ti][tj][q];
+                    }
+            __syncthreads();
+            d4 acc2[2][2];
+            tile_product(acc2);
+            double* P2n = P2 + (size_t)((k + 2) & 1) * NB * NB;
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int r = r0 + 16 * ti + (lane >> 4) + 4 * q, c = c0 + 16 * tj + (lane & 15);
+                        P2n[r * NB + c] = acc2[ti][tj][q];
+                    }
+            return;
+        }
         if (!lead) return;
         __syncthreads();
         // column k: S_dd -= L_dk L_dk^T with the panel block just formed (the stored values)

@@ -226,7 +226,7 @@ int global_ba_solve(vio_ctx* ctx, const vio_ba_problem& p, vio_ba_output* out) {
     W.Wo = take(sizeof(double) * 18 * Ns);
     W.Yo = take(sizeof(double) * 18 * Ns);
     W.S = take(sizeof(double) * (size_t)nfp * nfp);
-    W.Linv = take(sizeof(double) * (size_t)nfp * 64);
+    W.Linv = take(sizeof(double) * ((size_t)nfp + 2 * 64) * 64);  // + the chained Cholesky's two scratch blocks
     W.partial = take(sizeof(double) * (3 * nblk_max + 3 * (size_t)K));
     W.scal = take(sizeof(double) * 32);
     W.dfail = take(sizeof(int) * 4);
