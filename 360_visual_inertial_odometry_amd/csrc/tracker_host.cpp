@@ -222,9 +222,12 @@ int tracker_alloc(erp_tracker* t) {
     if ((rc = dalloc(t, &t->d_raw, sizeof(uint32_t) * ransac_raw_words()))) return rc;
     for (auto& e : t->ev)
         if (hipEventCreate(&e) != hipSuccess) return hip_fail(t->ctx, hipErrorUnknown, "hipEventCreate");
+    // pyr_done only orders GFTT pass 1 after the pyramids (contention, not data: pass 1 reads the uploaded level
+    // 0), so it needs no system-scope fence -- the fence costs the main stream ~3 us before LK
+    // (gpurun_out A/B, profiles/r6_notes.md); the join carries pass 1's results to the GFTT tail: default fences
     if (hipStreamCreateWithFlags(&t->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t->pyr_done, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&t->pyr_done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
         return hip_fail(t->ctx, hipErrorUnknown, "side stream / events");
     return VIO_OK;
 }
