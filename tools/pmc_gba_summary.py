@@ -36,10 +36,12 @@ def main(src, dst):
         per[k] = {"read_bytes": (a[0] - b[0]) / 2.0, "write_bytes": (a[1] - b[1]) / 2.0}
     total = sum(v["read_bytes"] + v["write_bytes"] for v in per.values())
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, 1- and 3-iteration "
-                     "config-5 solves (tools/gpu_pmc_gba.sh)",
+                     "config-5 solves (tools/gpu_prof.sh gba)",
            "correction": "reads = 2 x FETCH_SIZE (gfx950 half-count of wide coalesced reads), writes as reported",
            "hbm_bytes_per_iteration": total,
            "kernels_per_iteration": dict(sorted(per.items(), key=lambda kv: -(kv[1]["read_bytes"] + kv[1]["write_bytes"])))}
+    if os.environ.get("VIO_COMMIT"):  # the profiled build (tools/gpu_prof.sh); bench.py reports it with the traffic
+        doc["commit"] = os.environ["VIO_COMMIT"]
     with open(dst, "w") as f:
         json.dump(doc, f, indent=1)
     print(f"HBM bytes per LM iteration: {total / 1e9:.3f} GB")
