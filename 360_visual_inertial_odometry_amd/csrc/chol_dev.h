@@ -720,18 +720,20 @@ __device__ __forceinline__ bool chol_tile_solve2(double* A0, int n0, double* A1,
                 double* zrow = (lane < 12 && zr >= 0) ? P + zr * kTilePW : Ptrash;
 #pragma unroll
                 for (int p = 0; p < 3; ++p) *reinterpret_cast<cd2*>(zrow + 2 * p) = cd2{0.0, 0.0};
-                // L: the panel row, the diagonal block (lane u < 36: entry (u / 6, u % 6), zeros above), 1 / L[c][c]
+                // L: the panel row; the diagonal block's strictly lower entries and 1 / L[c][c] from lane 0 (every
+                // lane holds them: plain stores instead of per-lane select chains).  Nothing reads the block's
+                // diagonal or upper entries: the pivots go to inv, chol6_inv_upper writes L_JJ^-1 above the diagonal
                 double* arow = live ? A + rA * lda + c0 : trash;
 #pragma unroll
                 for (int c = 0; c < 6; ++c) arow[c] = ea[c];
-                double full[36];
+                if (lane == 0) {
 #pragma unroll
-                for (int i = 0; i < 6; ++i)
+                    for (int i = 1; i < 6; ++i)
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) full[6 * i + k] = k <= i ? l[i * (i + 1) / 2 + k] : 0.0;
-                const double lv = pick_d(full, lane);
-                *(lane < 36 ? A + (c0 + lane / 6) * lda + c0 + lane % 6 : trash + (lane & 7)) = lv;
-                *(lane < 6 ? inv + c0 + lane : trash + (lane & 7)) = pick_d(r, lane);
+                        for (int k = 0; k < i; ++k) A[(c0 + i) * lda + c0 + k] = l[i * (i + 1) / 2 + k];
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) inv[c0 + c] = r[c];
+                }
             }
             tmark(12);
             __syncthreads();  // panel J in P

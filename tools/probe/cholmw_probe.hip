@@ -404,7 +404,14 @@ int main() {
             for (int i = 0; i < (v == 7 ? 128 : 54); ++i)
                 if ((i < 54 || (i >= 64 && i < 100)) && memcmp(&x[i], &xall[v - 3][i], 8) != 0) same = 0;
         }
-        printf("V%d %-28s cycles/solve %7llu  resid %.2e %.2e%s\n", v, names[v], cyc, r0, r1,
+        unsigned long long h = 1469598103934665603ull;  // FNV-1a of the solution bytes (old / new builds compared)
+        for (int i = 0; i < 128; ++i)
+            if (i < 54 || (i >= 64 && i < 100)) {
+                unsigned char b[8];
+                memcpy(b, &x[i], 8);
+                for (int q = 0; q < 8; ++q) h = (h ^ b[q]) * 1099511628211ull;
+            }
+        printf("V%d %-28s cycles/solve %7llu  resid %.2e %.2e  x %016llx%s\n", v, names[v], cyc, r0, r1, h,
                same < 0 ? "" : same ? "  bitwise = tile_solve2" : "  DIFFERS from tile_solve2");
     }
     return 0;
