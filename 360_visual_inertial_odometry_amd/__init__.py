@@ -28,6 +28,7 @@ EXPORTS = [
     "erp_klt_track", "erp_gftt", "erp_rot_ransac", "erp_ransac_samples", "erp_tracker_create",
     "erp_tracker_upload", "erp_tracker_device_frame", "erp_tracker_swap", "erp_tracker_set_points",
     "erp_tracker_run", "erp_tracker_sync", "erp_tracker_download", "erp_tracker_stage_ms",
+    "erp_tracker_gftt_fallbacks",
     "erp_tracker_set_stage_timing",
     "erp_tracker_destroy", "erp_frontend_create", "erp_frontend_track", "erp_frontend_features",
     "erp_frontend_stats", "erp_frontend_destroy", "vio_imu_preintegrate", "vio_imu_preintegrate_kernel_ms", "vio_imu_preintegrate_device",
@@ -91,6 +92,8 @@ def lib():
     L.erp_tracker_sync.argtypes = [vp]
     L.erp_tracker_download.argtypes = [vp, vp, vp, vp, vp, C.POINTER(C.c_int)]
     L.erp_tracker_stage_ms.argtypes = [vp] + [C.POINTER(C.c_double)] * 5
+    if hasattr(L, "erp_tracker_gftt_fallbacks") or "VIO360_LIB" not in os.environ:  # (A/B: older builds)
+        L.erp_tracker_gftt_fallbacks.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.erp_tracker_set_stage_timing.argtypes = [vp, C.c_int]
     L.erp_tracker_destroy.argtypes = [vp]
     L.erp_frontend_create.argtypes = [vp, C.c_int, C.c_int, C.POINTER(abi.ErpFrontendParams), C.POINTER(C.c_void_p)]
@@ -564,6 +567,12 @@ class Tracker:
         v = [C.c_double() for _ in range(5)]
         self.ctx.check(lib().erp_tracker_stage_ms(self.h, *[C.byref(x) for x in v]), "erp_tracker_stage_ms")
         return dict(zip(["pyramids", "lk", "ransac", "gftt", "total"], [x.value for x in v]))
+
+    def gftt_fallbacks(self):
+        """(exact_tail, full_sort): downloads whose GFTT needed the masked-maximum tail / the full candidate sort"""
+        a, b = C.c_int(), C.c_int()
+        self.ctx.check(lib().erp_tracker_gftt_fallbacks(self.h, C.byref(a), C.byref(b)), "erp_tracker_gftt_fallbacks")
+        return a.value, b.value
 
     def close(self):
         if self.h:

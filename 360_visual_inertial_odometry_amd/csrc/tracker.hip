@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <hipcub/hipcub.hpp>
@@ -53,14 +54,25 @@ __device__ __forceinline__ int reflect101(int p, int n) {
     return p;
 }
 
-// ------------------------------------------------------------------------------------------
-// pyrDown.  Block = 64 x 8 outputs; LDS tile of the (2*8+4) REFLECT_101 source rows, columns
-// [2 ox - 16, 2 ox + 144), staged with one 16-B load per thread (the few reflected columns at the
-// left / right image edge are patched bytewise); each thread makes two adjacent outputs.
-constexpr int PD_BX = 64, PD_BY = 8;
-constexpr int PD_TW = 160, PD_TH = 2 * PD_BY + 4;
+__device__ __forceinline__ bool lm_static_in(const GfArgs& G, int x, int y) {
+    return y >= G.top_rows && y < G.bottom_start && x >= G.margin && x < G.W - G.margin;
+}
+__device__ __forceinline__ bool lm_disc(const GfArgs& G, int x, int y) {
+    return G.disc_bits && ((G.disc_bits[(size_t)y * G.disc_words + (x >> 5)] >> (x & 31)) & 1u);
+}
 
+// ------------------------------------------------------------------------------------------
+// pyrDown.  Block = 64 x BY outputs; LDS tile of the (2*BY+4) REFLECT_101 source rows, columns
+// [2 ox - 16, 2 ox + 144), staged with 16-B loads (all of a thread's loads issued before its LDS stores; the
+// few reflected columns at the left / right image edge are patched bytewise); each thread makes two adjacent
+// outputs in BY / 8 rows.  BY = 8 (BY = 32 for the large levels -- a quarter of the blocks and of the halo
+// rows, the 3840 x 1920 level-1 launch in one round of resident workgroups -- measured 15.0 against 13.2 us,
+// profiles/r6c_ab_pyr.log).
+constexpr int PD_BX = 64;
+constexpr int PD_TW = 160;
+template <int BY>
 __global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLevelPair dst) {
+    constexpr int PD_BY = BY, PD_TH = 2 * PD_BY + 4;
     __shared__ uint8_t tile[PD_TH][PD_TW];
     const int gxy = gridDim.x * gridDim.y;
     const int t = xcd_tile(blockIdx.x + gridDim.x * blockIdx.y + gxy * blockIdx.z, gxy * gridDim.z);
@@ -78,6 +90,7 @@ __global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLeve
         for (int it = 0; it < (NCH + 255) / 256; ++it) {
             const int e = threadIdx.x + 256 * it;
             const int x0 = cx0 + 16 * (e % (PD_TW / 16));
+            v[it] = make_uint4(0u, 0u, 0u, 0u);
             if (e < NCH && x0 >= 0 && x0 + 16 <= sp)
                 v[it] = *reinterpret_cast<const uint4*>(s + (size_t)reflect101(sy0 + e / (PD_TW / 16), sh) * sp + x0);
         }
@@ -97,28 +110,32 @@ __global__ void __launch_bounds__(256) pyr_down_kernel(PyrLevelPair src, PyrLeve
         }
     }
     __syncthreads();
-    const int q = threadIdx.x % (PD_BX / 2), ty = threadIdx.x / (PD_BX / 2);  // outputs 2q, 2q+1 of row ty
-    const int y = oy + ty;
-    if (y >= dh) return;
-    uint32_t packed = 0;
+    const int q = threadIdx.x % (PD_BX / 2);  // outputs 2q, 2q+1 of rows ty0 + 8 r
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int tx = 2 * q + j;
-        int tot = 0;
+    for (int rr = 0; rr < PD_BY / 8; ++rr) {
+        const int ty = threadIdx.x / (PD_BX / 2) + 8 * rr;
+        const int y = oy + ty;
+        if (y >= dh) break;
+        uint32_t packed = 0;
 #pragma unroll
-        for (int ky = 0; ky < 5; ++ky) {
-            const uint8_t* r = &tile[2 * ty + ky][2 * tx + 14];
-            const int rs = r[0] + 4 * r[1] + 6 * r[2] + 4 * r[3] + r[4];
-            tot += (ky == 0 || ky == 4 ? 1 : (ky == 2 ? 6 : 4)) * rs;
+        for (int j = 0; j < 2; ++j) {
+            const int tx = 2 * q + j;
+            int tot = 0;
+#pragma unroll
+            for (int ky = 0; ky < 5; ++ky) {
+                const uint8_t* r = &tile[2 * ty + ky][2 * tx + 14];
+                const int rs = r[0] + 4 * r[1] + 6 * r[2] + 4 * r[3] + r[4];
+                tot += (ky == 0 || ky == 4 ? 1 : (ky == 2 ? 6 : 4)) * rs;
+            }
+            packed |= (uint32_t)((tot + 128) >> 8) << (8 * j);
         }
-        packed |= (uint32_t)((tot + 128) >> 8) << (8 * j);
-    }
-    const int x = ox + 2 * q;
-    if (x + 1 < dw && ((dp & 1) == 0)) {
-        *reinterpret_cast<uint16_t*>(d + (size_t)y * dp + x) = (uint16_t)packed;
-    } else {
-        for (int j = 0; j < 2; ++j)
-            if (x + j < dw) d[(size_t)y * dp + x + j] = (uint8_t)(packed >> (8 * j));
+        const int x = ox + 2 * q;
+        if (x + 1 < dw && ((dp & 1) == 0)) {
+            *reinterpret_cast<uint16_t*>(d + (size_t)y * dp + x) = (uint16_t)packed;
+        } else {
+            for (int j = 0; j < 2; ++j)
+                if (x + j < dw) d[(size_t)y * dp + x + j] = (uint8_t)(packed >> (8 * j));
+        }
     }
 }
 
@@ -216,11 +233,14 @@ __device__ __forceinline__ void lk_region(uint8_t* Jr, int& rx0, int& ry0, const
 // the sequential values; the per-iteration update is computed by every thread from the same totals.
 template <int NT>
 __device__ void ransac_raw_body(uint32_t seed, uint32_t* raw, uint32_t* mt);  // (RANSAC section)
+__device__ float ransac_cos_bound(float thr);
+__device__ void pixel_to_bearing(float u, float v, int W, int H, float* b);
 constexpr int LK_AUX_BLOCKS = 17;  // LkAux: one workgroup for the raw draws, 16 for the reset and the bitmap clear
 __device__ void lk_aux(const LkAux& X, int b) {
     if (b == 0) {
         __shared__ uint32_t mt[624];
         if (X.raw) ransac_raw_body<LK_THREADS>(X.seed, X.raw, mt);
+        if (X.cmin && threadIdx.x == 0) *X.cmin = ransac_cos_bound(X.thresh);
         return;
     }
     const size_t t = (size_t)(b - 1) * LK_THREADS + threadIdx.x, stride = (size_t)(LK_AUX_BLOCKS - 1) * LK_THREADS;
@@ -233,6 +253,9 @@ __device__ void lk_aux(const LkAux& X, int b) {
         for (size_t i = t; i < (size_t)GF_BUCKETS; i += stride) X.hist[i] = 0u;
         for (size_t i = t; i < X.topk_cap; i += stride) X.topk[i] = 0ull;
     }
+    if (X.bear0)
+        for (size_t i = t; i < (size_t)X.n; i += stride)
+            pixel_to_bearing(X.pts[2 * i], X.pts[2 * i + 1], X.W, X.H, X.bear0 + 3 * i);
     if (X.disc) {
         const size_t n4 = X.disc_words / 4;
         uint4* d4p = reinterpret_cast<uint4*>(X.disc);
@@ -418,6 +441,8 @@ __global__ void __launch_bounds__(LK_THREADS) lk_kernel(LkArgs A, LkAux X) {
         A.status[pt] = (uint8_t)status;
         A.err[pt] = err;
     }
+    // the tracked point's bearing (RANSAC's input, FeatureTracker.cpp:262-271) by another wave, beside the stores
+    if (A.bear1 && tid == 64) pixel_to_bearing(nxt_x, nxt_y, A.lv[0].w, A.lv[0].h, A.bear1 + 3 * pt);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -471,8 +496,16 @@ __device__ int ransac_prep_body(const RansacArgs& R, int* wsum, int& base) {
         if (good) {
             int j = off + pre;
             R.gidx[j] = i;
-            pixel_to_bearing(R.p0[2 * i], R.p0[2 * i + 1], R.W, R.H, R.b0 + 3 * j);
-            pixel_to_bearing(R.p1[2 * i], R.p1[2 * i + 1], R.W, R.H, R.b1 + 3 * j);
+            if (R.bear0) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    R.b0[3 * j + c] = R.bear0[3 * i + c];
+                    R.b1[3 * j + c] = R.bear1[3 * i + c];
+                }
+            } else {
+                pixel_to_bearing(R.p0[2 * i], R.p0[2 * i + 1], R.W, R.H, R.b0 + 3 * j);
+                pixel_to_bearing(R.p1[2 * i], R.p1[2 * i + 1], R.W, R.H, R.b1 + 3 * j);
+            }
         }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -485,10 +518,35 @@ __device__ int ransac_prep_body(const RansacArgs& R, int* wsum, int& base) {
     if (threadIdx.x == 0) *R.n_good = base;
     return base;
 }
+// The inlier test (float)acos((double)c) < thr (FeatureTracker.cpp:365-375 + Camera::AngularDistance, Camera.cpp:89-98,
+// in the oracle's form) is
+// monotone non-increasing in the float cosine c, so it is c >= c_min for the smallest float c in [-1, 1] that
+// passes it: found once per run by bisection over the floats' order (31 evaluations of the same acos), every
+// hypothesis' inlier count is then a compare per point instead of a double acos.  (Adjacent floats near the
+// crossing differ in acos by ~1e-6, far above the double evaluation's error: the two tests agree bit for bit.)
+// +inf when no cosine passes (an empty inlier set: no c >= +inf; NaN compares false in both forms).
+__device__ float ransac_cos_bound(float thr) {
+    auto pass = [&](float c) { return (float)acos((double)c) < thr; };
+    auto ord = [](float x) {
+        const uint32_t b = __float_as_uint(x);
+        return (b >> 31) ? ~b : (b | 0x80000000u);
+    };
+    auto unord = [](uint32_t m) { return __uint_as_float((m >> 31) ? (m & 0x7fffffffu) : ~m); };
+    if (!pass(1.0f)) return INFINITY;
+    uint32_t lo = ord(-1.0f), hi = ord(1.0f);  // pass(unord(hi)) holds throughout
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (pass(unord(mid))) hi = mid;
+        else lo = mid + 1;
+    }
+    return unord(hi);
+}
+
 __global__ void __launch_bounds__(RP_THREADS) ransac_prep_kernel(RansacArgs R) {
     __shared__ int wsum[RP_THREADS / 64];
     __shared__ int base;
     ransac_prep_body<RP_THREADS>(R, wsum, base);
+    if (threadIdx.x == 0) *R.cmin = ransac_cos_bound(R.thresh);
 }
 
 // mt19937 + libstdc++-11 uniform_int_distribution (Lemire) — the reference's sampler
@@ -617,7 +675,13 @@ __global__ void __launch_bounds__(RS_SAMPLE_THREADS) ransac_sample_kernel(Ransac
     __shared__ uint8_t len3[RS_RAW];    // 1: a hypothesis starting at draw p consumes exactly 3 draws
     __shared__ int wsum[RS_SAMPLE_THREADS / 64];
     __shared__ int s_fallback, s_base;
+#ifdef TRK_STAMPS
+    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+#endif
     const int n = PREP ? ransac_prep_body<RS_SAMPLE_THREADS>(R, wsum, s_base) : *R.n_good;
+#ifdef TRK_STAMPS
+    const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+#endif
     if (PREP) __syncthreads();  // wsum is reused below
     if (n < 3 || R.iters <= 0) return;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -659,6 +723,9 @@ __global__ void __launch_bounds__(RS_SAMPLE_THREADS) ransac_sample_kernel(Ransac
     for (int p = tid; p < M; p += RS_SAMPLE_THREADS)
         len3[p] = (p + 2 < M && acc[p] != acc[p + 1] && acc[p] != acc[p + 2] && acc[p + 1] != acc[p + 2]) ? 1 : 0;
     __syncthreads();
+#ifdef TRK_STAMPS
+    const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
+#endif
     if (wid == 0) {
         int s = 0, h = 0;
         bool fb = false;
@@ -696,6 +763,11 @@ __global__ void __launch_bounds__(RS_SAMPLE_THREADS) ransac_sample_kernel(Ransac
         if (lane == 0) s_fallback = fb ? 1 : 0;
     }
     __syncthreads();
+#ifdef TRK_STAMPS
+    if (tid == 0)
+        printf("ransac_sample: prep %llu draws %llu chain %llu (n %d, M %d)\n", ts1 - ts0, ts2 - ts1,
+               __builtin_amdgcn_s_memtime() - ts2, n, M);
+#endif
     if (s_fallback && tid == 0) {
         __shared__ Mt19937 g;  // stream exhausted: the sequential sampler from the seed
         ransac_sample_seq(R, g, n);
@@ -770,13 +842,13 @@ __device__ __forceinline__ float det3f(const float* m) {
     return m[0] * (m[4] * m[8] - m[7] * m[5]) - m[3] * (m[1] * m[8] - m[7] * m[2]) + m[6] * (m[1] * m[5] - m[4] * m[2]);
 }
 
-__device__ __forceinline__ bool rot_inlier(const float* R, const float* a, const float* q, float thr) {
+__device__ __forceinline__ bool rot_inlier(const float* R, const float* a, const float* q, float cmin) {
     float r0 = (R[0] * a[0] + R[1] * a[1]) + R[2] * a[2];
     float r1 = (R[3] * a[0] + R[4] * a[1]) + R[5] * a[2];
     float r2 = (R[6] * a[0] + R[7] * a[1]) + R[8] * a[2];
     float c = (r0 * q[0] + r1 * q[1]) + r2 * q[2];
     c = c < -1.f ? -1.f : (c > 1.f ? 1.f : c);
-    return (float)acos((double)c) < thr;
+    return c >= cmin;  // (float)acos((double)c) < thr (ransac_cos_bound)
 }
 
 // one wavefront per hypothesis: count[it] = inliers, or -1 when |det R - 1| > 0.1 (skipped)
@@ -786,6 +858,9 @@ __global__ void __launch_bounds__(256) ransac_hyp_kernel(RansacArgs R) {
     if (it >= R.iters) return;
     const int n = *R.n_good;
     if (n < 3) return;
+#ifdef TRK_STAMPS
+    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+#endif
     float Hm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (int s = 0; s < 3; ++s) {
         int k = R.samples[3 * it + s];
@@ -795,7 +870,13 @@ __global__ void __launch_bounds__(256) ransac_hyp_kernel(RansacArgs R) {
             for (int c = 0; c < 3; ++c) Hm[3 * r + c] += q[r] * a[c];
     }
     float Rm[9];
+#ifdef TRK_STAMPS
+    const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+#endif
     kabsch_rotation(Hm, Rm);
+#ifdef TRK_STAMPS
+    const unsigned long long ts2 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
     for (int i = 0; i < 9; ++i)  // ransac_select reads the best one back
         if (lane == i) R.rot[9 * it + i] = Rm[i];
@@ -804,17 +885,19 @@ __global__ void __launch_bounds__(256) ransac_hyp_kernel(RansacArgs R) {
         return;
     }
     int cnt = 0;
-    for (int i = lane; i < n; i += 64) cnt += rot_inlier(Rm, R.b0 + 3 * i, R.b1 + 3 * i, R.thresh) ? 1 : 0;
+    const float cmin = *R.cmin;
+    for (int i = lane; i < n; i += 64) cnt += rot_inlier(Rm, R.b0 + 3 * i, R.b1 + 3 * i, cmin) ? 1 : 0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
     if (lane == 0) R.count[it] = cnt;
+#ifdef TRK_STAMPS
+    if (it == 0 && lane == 0)
+        printf("ransac_hyp: loads %llu kabsch %llu count %llu\n", ts1 - ts0, ts2 - ts1, __builtin_amdgcn_s_memtime() - ts2);
+#endif
 }
 
-// first strictly-best hypothesis -> mask over the good points, scattered to the input order
-__global__ void __launch_bounds__(256) ransac_select_kernel(RansacArgs R) {
-    __shared__ int sbest[256], sidx[256];
-    __shared__ float Rs[9];
-    const int n = *R.n_good;
+// first strictly-best hypothesis (256 threads; its rotation into Rs): returns its index, -1 when none
+__device__ int ransac_best(const RansacArgs& R, int n, int* sbest, int* sidx, float* Rs) {
     int best = 0, bi = -1;
     if (n >= 3)
         for (int it = threadIdx.x; it < R.iters; it += 256) {
@@ -835,14 +918,20 @@ __global__ void __launch_bounds__(256) ransac_select_kernel(RansacArgs R) {
         __syncthreads();
     }
     const int bit = sidx[0];
-    if (threadIdx.x == 0) {
-        *R.n_in = n < 3 ? n : sbest[0];
-    }
+    if (threadIdx.x == 0 && blockIdx.x == 0) *R.n_in = n < 3 ? n : sbest[0];
     if (bit >= 0 && threadIdx.x < 9) Rs[threadIdx.x] = R.rot[9 * bit + threadIdx.x];  // ransac_hyp's rotation
     __syncthreads();
+    return bit;
+}
+// -> mask over the good points, scattered to the input order
+__global__ void __launch_bounds__(256) ransac_select_kernel(RansacArgs R) {
+    __shared__ int sbest[256], sidx[256];
+    __shared__ float Rs[9];
+    const int n = *R.n_good;
+    const int bit = ransac_best(R, n, sbest, sidx, Rs);
     for (int j = threadIdx.x; j < n; j += 256) {
         uint8_t m = 1;
-        if (n >= 3 && bit >= 0) m = rot_inlier(Rs, R.b0 + 3 * j, R.b1 + 3 * j, R.thresh) ? 1 : 0;
+        if (n >= 3 && bit >= 0) m = rot_inlier(Rs, R.b0 + 3 * j, R.b1 + 3 * j, *R.cmin) ? 1 : 0;
         R.kept[R.gidx[j]] = m;
     }
 }
@@ -1110,6 +1199,13 @@ __global__ void __launch_bounds__(256) gftt_cand_kernel(GfArgs G) {
         if (base + i < G.cand_cap) G.cand[base + i] = keys[i];
 }
 
+// the response threshold of a masked maximum mo (ordered-int; 0: empty mask)
+__device__ __forceinline__ float lm_thr_of(const GfArgs& G, uint32_t mo) {
+    double maxv = mo ? (double)unord_f32(mo) : 0.0;  // minMaxLoc over the mask, 0 when empty
+    if (maxv < 0.0) maxv = 0.0;
+    return (float)(maxv * G.quality);
+}
+
 // greedy min-distance selection over the sorted candidates (goodFeaturesToTrack tail).
 // One workgroup.  Accepted corners live in a grid of cell = round(min_dist) with <= 3 per cell.
 constexpr int GS_THREADS = 256;
@@ -1118,6 +1214,17 @@ constexpr int GS_SLOTS = 3;
 // after the grid), so a survivor compares only with the survivors of its 3x3 cells (every pair within
 // min_dist lies there, as for the grid test) and the insertion walks only its own cell: the same
 // conflict masks and slots as the all-pairs walks, in O(cell occupancy) instead of O(batch).
+// G.presel (tracker pipeline, local-maximum path): `keys` is the presorted prefix of EVERY local maximum
+// of the static region (gftt_presort on the side stream, before the disc mask exists), so the pre-filter
+// also drops the keys inside a disc, and the threshold is bounded from above by thr_hi = quality x the
+// static region's maximum (the masked maximum is at most that): a key above thr_hi is a candidate whatever
+// the exact threshold, the first key at or below it ends the walk.  A walk that ends there (or runs out of
+// a prefix that does not hold every local maximum) before max_corners raises `incomplete` and the host runs
+// the exact tail (masked maximum, candidate top-K, this kernel); otherwise the corners are those of the
+// exact tail by construction (the same keys in the same order reach the greedy pass).  The prefix is staged
+// GS_STAGE keys at a time: their disc / threshold tests run in parallel (two memory round trips per stage
+// instead of per batch) and the batches are formed from the staged survivors only.
+constexpr int GS_STAGE = 4 * GS_THREADS;
 template <bool GLOBAL_GRID, bool HASH>
 __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const unsigned long long* keys,
                                                                   const unsigned int* n_keys, unsigned int cap,
@@ -1136,14 +1243,45 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
     __shared__ int s_slot_idx[GS_THREADS];
     __shared__ int s_acc;
     __shared__ int s_stop;
+    __shared__ int s_trunc;
+    __shared__ float s_thr;
+    __shared__ unsigned int s_st[GS_STAGE + GS_THREADS];  // presel: staged survivors (addresses, key order)
+    __shared__ int s_nst;                                  // presel: staged survivors
+    __shared__ unsigned int s_kpos;                        // presel: keys staged so far
     uint32_t* grid = GLOBAL_GRID ? G.grid_global : grid_lds;  // static address space (no flat access)
     const int ncell = G.gw * G.gh;
     int* head = reinterpret_cast<int*>(grid_lds + (GLOBAL_GRID ? 0 : ncell * GS_SLOTS));
     for (int e = threadIdx.x; e < ncell * GS_SLOTS; e += GS_THREADS) grid[e] = 0xffffffffu;
     if (HASH)
         for (int e = threadIdx.x; e < ncell; e += GS_THREADS) head[e] = -1;
-    if (threadIdx.x == 0) { s_acc = 0; s_stop = 0; }
+    const bool presel = G.presel != 0;
+    __shared__ int s_ok;
+    if (threadIdx.x == 0) {
+        s_acc = 0; s_stop = 0; s_trunc = 0; s_nst = 0; s_kpos = 0;
+        int ok = 1;
+        if (G.wait_ctr) {  // the presort's hand-off (the grid's initialisation above runs meanwhile)
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while ((int)(__hip_atomic_load(G.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - G.wait_target) < 0) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz: the exact tail decides
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s_ok = ok;
+        if (presel && ok) s_thr = lm_thr_of(G, *G.smax);  // thr_hi: the static region's maximum (the presort's)
+    }
     __syncthreads();
+    if (!s_ok) {
+        if (threadIdx.x == 0) {
+            *G.n_out = 0;
+            *G.incomplete = 1;
+        }
+        return;
+    }
     const unsigned int total = min(*n_keys, cap);
     const int cell = G.cell;
     const double md2 = G.min_dist * G.min_dist;
@@ -1168,13 +1306,79 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
 #ifdef GFTT_DEBUG
     unsigned long long t_start = __builtin_amdgcn_s_memtime(), t_pre = 0, t_mask = 0, t_greedy = 0, tq;
     int nb_dbg = 0, nsv_dbg = 0;
-    unsigned long long dbgv[4][4] = {};
+    unsigned long long dbgv[4][4] = {}, dbgs[4] = {};
 #endif
-    for (unsigned int c0 = 0; c0 < total; c0 += GS_THREADS) {
+    int sb = 0;  // presel: the batch's first staged survivor
+    for (unsigned int c0 = 0;; c0 += GS_THREADS) {
+        int nb = GS_THREADS;  // presel: survivors in this batch
+        if (!presel) {
+            if (c0 >= total) break;
+        } else {
+            if (s_nst - sb < GS_THREADS && !s_trunc && s_kpos < total) {
+                // stage the next GS_STAGE keys behind the survivors still staged: thread t tests keys
+                // s_kpos + 4t .. +3 (threshold bound, then the disc bit), one block scan places the survivors
+                const int rem = s_nst - sb;
+                const unsigned int mv = (int)threadIdx.x < rem ? s_st[sb + threadIdx.x] : 0u;
+                const unsigned int k0 = s_kpos + 4 * threadIdx.x;
+                unsigned long long kv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) kv[u] = k0 + u < total ? keys[k0 + u] : 0ull;
+                bool pass[4];
+                int cnt = 0;
+                bool tr = false;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const unsigned int idx = (unsigned int)(kv[u] & 0xffffffffu);
+                    const bool in = k0 + u < total;
+                    const bool above = __uint_as_float((unsigned int)(kv[u] >> 32)) > s_thr;
+                    tr |= in && !above;  // this key and every later one: undecided against the exact threshold
+                    pass[u] = in && above && !lm_disc(G, (int)(idx % G.W), (int)(idx / G.W));
+                    cnt += pass[u] ? 1 : 0;
+                }
+                const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+                int incl = cnt;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int v = __shfl_up(incl, off, 64);
+                    if (lane >= off) incl += v;
+                }
+                if (lane == 63) s_wcnt[wid] = incl;
+                __syncthreads();  // (every thread's read of s_st / s_nst / s_kpos above is done)
+                if ((int)threadIdx.x < rem) s_st[threadIdx.x] = mv;
+                int pos = rem + incl - cnt, tot = 0;
+#pragma unroll
+                for (int q = 0; q < GS_THREADS / 64; ++q) {
+                    pos += q < wid ? s_wcnt[q] : 0;
+                    tot += s_wcnt[q];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (pass[u]) s_st[pos++] = (unsigned int)(kv[u] & 0xffffffffu);
+                if (tr) s_trunc = 1;
+                __syncthreads();  // s_wcnt is reused by the batch
+                if (threadIdx.x == 0) {
+                    s_nst = rem + tot;
+                    s_kpos += GS_STAGE;
+                }
+                sb = 0;
+                __syncthreads();
+            }
+            nb = min(GS_THREADS, s_nst - sb);
+            if (nb <= 0) break;
+        }
         // (1) parallel pre-filter against the corners accepted in earlier batches
         unsigned int ci = c0 + threadIdx.x;
         int good = 0;
-        if (ci < total) {
+#ifdef GFTT_DEBUG
+        if (nb_dbg < 4) dbgs[nb_dbg] = __builtin_amdgcn_s_memtime() - t_start;  // (presel: staging so far)
+#endif
+        if (presel) {
+            if ((int)threadIdx.x < nb) {
+                const unsigned int idx = s_st[sb + threadIdx.x];
+                good = s_acc == 0 || !conflicts((int)(idx % G.W), (int)(idx / G.W), 0);  // (empty grid: no test)
+                s_idx[threadIdx.x] = idx;
+            }
+        } else if (ci < total) {
             unsigned int idx = (unsigned int)(keys[ci] & 0xffffffffu);
             good = !conflicts((int)(idx % G.W), (int)(idx / G.W), 0);
             s_idx[threadIdx.x] = idx;
@@ -1353,6 +1557,7 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
         }
         __syncthreads();
         if (s_stop) break;
+        sb += nb;
     }
 #ifdef GFTT_DEBUG
     if (threadIdx.x == 0)
@@ -1360,12 +1565,12 @@ __global__ void __launch_bounds__(GS_THREADS) gftt_select_kernel(GfArgs G, const
                t_pre, t_mask, t_greedy, __builtin_amdgcn_s_memtime() - t_start);
     if (threadIdx.x == 0)
         for (int q = 0; q < 2; ++q)
-            printf("gftt_select batch %d: pre %llu mask %llu rounds %llu insert %llu\n", q, dbgv[q][0], dbgv[q][1], dbgv[q][2], dbgv[q][3]);
+            printf("gftt_select batch %d: stage %llu pre %llu mask %llu rounds %llu insert %llu\n", q, dbgs[q], dbgv[q][0], dbgv[q][1], dbgv[q][2], dbgv[q][3]);
 #endif
     if (threadIdx.x == 0) {
         *G.n_out = s_acc;
         // the top-K subset ran dry before max_corners: the exact pass over every candidate must decide
-        if (fast) *G.incomplete = (!s_stop && G.cut[1] == 0) ? 1 : 0;
+        if (fast) *G.incomplete = (!s_stop && (s_trunc || G.cut[1] == 0)) ? 1 : 0;
     }
 }
 
@@ -1513,15 +1718,11 @@ hipError_t launch_gftt_reset(const GfArgs& g, int* scal, hipStream_t st) {
 
 // rasterise the discs of CreateFeatureMask (cv::circle filled, LINE_8; half-widths precomputed
 // on the host from OpenCV's midpoint Circle()) into a 1-bit-per-pixel exclusion mask
-__global__ void __launch_bounds__(128) disc_mask_kernel(DiscArgs D) {
-    const int k = blockIdx.x;
-    if (D.n_pts_dev && k >= *D.n_pts_dev) return;  // null: the grid is exactly the point count
-    if (D.kept && !D.kept[D.src_index ? D.src_index[k] : k]) return;
-    const int i = D.src_index ? D.src_index[k] : k;
+__device__ __forceinline__ void disc_raster(const DiscArgs& D, int i, int nthreads) {
     const float fx = D.pts[2 * i], fy = D.pts[2 * i + 1];
     const int cx = (int)rintf(fx), cy = (int)rintf(fy);  // Point2f -> Point (cvRound)
     const int r = D.radius;
-    for (int dy = -r + (int)threadIdx.x; dy <= r; dy += 128) {
+    for (int dy = -r + (int)threadIdx.x; dy <= r; dy += nthreads) {
         int y = cy + dy;
         if (y < 0 || y >= D.H) continue;
         int hwd = D.halfw[dy < 0 ? -dy : dy];
@@ -1535,6 +1736,35 @@ __global__ void __launch_bounds__(128) disc_mask_kernel(DiscArgs D) {
             x = (wi + 1) << 5;
         }
     }
+}
+__global__ void __launch_bounds__(128) disc_mask_kernel(DiscArgs D) {
+    const int k = blockIdx.x;
+    if (D.n_pts_dev && k >= *D.n_pts_dev) return;  // null: the grid is exactly the point count
+    if (D.kept && !D.kept[D.src_index ? D.src_index[k] : k]) return;
+    disc_raster(D, D.src_index ? D.src_index[k] : k, 128);
+}
+
+// tracker pipeline: RANSAC's selection and CreateFeatureMask's discs in one launch (one launch fewer on the
+// critical path).  Workgroup j (compacted point j < n_good; the grid covers every input point) finds the best
+// hypothesis itself -- the same reduction in every workgroup -- tests its point, scatters the kept flag and,
+// when kept, rasterises the point's disc (disc_mask_kernel's rows; D.radius <= 0: no discs)
+__global__ void __launch_bounds__(256) ransac_select_disc_kernel(RansacArgs R, DiscArgs D) {
+    __shared__ int sbest[256], sidx[256];
+    __shared__ float Rs[9];
+    __shared__ int s_m;
+    const int n = *R.n_good;
+    if ((int)blockIdx.x >= max(n, 1)) return;  // (workgroup 0 always runs: it writes n_in)
+    const int bit = ransac_best(R, n, sbest, sidx, Rs);
+    const int j = blockIdx.x;
+    if (j >= n) return;
+    if (threadIdx.x == 0) {
+        uint8_t m = 1;
+        if (n >= 3 && bit >= 0) m = rot_inlier(Rs, R.b0 + 3 * j, R.b1 + 3 * j, *R.cmin) ? 1 : 0;
+        R.kept[R.gidx[j]] = m;
+        s_m = m;
+    }
+    __syncthreads();
+    if (s_m && D.radius > 0) disc_raster(D, R.gidx[j], 256);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1558,12 +1788,6 @@ struct LmShared {
     float eig[EH][LM_EW];
 };
 
-__device__ __forceinline__ bool lm_static_in(const GfArgs& G, int x, int y) {
-    return y >= G.top_rows && y < G.bottom_start && x >= G.margin && x < G.W - G.margin;
-}
-__device__ __forceinline__ bool lm_disc(const GfArgs& G, int x, int y) {
-    return G.disc_bits && ((G.disc_bits[(size_t)y * G.disc_words + (x >> 5)] >> (x & 31)) & 1u);
-}
 
 // Tiles whose eig positions all lie at least one pixel inside the image (no reflected box positions):
 // the Sobel sums roll down a column (three source reads per cov position instead of nine: the
@@ -1722,6 +1946,8 @@ __global__ void __launch_bounds__(256) gftt_lmax_kernel(GfArgs G) {
     __shared__ uint32_t red[4];
     const int tile = xcd_tile(blockIdx.x, G.tiles_x * G.tiles_y);
     const int ox = (tile % G.tiles_x) * LM_TX, oy = (tile / G.tiles_x) * LM_TY;
+    if (G.clear && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < G.clear_n; i += 256) G.clear[i] = 0u;
     if (threadIdx.x == 0) s_cnt = 0;
     lm_eig_tile<LM_TY>(G, ox, oy, S);
     uint32_t m = 0, kmax = 0;
@@ -1827,12 +2053,7 @@ __global__ void __launch_bounds__(256) gftt_dirty_kernel(GfArgs G) {
     if (threadIdx.x == 0 && m) atomicMax(G.max_ord, m);
 }
 
-__device__ __forceinline__ float lm_threshold(const GfArgs& G) {
-    const uint32_t mo = *G.max_ord;
-    double maxv = mo ? (double)unord_f32(mo) : 0.0;  // minMaxLoc over the mask, 0 when empty
-    if (maxv < 0.0) maxv = 0.0;
-    return (float)(maxv * G.quality);
-}
+__device__ __forceinline__ float lm_threshold(const GfArgs& G) { return lm_thr_of(G, *G.max_ord); }
 __device__ __forceinline__ bool lm_survives(const GfArgs& G, unsigned long long k, float thr) {
     const float v = __uint_as_float((unsigned int)(k >> 32));
     const unsigned int a = (unsigned int)k;
@@ -1851,7 +2072,9 @@ __global__ void __launch_bounds__(256) gftt_lm_hist_kernel(GfArgs G) {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n_tiles = G.tiles_x * G.tiles_y;
     unsigned int cnt = 0;
+    uint32_t sm = 0;  // (the presort: the static region's maximum over the wave's tiles)
     for (int tile = blockIdx.x * 4 + wid; tile < n_tiles; tile += gridDim.x * 4) {
+        if (G.smax) sm = max(sm, G.tile_max[tile]);
         const unsigned int nk = G.lmax_n[tile];
         if (nk > LM_CAP && lane == 0) *G.lmax_over = 1;
         const unsigned long long* keys = G.lmax + (size_t)tile * LM_CAP;
@@ -1866,6 +2089,7 @@ __global__ void __launch_bounds__(256) gftt_lm_hist_kernel(GfArgs G) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += (unsigned int)__shfl_xor((int)cnt, off, 64);
     if (lane == 0 && cnt) atomicAdd(&s_n, cnt);
+    if (G.smax && lane == 0 && sm) atomicMax(G.smax, sm);
     __syncthreads();
     for (int b = threadIdx.x; b < GF_BUCKETS; b += 256)
         if (h[b]) atomicAdd(&G.hist[b], h[b]);
@@ -1960,8 +2184,9 @@ __global__ void __launch_bounds__(256) gftt_lm_flatten_kernel(GfArgs G) {
 // ------------------------------------------------------------------------------------------
 // launchers
 hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int frames, hipStream_t st) {
-    dim3 g((d.w + PD_BX - 1) / PD_BX, (d.h + PD_BY - 1) / PD_BY, frames);
-    hipLaunchKernelGGL(pyr_down_kernel, g, dim3(256), 0, st, s, d);
+    constexpr int by = 8;
+    dim3 g((d.w + PD_BX - 1) / PD_BX, (d.h + by - 1) / by, frames);
+    hipLaunchKernelGGL(pyr_down_kernel<by>, g, dim3(256), 0, st, s, d);
     return hipGetLastError();
 }
 hipError_t launch_lk(const LkArgs& a, hipStream_t st, const LkAux* aux) {
@@ -1987,6 +2212,12 @@ hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st) 
         hipLaunchKernelGGL(ransac_prep_kernel, dim3(1), dim3(RP_THREADS), 0, st, r);
     if (r.iters > 0) hipLaunchKernelGGL(ransac_hyp_kernel, dim3((r.iters + 3) / 4), dim3(256), 0, st, r);
     hipLaunchKernelGGL(ransac_select_kernel, dim3(1), dim3(256), 0, st, r);
+    return hipGetLastError();
+}
+hipError_t launch_ransac_pipeline(const RansacArgs& r, const DiscArgs& d, hipStream_t st) {
+    hipLaunchKernelGGL(ransac_sample_kernel<true>, dim3(1), dim3(RS_SAMPLE_THREADS), 0, st, r);
+    if (r.iters > 0) hipLaunchKernelGGL(ransac_hyp_kernel, dim3((r.iters + 3) / 4), dim3(256), 0, st, r);
+    hipLaunchKernelGGL(ransac_select_disc_kernel, dim3(r.n > 0 ? r.n : 1), dim3(256), 0, st, r, d);
     return hipGetLastError();
 }
 hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st) {
@@ -2031,13 +2262,29 @@ static hipError_t launch_select(const GfArgs& g, const unsigned long long* keys,
 // waves counts over one sixteenth of the list, staged through LDS in 512-key chunks (coalesced 8-key-per-
 // lane loads of the next chunk in flight while the current one is compared; ds_read_b128 broadcasts,
 // two comparands per read); the partial counts are summed in LDS and the key written to its position.
-constexpr int TS_WAVES = 16, TS_CHUNK = 512;
+// TS_WAVES = 16 for the masked tail's top-K (~5 k keys); the presort's prefix (~2-4 k keys) uses 4-wave
+// workgroups (its 256-workgroup grid of 16-wave ones took 13 us, most of it launching idle workgroups)
+constexpr int TS_CHUNK = 512;
+template <int TS_WAVES>
 __global__ void __launch_bounds__(64 * TS_WAVES) gftt_topk_sort_kernel(GfArgs G) {
     __shared__ unsigned int part[TS_WAVES][64];
     __shared__ __align__(16) unsigned long long buf[TS_WAVES][TS_CHUNK];
     const unsigned int n = min(*G.n_top, G.topk_cap);
     const unsigned int i0 = blockIdx.x * 64;
-    if (i0 >= n) return;
+    auto signal = [&]() {  // presort: this workgroup's stores are done (every storing wave drained, then one release)
+        if (!G.done) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(G.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    if (i0 >= n) {
+        signal();
+        return;
+    }
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
     const unsigned int i = i0 + lane;
     const unsigned long long k = i < n ? G.topk[i] : ~0ull;
@@ -2079,9 +2326,10 @@ __global__ void __launch_bounds__(64 * TS_WAVES) gftt_topk_sort_kernel(GfArgs G)
         for (int q = 0; q < TS_WAVES; ++q) r += part[q][lane];
         G.topk_sorted[r] = k;
     }
+    signal();
 }
 static hipError_t gftt_sort_topk(const GfArgs& g, void*, size_t, hipStream_t st) {
-    hipLaunchKernelGGL(gftt_topk_sort_kernel, dim3((g.topk_cap + 63) / 64), dim3(64 * TS_WAVES), 0, st, g);
+    hipLaunchKernelGGL(gftt_topk_sort_kernel<16>, dim3((g.topk_cap + 63) / 64), dim3(64 * 16), 0, st, g);
     return hipGetLastError();
 }
 // fast path: candidates -> histogram -> top-K compaction -> sort of the top-K keys -> greedy
@@ -2109,6 +2357,16 @@ hipError_t launch_gftt_after_lmax(const GfArgs& g, void* sort_tmp, size_t sort_t
     hipError_t e = gftt_sort_topk(g, sort_tmp, sort_tmp_bytes, st);
     if (e != hipSuccess) return e;
     return launch_select(g, (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1, st);
+}
+hipError_t launch_gftt_presort(const GfArgs& g, hipStream_t st) {
+    hipLaunchKernelGGL(gftt_lm_hist_kernel, dim3(256), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gftt_lm_topk_kernel, dim3(256), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gftt_topk_sort_kernel<4>, dim3((g.topk_cap + 63) / 64), dim3(64 * 4), 0, st, g);
+    return hipGetLastError();
+}
+hipError_t launch_gftt_presel(const GfArgs& g, const unsigned long long* keys, const unsigned int* n_keys,
+                              hipStream_t st) {
+    return launch_select(g, keys, n_keys, g.topk_cap, 1, st);
 }
 hipError_t launch_gftt_flatten(const GfArgs& g, hipStream_t st) {
     hipLaunchKernelGGL(gftt_lm_flatten_kernel, dim3(256), dim3(256), 0, st, g);

@@ -55,13 +55,15 @@ struct erp_tracker {
     uint8_t* lvl[2][TRK_MAX_LEVELS] = {};
     // points
     float *d_pts = nullptr, *d_next = nullptr, *d_err = nullptr, *d_b0 = nullptr, *d_b1 = nullptr;
+    float *d_bear0 = nullptr, *d_bear1 = nullptr;  // pipeline: bearings of every input / tracked point (LK launch)
     uint8_t *d_status = nullptr, *d_kept = nullptr;
     int *d_gidx = nullptr, *d_count = nullptr;
     float* d_rot = nullptr;
     int32_t* d_samples = nullptr;
     int iters_cap = 0;
     int n_pts = 0;
-    // scalars: [0] n_good [1] n_in [2] max_ord [3] n_cand [4] n_out [5] n_pts
+    // scalars: [0] n_good [1] n_in [2] max_ord [3] n_cand [4] n_out [6] n_top [7..8] cut [9] incomplete
+    // [10] lmax_over [11] n_flat
     int* d_scal = nullptr;
     // gftt
     unsigned long long *d_cand = nullptr, *d_cand_sorted = nullptr;
@@ -83,6 +85,15 @@ struct erp_tracker {
     unsigned long long *d_topk = nullptr, *d_topk_sorted = nullptr;
     unsigned int topk_cap = 0;
     GfArgs last_gf{};           // arguments of the last enqueued GFTT (exact fallback)
+    // presort of every local maximum (pipeline, side stream) and the greedy pass over it after the discs:
+    // histogram [GF_BUCKETS], then its scalars [0] n_top [1..2] cut [3] zero max_ord [4] n_cand [5] static-region
+    // maximum (cleared by gftt_lmax_kernel on the side stream)
+    unsigned int* d_hist2 = nullptr;
+    unsigned long long *d_topk2 = nullptr, *d_topk2_sorted = nullptr;
+    bool presel_used = false;   // the last pipeline GFTT ran the presel pass (its fallback: the exact tail)
+    bool presel_flag = false;   // ... and took the presort's result through the device counter (no stream join)
+    unsigned int presort_gen = 0;  // runs with a presort: the hand-off counter's target is gen x the sort's grid
+    int n_exact_tail = 0, n_full_sort = 0;  // fallbacks taken by read_corners (erp_tracker_gftt_fallbacks)
     // local-maximum path: per-tile local maxima, counts, static-region maxima, disc flags
     unsigned long long* d_lmax = nullptr;
     unsigned int* d_lmax_n = nullptr;
@@ -125,6 +136,7 @@ int dalloc(erp_tracker* t, T** p, size_t bytes) {
 }
 
 void tracker_free(erp_tracker* t) {
+    if (t->side) (void)hipStreamSynchronize(t->side);  // (the presel hand-off leaves the side stream unjoined)
     for (void* p : t->allocs) (void)hipFree(p);
     t->allocs.clear();
     for (auto& e : t->ev)
@@ -166,6 +178,10 @@ int ensure_gftt(erp_tracker* t, double min_dist) {
         if ((rc = dalloc(t, &t->d_hist, sizeof(unsigned int) * GF_BUCKETS)) != VIO_OK) return rc;
         if ((rc = dalloc(t, &t->d_topk, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
         if ((rc = dalloc(t, &t->d_topk_sorted, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_hist2, sizeof(unsigned int) * kPresortWords)) != VIO_OK) return rc;
+        VIO_HIP(t->ctx, hipMemset(t->d_hist2, 0, sizeof(unsigned int) * kPresortWords));  // the hand-off counter
+        if ((rc = dalloc(t, &t->d_topk2, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
+        if ((rc = dalloc(t, &t->d_topk2_sorted, sizeof(unsigned long long) * t->topk_cap)) != VIO_OK) return rc;
         t->tiles_x = (t->W + LM_TX - 1) / LM_TX;
         t->tiles_y = (t->H + LM_TY - 1) / LM_TY;
         const size_t nt = (size_t)t->tiles_x * t->tiles_y;
@@ -214,6 +230,8 @@ int tracker_alloc(erp_tracker* t) {
     if ((rc = dalloc(t, &t->d_gidx, sizeof(int) * P))) return rc;
     if ((rc = dalloc(t, &t->d_b0, sizeof(float) * 3 * P))) return rc;
     if ((rc = dalloc(t, &t->d_b1, sizeof(float) * 3 * P))) return rc;
+    if ((rc = dalloc(t, &t->d_bear0, sizeof(float) * 3 * P))) return rc;
+    if ((rc = dalloc(t, &t->d_bear1, sizeof(float) * 3 * P))) return rc;
     if ((rc = dalloc(t, &t->d_scal, sizeof(int) * 16))) return rc;
     if ((rc = dalloc(t, &t->d_corners, sizeof(float) * 2 * std::max(t->max_corners, 1)))) return rc;
     t->disc_words = (t->W + 31) / 32;
@@ -283,6 +301,7 @@ int enqueue_lk(erp_tracker* t, const erp_klt_params* p, int n, bool pyr_built = 
     double eps = std::min(std::max((double)p->epsilon, 0.0), 10.0);
     a.eps2 = eps * eps;
     a.min_eig = p->min_eig_threshold;
+    if (aux) a.bear1 = t->d_bear1;  // the pipeline's RANSAC input (its previous points' bearings: aux workgroups)
     if (t->ev[1] && (!aux || t->stage_timing)) (void)hipEventRecord(t->ev[1], t->ctx->stream);
     hipError_t e = launch_lk(a, t->ctx->stream, aux);
     if (e != hipSuccess) return hip_fail(t->ctx, e, "lk_kernel");
@@ -299,6 +318,7 @@ RansacArgs ransac_args(erp_tracker* t, int n, int mode, int iters, uint32_t seed
     r.gidx = t->d_gidx; r.n_good = t->d_scal + 0;
     r.b0 = t->d_b0; r.b1 = t->d_b1;
     r.samples = t->d_samples; r.iters = iters; r.seed = seed; r.thresh = thr;
+    r.cmin = reinterpret_cast<float*>(t->d_scal + 12);
     r.raw = t->d_raw;
     r.count = t->d_count; r.rot = t->d_rot; r.kept = t->d_kept; r.n_in = t->d_scal + 1;
     return r;
@@ -328,10 +348,33 @@ GfArgs gf_lmax_args(erp_tracker* t, const uint8_t* img, int pitch, int margin, f
     return g;
 }
 
+// the presort of every local maximum of pass 1 (side stream): no disc bitmap, a zero masked maximum (every
+// key passes the threshold test), the presort's own histogram / top-K / scalars
+GfArgs gf_presort_args(erp_tracker* t, const uint8_t* img, int pitch, int margin, float polar, int max_corners) {
+    GfArgs g = gf_lmax_args(t, img, pitch, margin, polar);
+    unsigned int* sc = t->d_hist2 + GF_BUCKETS;
+    g.max_ord = sc + 3;
+    g.n_cand = sc + 4;
+    g.hist = t->d_hist2;
+    g.topk = t->d_topk2;
+    g.topk_sorted = t->d_topk2_sorted;
+    g.n_top = sc;
+    g.cut = reinterpret_cast<int*>(sc + 1);
+    g.smax = sc + 5;
+    if (t->presel_flag) g.done = sc + 6;
+    g.topk_cap = t->topk_cap;
+    // the discs remove the strongest keys near the tracked points: 8 keys per corner (config 1: the greedy pass
+    // fills 300 corners from the first ~770 keys; the rank sort's cost grows with the square of the prefix)
+    g.topk_target = (unsigned int)std::min<size_t>(t->topk_cap, std::max<size_t>(2048, 8 * (size_t)max_corners));
+    return g;
+}
+
 // eig_ready: the map of `img` was already produced (launch_gftt_eig joined into the context stream)
+// presel: the pipeline's presort ran on the side stream (gf_presort_args): only the greedy pass over its
+// prefix is enqueued here; read_corners runs the exact tail if that pass cannot decide
 int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* mask, int mask_pitch, int max_corners,
                  double quality, double min_dist, bool discs, int margin, float polar, bool eig_ready = false,
-                 bool reset_done = false) {
+                 bool reset_done = false, bool presel = false) {
     int rc = ensure_gftt(t, min_dist);
     if (rc) return rc;
     GfArgs g;
@@ -367,10 +410,23 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
     g.topk_target = (unsigned int)std::min<size_t>(t->topk_cap, std::max<size_t>(4096, 16 * (size_t)max_corners));
     // scalars [2] max_ord [3] n_cand [4] n_out [6] n_top [7..8] cut [9] incomplete
     t->last_gf = g;
+    t->presel_used = presel && g.lmax;
     hipError_t e = reset_done ? hipSuccess : launch_gftt_reset(g, t->d_scal, t->ctx->stream);
     if (g.lmax) {
         if (e == hipSuccess && !eig_ready) e = launch_gftt_lmax(g, t->ctx->stream);
-        if (e == hipSuccess) e = launch_gftt_after_lmax(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+        if (e == hipSuccess && t->presel_used) {
+            GfArgs gs = g;
+            gs.presel = 1;
+            gs.cut = reinterpret_cast<int*>(t->d_hist2 + GF_BUCKETS + 1);  // the presort's cut: [1] nothing below it
+            gs.smax = t->d_hist2 + GF_BUCKETS + 5;                          // its static-region maximum
+            if (t->presel_flag) {  // the presort's device hand-off instead of the stream join
+                gs.wait_ctr = t->d_hist2 + GF_BUCKETS + 6;
+                gs.wait_target = t->presort_gen * ((t->topk_cap + 63) / 64);
+            }
+            e = launch_gftt_presel(gs, t->d_topk2_sorted, t->d_hist2 + GF_BUCKETS, t->ctx->stream);
+        } else if (e == hipSuccess) {
+            e = launch_gftt_after_lmax(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+        }
     } else {
         if (e == hipSuccess && !eig_ready) e = launch_gftt_eig(g, t->ctx->stream);
         if (e == hipSuccess) e = launch_gftt(g, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
@@ -392,7 +448,11 @@ int read_corners(erp_tracker* t, float* out_xy, int* n_out) {
     int sc[12];
     VIO_HIP(t->ctx, hipMemcpyAsync(sc, t->d_scal, sizeof(sc), hipMemcpyDeviceToHost, t->ctx->stream));
     VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    // the side stream's pass 1 / presort (the presel hand-off does not join it): the fallbacks below read them
+    VIO_HIP(t->ctx, hipStreamSynchronize(t->side));
+    bool map_path = false;
     if (t->last_gf.lmax && sc[10]) {  // a tile held more local maxima than its slots: the map path
+        map_path = true;
         GfArgs g = t->last_gf;
         g.lmax = nullptr;
         hipError_t e = launch_gftt_reset(g, t->d_scal, t->ctx->stream);
@@ -403,12 +463,23 @@ int read_corners(erp_tracker* t, float* out_xy, int* n_out) {
         VIO_HIP(t->ctx, hipMemcpyAsync(sc, t->d_scal, sizeof(sc), hipMemcpyDeviceToHost, t->ctx->stream));
         VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
     }
+    if (!map_path && t->presel_used && sc[9]) {
+        // the presorted prefix did not decide (threshold bound reached or prefix exhausted before max_corners):
+        // the exact tail -- masked maximum, candidate top-K, greedy pass (its buffers are untouched by presel)
+        hipError_t e = launch_gftt_after_lmax(t->last_gf, t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt exact tail");
+        ++t->n_exact_tail;
+        VIO_HIP(t->ctx, hipMemcpyAsync(sc, t->d_scal, sizeof(sc), hipMemcpyDeviceToHost, t->ctx->stream));
+        VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    }
+    t->presel_used = false;
     if ((unsigned int)sc[3] > t->cand_cap) {  // NMS survivors beyond the candidate buffer: the corner set
         set_error(t->ctx, "GFTT candidate buffer overflow");  // would differ from goodFeaturesToTrack
         return VIO_ENOSYS;
     }
     inc = sc[9];
     if (inc) {  // the top-K subset did not decide: exact pass over every candidate
+        ++t->n_full_sort;
         hipError_t e = t->last_gf.lmax ? launch_gftt_flatten(t->last_gf, t->ctx->stream) : hipSuccess;
         if (e == hipSuccess)
             e = launch_gftt_full(t->last_gf, (unsigned int)sc[3], t->d_sort_tmp, t->sort_tmp_bytes, t->ctx->stream);
@@ -454,6 +525,13 @@ int erp_tracker_create(vio_ctx* ctx, int W, int H, int max_points, int max_corne
     int rc = tracker_alloc(t);
     if (rc) { tracker_free(t); delete t; return rc; }
     *out = t;
+    return VIO_OK;
+}
+
+int erp_tracker_gftt_fallbacks(erp_tracker* t, int* exact_tail, int* full_sort) {
+    if (!t || !exact_tail || !full_sort) return VIO_EINVAL;
+    *exact_tail = t->n_exact_tail;
+    *full_sort = t->n_full_sort;
     return VIO_OK;
 }
 
@@ -510,9 +588,53 @@ int erp_tracker_set_points(erp_tracker* t, const float* pts, int n) {
 }
 
 // the enqueue sequence of one pipeline run (directly, or into the stream capture of erp_tracker_run)
-static int enqueue_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p, int n, int radius) {
+static int enqueue_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker_params* p, int n, int radius,
+                       bool capture) {
     int rc;
     hipStream_t st = t->ctx->stream;
+    // GFTT's candidate order is known before the disc mask: the side stream presorts every local maximum after
+    // pass 1 and the tail after the join is one greedy pass (VIO_TRK_PRESEL=0: the masked-maximum tail)
+    static const bool presel_env = [] {
+        const char* v = std::getenv("VIO_TRK_PRESEL");
+        return !(v && v[0] == '0');
+    }();
+    const bool presel = presel_env;
+    // the presort reaches the greedy pass through a device counter (VIO_TRK_PRESEL_FLAG=0: through the stream
+    // join, ~6-14 us of event latency on the critical path); a captured graph keeps the join (the counter's
+    // target is per run)
+    static const bool flag_env = [] {
+        const char* v = std::getenv("VIO_TRK_PRESEL_FLAG");
+        return !(v && v[0] == '0');
+    }();
+    t->presel_flag = presel && flag_env && !capture;
+    if (t->presel_flag) ++t->presort_gen;
+    // The side stream (pass 1 + presort) is the longer path once the tail is one greedy pass, and the host's
+    // enqueue order decides when the GPU first sees it (each launch costs the host a few microseconds, which the
+    // GPU outruns).  VIO_TRK_SIDE: 0 (default) -- side work enqueued after LK (pass 1 dispatched ~14 us after
+    // the pyramids); 1 -- enqueued right after the pyramids, before LK (pass 1 then delays LK: the same total,
+    // profiles/r6c_ab_side.log); 2 -- enqueued first, pass 1 beside the pyramids (3-5 % slower)
+    static const int side_env = [] {
+        const char* v = std::getenv("VIO_TRK_SIDE");
+        return v ? std::atoi(v) : 0;
+    }();
+    auto enqueue_side = [&]() -> int {
+        VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->pyr_done, 0));
+        GfArgs gl = gf_lmax_args(t, t->lvl[1][0], t->lp[0], p->boundary_margin, p->polar_ratio);
+        if (presel) {  // pass 1 clears the presort's histogram and scalars (ordered before the presort, and after
+                       // the previous run's greedy pass through the pyramid event)
+            gl.clear = t->d_hist2;
+            gl.clear_n = kPresortClear;
+        }
+        hipError_t e = launch_gftt_lmax(gl, t->side);
+        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_lmax_kernel");
+        if (presel) {
+            e = launch_gftt_presort(
+                gf_presort_args(t, t->lvl[1][0], t->lp[0], p->boundary_margin, p->polar_ratio, p->max_corners), t->side);
+            if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt presort");
+        }
+        VIO_HIP(t->ctx, hipEventRecord(t->join, t->side));
+        return VIO_OK;
+    };
     // main stream: pyramids, then LK, whose launch also carries the RANSAC draws' raw stream (seed only),
     // the GFTT counters / histogram / top-K reset and the disc bitmap clear in extra workgroups (on the
     // side stream they cost the main stream a cross-stream wait before RANSAC); side stream: GFTT pass 1
@@ -523,44 +645,49 @@ static int enqueue_run(erp_tracker* t, const erp_klt_params* klt, const erp_trac
         std::memset(&x, 0, sizeof x);
         x.raw = t->d_raw;
         x.seed = p->ransac_seed;
+        x.thresh = p->ransac_thresh_rad;
+        x.cmin = reinterpret_cast<float*>(t->d_scal + 12);
         x.hist = t->d_hist;
         x.topk = t->d_topk;
         x.topk_cap = t->topk_cap;
         x.scal = t->d_scal;
         x.disc = t->d_disc;
         x.disc_words = (size_t)t->disc_words * t->H;
+        x.pts = t->d_pts;
+        x.bear0 = t->d_bear0;
+        x.n = n;
+        x.W = t->W;
+        x.H = t->H;
         int top = lk_top_level(t, klt->win, klt->max_level);
+        if (side_env == 2) {
+            VIO_HIP(t->ctx, hipEventRecord(t->pyr_done, st));
+            if ((rc = enqueue_side())) return rc;
+        }
         if ((rc = build_pyramids(t, top))) return rc;
-        VIO_HIP(t->ctx, hipEventRecord(t->pyr_done, st));
+        if (side_env != 2) VIO_HIP(t->ctx, hipEventRecord(t->pyr_done, st));
+        if (side_env == 1 && (rc = enqueue_side())) return rc;
         if ((rc = enqueue_lk(t, klt, n, true, &x))) return rc;
     }
-    {
-        VIO_HIP(t->ctx, hipStreamWaitEvent(t->side, t->pyr_done, 0));
-        hipError_t e =
-            launch_gftt_lmax(gf_lmax_args(t, t->lvl[1][0], t->lp[0], p->boundary_margin, p->polar_ratio), t->side);
-        if (e != hipSuccess) return hip_fail(t->ctx, e, "gftt_lmax_kernel");
-    }
-    VIO_HIP(t->ctx, hipEventRecord(t->join, t->side));
+    if (side_env == 0 && (rc = enqueue_side())) return rc;
     if (t->stage_timing) VIO_HIP(t->ctx, hipEventRecord(t->ev[2], st));
     RansacArgs r = ransac_args(t, n, 1, p->ransac_iters, p->ransac_seed, p->ransac_thresh_rad, p->polar_ratio,
                                p->boundary_margin, t->d_pts, t->d_next);
+    r.bear0 = t->d_bear0;  // formed by the LK launch
+    r.bear1 = t->d_bear1;
     if (n > 0) {
-        hipError_t e = launch_ransac(r, true, st);
+        // RANSAC, then its selection and CreateFeatureMask's discs of radius (int)min_dist around every kept
+        // point in one launch (bitmap cleared in the LK launch; radius 0: no discs)
+        DiscArgs d{t->d_next, t->d_kept, nullptr, nullptr, t->d_disc, t->disc_words, t->W, t->H, radius,
+                   t->d_halfw};
+        hipError_t e = launch_ransac_pipeline(r, d, st);
         if (e != hipSuccess) return hip_fail(t->ctx, e, "ransac kernels");
     } else {
         VIO_HIP(t->ctx, hipMemsetAsync(t->d_scal, 0, 2 * sizeof(int), st));
     }
     if (t->stage_timing) VIO_HIP(t->ctx, hipEventRecord(t->ev[3], st));
-    // CreateFeatureMask: discs of radius (int)min_dist around every kept point (bitmap cleared in the LK launch)
-    if (n > 0 && radius > 0) {
-        DiscArgs d{t->d_next, t->d_kept, nullptr, nullptr, t->d_disc, t->disc_words, t->W, t->H, radius,
-                   t->d_halfw};
-        hipError_t e = launch_disc_mask(d, n, st);
-        if (e != hipSuccess) return hip_fail(t->ctx, e, "disc_mask_kernel");
-    }
-    VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->join, 0));
+    if (!t->presel_flag) VIO_HIP(t->ctx, hipStreamWaitEvent(st, t->join, 0));
     if ((rc = enqueue_gftt(t, t->lvl[1][0], t->lp[0], nullptr, 0, p->max_corners, p->quality, p->min_dist, true,
-                           p->boundary_margin, p->polar_ratio, true, true)))
+                           p->boundary_margin, p->polar_ratio, true, true, presel)))
         return rc;
     return VIO_OK;
 }
@@ -606,7 +733,7 @@ int erp_tracker_run(erp_tracker* t, const erp_klt_params* klt, const erp_tracker
             t->run_graph = nullptr;
         }
         if (use_graph) VIO_HIP(t->ctx, hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        rc = enqueue_run(t, klt, p, n, radius);
+        rc = enqueue_run(t, klt, p, n, radius, use_graph);
         if (use_graph) {
             hipGraph_t g = nullptr;
             hipError_t e = hipStreamEndCapture(st, &g);
@@ -633,6 +760,7 @@ int erp_tracker_sync(erp_tracker* t) {
     if (!t) return VIO_EINVAL;
     VIO_DEVICE(t->ctx);
     VIO_HIP(t->ctx, hipStreamSynchronize(t->ctx->stream));
+    VIO_HIP(t->ctx, hipStreamSynchronize(t->side));  // (the presel hand-off leaves the side stream unjoined)
     return VIO_OK;
 }
 

@@ -30,6 +30,7 @@ struct LkArgs {
     int n, win, max_iters;
     float min_eig;
     double eps2;
+    float* bear1;  // [n][3] or null: the bearing of each tracked point (tracker pipeline: RANSAC's input)
 };
 
 struct RansacArgs {
@@ -43,11 +44,14 @@ struct RansacArgs {
     int* n_good;           // device scalar
     float* b0;             // [n][3] bearings of the compacted points
     float* b1;
+    const float* bear0;    // [n][3] or null: every input point's bearings already formed (tracker pipeline: the
+    const float* bear1;    // LK launch); the compaction then copies them instead of evaluating the trigonometry
     int32_t* samples;      // [iters][3]
     const uint32_t* raw;   // [RS_RAW] tempered mt19937 words of `seed` (ransac_raw_kernel)
     int iters;
     uint32_t seed;
     float thresh;
+    float* cmin;           // device scalar: the inlier test's cosine bound for thresh (ransac_cos_bound)
     int* count;            // [iters]
     float* rot;            // [iters][9] each hypothesis' rotation (ransac_hyp), read back for the best
     uint8_t* kept;         // [n] output mask in input order
@@ -96,17 +100,34 @@ struct GfArgs {
     int tiles_x, tiles_y;
     int* lmax_over;                 // device scalar: some tile overflowed its slots
     unsigned int* n_flat;           // device scalar: fill counter of the flattened candidate list
+    // gftt_select_kernel over the presorted prefix of every local maximum (launch_gftt_presel): disc test
+    // and the threshold's upper bound in its pre-filter, `incomplete` when the prefix cannot decide
+    int presel;
+    uint32_t* smax;       // ordered-int max of the tiles' static-region maxima: gftt_lm_hist_kernel reduces it when
+                          // non-null (the presort), the presel pass reads it (its threshold bound)
+    unsigned int* clear;  // gftt_lmax_kernel: words zeroed by its first workgroup (the presort's histogram)
+    int clear_n;
+    // device-side hand-off of the presort's result to the presel pass (no cross-stream event wait between them):
+    // every workgroup of the presort's sort kernel adds 1 to *done after its stores (agent-scope release); the
+    // presel pass polls *wait_ctr until it reaches wait_target (a per-run generation x the sort's grid), then
+    // acquires; on a time-out it reports `incomplete` and the host runs the exact tail after syncing both streams
+    unsigned int* done;
+    const unsigned int* wait_ctr;
+    unsigned int wait_target;
 };
 
 constexpr int LM_TX = 64, LM_TY = 32, LM_CAP = 1024;
 
 constexpr int GF_BUCKETS = 2048;    // float bits >> 20 of a positive response
+constexpr int kPresortWords = GF_BUCKETS + 8;  // the presort's histogram + scalars
+constexpr int kPresortClear = GF_BUCKETS + 6;  // cleared per run (word 6: the monotonic hand-off counter)
 // top-K buffer: the strongest candidates (>= 16 x max_corners of them when the buckets allow) sorted
 // for the greedy selection; a selection that runs dry falls back to the full candidate sort
 constexpr unsigned int GF_TOPK_CAP = 16384;
 // dynamic LDS of the greedy selection (grid of 3 slots x 4 B per min-distance cell, + 4 B chain head per
-// cell), next to its ~15 KB of static LDS; larger grids live in global memory
-constexpr size_t GF_SELECT_LDS_MAX = 140 * 1024;
+// cell), next to its ~20.4 KB of static LDS (the presel stage buffer included) within the CU's 160 KB;
+// larger grids live in global memory
+constexpr size_t GF_SELECT_LDS_MAX = 136 * 1024;
 
 struct DiscArgs {
     const float* pts;       // [n][2]
@@ -125,12 +146,17 @@ hipError_t launch_pyr_down(const PyrLevelPair& s, const PyrLevelPair& d, int fra
 struct LkAux {
     uint32_t* raw;
     uint32_t seed;
+    float thresh;  // RANSAC angle threshold: its cosine bound into *cmin (beside the raw draws)
+    float* cmin;
     unsigned int* hist;
     unsigned long long* topk;
     unsigned int topk_cap;
     int* scal;
     uint32_t* disc;
     size_t disc_words;  // total 32-bit words of the bitmap
+    const float* pts;   // the previous points' bearings (RANSAC's input) into bear0 [n][3] (null: none)
+    float* bear0;
+    int n, W, H;
 };
 hipError_t launch_lk(const LkArgs& a, hipStream_t st, const LkAux* aux = nullptr);
 // the tempered mt19937 stream of a seed (independent of the points: may run on another stream)
@@ -139,7 +165,16 @@ size_t ransac_raw_words();
 // gen_samples: hypotheses drawn on device from r.raw (launch_ransac_raw of r.seed must precede)
 hipError_t launch_ransac(const RansacArgs& r, bool gen_samples, hipStream_t st);
 hipError_t launch_disc_mask(const DiscArgs& d, int max_pts, hipStream_t st);
+// tracker pipeline: sampler (with the input compaction), hypotheses, then selection + discs in one launch
+hipError_t launch_ransac_pipeline(const RansacArgs& r, const DiscArgs& d, hipStream_t st);
 // fast path (top-K) and the exact fallback over every candidate (used when `incomplete` is raised)
+// presort (side stream, after pass 1, before the disc mask): histogram, top-K cut and sort of EVERY local
+// maximum of the static region (g: the pass-1 arguments with the presort's hist / topk / n_top / cut and a
+// zero max_ord, no disc bitmap); presel: the greedy pass over that prefix with the disc test (g: the full
+// arguments with presel = 1 and the presort's cut)
+hipError_t launch_gftt_presort(const GfArgs& g, hipStream_t st);
+hipError_t launch_gftt_presel(const GfArgs& g, const unsigned long long* keys, const unsigned int* n_keys,
+                              hipStream_t st);
 hipError_t launch_gftt_eig(const GfArgs& g, hipStream_t st);  // the min-eigenvalue map (needs img, W, H, pitch, eig)
 hipError_t launch_gftt(const GfArgs& g, void* sort_tmp, size_t sort_tmp_bytes, hipStream_t st);  // after the map
 hipError_t launch_gftt_full(const GfArgs& g, unsigned int count, void* sort_tmp, size_t sort_tmp_bytes,

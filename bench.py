@@ -486,6 +486,7 @@ def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
     stage["total_with_stage_markers"] = stage.pop("total")
     stage["total"] = total
     res = t.download()
+    fb = t.gftt_fallbacks()
     t.close()
     mpx = W * H / 1e6
     alg_bytes = 2.0 * W * H  # each u8 frame read once
@@ -497,6 +498,7 @@ def klt_bench(vio, synth, ctx, steps, warmup, cpu_seconds, want_cpu):
         "device_ms_per_step": stage["total"],
         "stage_ms": stage,
         "tracked": int(res["status"].sum()),
+        "gftt_fallbacks": dict(zip(("exact_tail", "full_sort"), fb)),
         "kept": int(res["kept"].sum()),
         "new_corners": int(len(res["corners"])),
         "roofline": {

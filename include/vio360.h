@@ -458,6 +458,10 @@ int erp_tracker_stage_ms(erp_tracker* t, double* pyr_ms, double* lk_ms, double* 
 /* on (default): runs record the per-stage events; off: only the pipeline's start and end (each event
    marker costs the stream a few microseconds) */
 int erp_tracker_set_stage_timing(erp_tracker* t, int on);
+/* GFTT fallbacks taken by erp_tracker_download since the tracker was created: exact_tail = runs whose greedy
+   pass over the presorted local maxima could not decide (the masked-maximum tail ran after the download's
+   sync), full_sort = runs whose top-K candidate prefix could not decide (every candidate sorted) */
+int erp_tracker_gftt_fallbacks(erp_tracker* t, int* exact_tail, int* full_sort);
 void erp_tracker_destroy(erp_tracker* t);
 
 /* ------------------------------------------------------------------------------------------ */

@@ -168,7 +168,9 @@ def test_pipeline_full_size_config1(vio, gpu_ctx, synth):
     t.set_points(pts)
     t.run(prm, klt)
     res = t.download()
+    fb = t.gftt_fallbacks()
     t.close()
+    assert fb == (0, 0)  # the bench's configuration: decided by the presorted greedy pass on the device
     truth = synth.erp_flow_truth(pts, Wf, Hf, R21)
     ok = res["status"] == 1
     assert ok.mean() > 0.95
@@ -177,6 +179,34 @@ def test_pipeline_full_size_config1(vio, gpu_ctx, synth):
     nxt, st, kept, corners = pipeline_oracle(vio, a, b, pts, prm, klt)
     assert np.array_equal(res["next"], nxt) and np.array_equal(res["kept"], kept)
     assert np.array_equal(res["corners"], corners)
+
+
+@pytest.mark.parametrize("npts,max_corners,quality,tail", [(300, 1000, 0.01, 1), (300, 300, 0.3, 1), (300, 4, 0.01, 1),
+                                                            (100, 20, 0.01, 0), (40, 4, 0.01, 0)])
+def test_pipeline_presel_cases_bitwise(vio, gpu_ctx, pair, npts, max_corners, quality, tail):
+    """The pipeline's GFTT greedy pass runs over the presorted strongest local maxima (side stream, before the
+    discs exist) and hands frames it cannot decide to the exact tail.  On this 960x480 pair 300 tracked points'
+    discs cover the prefix's keys (~2.7 k) but one, so every 300-point case takes the exact tail (more corners
+    than the frame holds, a high quality level, a small max_corners); 100 and 40 points leave enough of the
+    prefix outside the discs to decide on the device.  All give the oracle's corners bit for bit (the expected
+    paths follow a CPU emulation of the prefix: the oracle's eigenvalue map, the bucket cut, the discs)."""
+    a, b, _ = pair
+    pts = oracle_lib.gftt(a, region_mask(W, H), 300, float(np.float32(0.01)), 30.0)[:npts]
+    prm = vio.default_tracker_params(max_corners=max_corners, seed=5)
+    prm.quality = float(np.float32(quality))
+    klt = vio.default_klt_params()
+    t = vio.Tracker(gpu_ctx, W, H, max_points=1024, max_corners=1024)
+    t.upload(0, a)
+    t.upload(1, b)
+    t.set_points(pts)
+    t.run(prm, klt)
+    res = t.download()
+    fb = t.gftt_fallbacks()
+    t.close()
+    nxt, st, kept, corners = pipeline_oracle(vio, a, b, pts, prm, klt)
+    assert np.array_equal(res["kept"], kept)
+    assert np.array_equal(res["corners"], corners)
+    assert fb == (tail, 0)
 
 
 def test_pipeline_graph_replay_bitwise(vio, gpu_ctx, synth):
