@@ -13,6 +13,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <atomic>
 #include <vector>
 
 #include "ctx.h"
@@ -422,6 +423,13 @@ int enqueue_gftt(erp_tracker* t, const uint8_t* img, int pitch, const uint8_t* m
             if (t->presel_flag) {  // the presort's device hand-off instead of the stream join
                 gs.wait_ctr = t->d_hist2 + GF_BUCKETS + 6;
                 gs.wait_target = t->presort_gen * ((t->topk_cap + 63) / 64);
+                // (VIO_TRK_TEST_PRESEL_TIMEOUT=1: the first hand-off of the process waits for a count it never
+                // reaches -- the bounded wait's path, exercised by tests/test_tracker_gpu.py)
+                static std::atomic<int> test_tmo{[] {
+                    const char* v = std::getenv("VIO_TRK_TEST_PRESEL_TIMEOUT");
+                    return v && v[0] == '1' ? 1 : 0;
+                }()};
+                if (test_tmo.exchange(0)) gs.wait_target += 1u << 30;
             }
             e = launch_gftt_presel(gs, t->d_topk2_sorted, t->d_hist2 + GF_BUCKETS, t->ctx->stream);
         } else if (e == hipSuccess) {

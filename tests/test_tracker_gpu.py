@@ -209,6 +209,54 @@ def test_pipeline_presel_cases_bitwise(vio, gpu_ctx, pair, npts, max_corners, qu
     assert fb == (tail, 0)
 
 
+_PRESEL_TIMEOUT_CHILD = r"""
+import importlib, sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+vio = importlib.import_module("360_visual_inertial_odometry_amd")
+synth = importlib.import_module("360_visual_inertial_odometry_amd.synth")
+W, H = 3840, 1920
+a, b, _ = synth.config1(W, H)
+ctx = vio.Context(0)
+mask = np.zeros((H, W), np.uint8)
+mask[int(np.float32(H) * np.float32(0.15)):int(np.float32(H) * np.float32(0.85)), 20:W - 20] = 255
+pts = ctx.gftt(a, mask, 300, float(np.float32(0.01)), 30.0)
+t = vio.Tracker(ctx, W, H, max_points=512, max_corners=512)
+t.upload(0, a)
+t.upload(1, b)
+t.set_points(pts)
+prm = vio.default_tracker_params(max_corners=300, seed=1)
+res = []
+for _ in range(2):
+    t.run(prm)
+    r = t.download()
+    res.append({k: r[k].copy() for k in ("next", "kept", "corners")})
+    print("FALLBACKS", *t.gftt_fallbacks())
+print("SAME", all(np.array_equal(res[0][k], res[1][k]) for k in res[0]), len(res[0]["corners"]))
+t.close()
+ctx.close()
+"""
+
+
+def test_presel_handoff_timeout_takes_the_exact_tail():
+    """The greedy pass's wait for the presort (a device counter polled under a 2 s wall-clock bound) never hangs
+    and never returns a wrong corner set: a one-shot hook makes the first run's target unreachable; that run's
+    pass reports `incomplete`, the download runs the exact tail (one fallback counted) and its corners equal the
+    second, normal run's (decided on the device: no further fallback)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _PRESEL_TIMEOUT_CHILD, root],
+                       env=dict(os.environ, VIO_TRK_TEST_PRESEL_TIMEOUT="1"), capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.split("\n")
+    fb = [x for x in lines if x.startswith("FALLBACKS")]
+    assert fb == ["FALLBACKS 1 0", "FALLBACKS 1 0"], r.stdout
+    same = [x for x in lines if x.startswith("SAME")][0].split()
+    assert same[1] == "True" and int(same[2]) > 0, r.stdout
+
+
 def test_pipeline_graph_replay_bitwise(vio, gpu_ctx, synth):
     """Runs without stage markers (the bench's timed mode; with VIO_TRK_GRAPH=1 captured into a graph
     and replayed) give bitwise the outputs of a run with them, also after the parameter set and the
