@@ -138,3 +138,15 @@ def test_wide_phase_kernels_have_no_scratch(vio):
                     found[w] = kd[".private_segment_fixed_size"]
     assert set(found) == set(want), found
     assert all(v == 0 for v in found.values()), found
+
+
+def test_walk_kernel_fits_five_waves_per_simd(vio):
+    """ph_back_kernel (the 256-window step's largest kernel) stays at <= 96 VGPRs, i.e. five waves per SIMD with
+    its 28.3 KB of LDS (five workgroups per CU): at 110 VGPRs / four waves it took 107 us per launch against
+    98 us (profiles/r6g_ab_back.log)"""
+    blob = open(vio.lib()._name, "rb").read()
+    found = [kd for co in _gfx950_code_objects(blob) for kd in _kernel_descriptors(co)
+             if "ph_back_kernelE" in kd[".name"]]
+    assert len(found) == 1, [kd[".name"] for kd in found]
+    assert found[0][".vgpr_count"] <= 96, found[0][".vgpr_count"]
+    assert found[0][".group_segment_fixed_size"] * 5 <= 160 * 1024, found[0][".group_segment_fixed_size"]
