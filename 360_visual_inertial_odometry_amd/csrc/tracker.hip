@@ -1784,15 +1784,16 @@ template <int TY>  // tile height: eig rows [oy-1, oy+TY+1), cov rows [oy-2, oy+
 struct LmShared {
     static constexpr int CH = TY + 4, EH = TY + 2, SH = TY + 6;
     uint8_t src[SH][LM_SRC_W];
-    float cov[CH][LM_CW][3];
+    float d[2][CH][LM_CW];  // the scaled Sobel derivatives dx, dy (planar); the box sums form their products
     float eig[EH][LM_EW];
 };
 
 
 // Tiles whose eig positions all lie at least one pixel inside the image (no reflected box positions):
 // the Sobel sums roll down a column (three source reads per cov position instead of nine: the
-// horizontal difference / smoothing of each source row kept for the next two), cov in planar LDS, and
-// eig from rolling vertical sums of horizontal triple sums (nine cov reads per position instead of 27).
+// horizontal difference / smoothing of each source row kept for the next two), dx / dy in planar LDS (2
+// floats per position instead of the 3 products: 4 workgroups per CU), and eig from rolling vertical sums
+// of horizontal triple sums of the products (the same f32 products dx*dx, dx*dy, dy*dy as before).
 // The box sums are exact, so any summation order gives the ky / kx order's bits: each f32 product is a
 // multiple of 2^-47 (|Sobel| <= 1020 and the scale 1/3060 make a nonzero product >= scale^2 > 2^-24,
 // whose ulp is >= 2^-47) below 1/8 in magnitude, so every partial sum of nine fits 53 bits.
@@ -1800,7 +1801,7 @@ template <int TY>
 __device__ void lm_eig_interior(LmShared<TY>& S) {
     constexpr int CH = LmShared<TY>::CH, EH = LmShared<TY>::EH, CG = 3;  // CG row groups per column
     static_assert(CG * LM_CW <= 256 && CG * LM_EW <= 256, "one column of a row group per thread");
-    float(*cv)[CH][LM_CW] = reinterpret_cast<float(*)[CH][LM_CW]>(&S.cov[0][0][0]);
+    float(*cv)[CH][LM_CW] = S.d;
     const float scale = (float)(1.0 / 3060.0);
     const int t = threadIdx.x;
     if (t < CG * LM_CW) {  // cov column cx (image x = ox-2+cx: source columns cx+13 .. cx+15), rows [r0, r1)
@@ -1818,10 +1819,8 @@ __device__ void lm_eig_interior(LmShared<TY>& S) {
             d[2] = r[c0 + 2] - r[c0];
             m[2] = r[c0] + 2 * r[c0 + 1] + r[c0 + 2];
             const int sx = d[0] + 2 * d[1] + d[2], sy = m[2] - m[0];
-            const float dx = (float)sx * scale, dy = (float)sy * scale;
-            cv[0][cy][cx] = dx * dx;
-            cv[1][cy][cx] = dx * dy;
-            cv[2][cy][cx] = dy * dy;
+            cv[0][cy][cx] = (float)sx * scale;
+            cv[1][cy][cx] = (float)sy * scale;
             d[0] = d[1]; d[1] = d[2];
             m[0] = m[1]; m[1] = m[2];
         }
@@ -1831,8 +1830,16 @@ __device__ void lm_eig_interior(LmShared<TY>& S) {
         const int ex = t % LM_EW, g = t / LM_EW, e0 = g * EH / CG, e1 = (g + 1) * EH / CG;
         double h[3][3];  // [cov row slot][component]: horizontal triple sums
         auto hsum = [&](int cy, double* o) {
+            float p[3][3];  // [column][component]: dx*dx, dx*dy, dy*dy
 #pragma unroll
-            for (int j = 0; j < 3; ++j) o[j] = ((double)cv[j][cy][ex] + (double)cv[j][cy][ex + 1]) + (double)cv[j][cy][ex + 2];
+            for (int i = 0; i < 3; ++i) {
+                const float dx = cv[0][cy][ex + i], dy = cv[1][cy][ex + i];
+                p[i][0] = dx * dx;
+                p[i][1] = dx * dy;
+                p[i][2] = dy * dy;
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j) o[j] = ((double)p[0][j] + (double)p[1][j]) + (double)p[2][j];
         };
         hsum(e0, h[0]);
         hsum(e0 + 1, h[1]);
@@ -1891,10 +1898,8 @@ __device__ void lm_eig_tile(const GfArgs& G, int ox, int oy, LmShared<TY>& S) {
         const int c0 = cx + 13, c1 = cx + 14, c2 = cx + 15;
         const int sx = (r0[c2] - r0[c0]) + 2 * (r1[c2] - r1[c0]) + (r2[c2] - r2[c0]);
         const int sy = (r2[c0] + 2 * r2[c1] + r2[c2]) - (r0[c0] + 2 * r0[c1] + r0[c2]);
-        const float dx = (float)sx * scale, dy = (float)sy * scale;
-        S.cov[cy][cx][0] = dx * dx;
-        S.cov[cy][cx][1] = dx * dy;
-        S.cov[cy][cx][2] = dy * dy;
+        S.d[0][cy][cx] = (float)sx * scale;
+        S.d[1][cy][cx] = (float)sy * scale;
     }
     __syncthreads();
     for (int e = threadIdx.x; e < LM_EW * LM_EH; e += 256) {
@@ -1908,16 +1913,18 @@ __device__ void lm_eig_tile(const GfArgs& G, int ox, int oy, LmShared<TY>& S) {
         if (X >= 1 && X < W - 1 && Y >= 1 && Y < H - 1) {
             for (int ky = 0; ky < 3; ++ky)
                 for (int kx = 0; kx < 3; ++kx) {
-                    const float* c = S.cov[ey + ky][ex + kx];
-                    s0 += c[0]; s1 += c[1]; s2 += c[2];
+                    const float dx = S.d[0][ey + ky][ex + kx], dy = S.d[1][ey + ky][ex + kx];
+                    const float c0 = dx * dx, c1 = dx * dy, c2 = dy * dy;
+                    s0 += c0; s1 += c1; s2 += c2;
                 }
         } else {
             for (int ky = -1; ky <= 1; ++ky) {
                 const int yy = reflect101(Y + ky, H) - (oy - 2);
                 for (int kx = -1; kx <= 1; ++kx) {
                     const int xx = reflect101(X + kx, W) - (ox - 2);
-                    const float* c = S.cov[yy][xx];
-                    s0 += c[0]; s1 += c[1]; s2 += c[2];
+                    const float dx = S.d[0][yy][xx], dy = S.d[1][yy][xx];
+                    const float c0 = dx * dx, c1 = dx * dy, c2 = dy * dy;
+                    s0 += c0; s1 += c1; s2 += c2;
                 }
             }
         }
@@ -1941,7 +1948,9 @@ __device__ __forceinline__ uint32_t lm_block_max(uint32_t m, uint32_t* red) {
 // pass 1: per tile, the 3x3 local maxima inside the static region and the region's maximum
 __global__ void __launch_bounds__(256) gftt_lmax_kernel(GfArgs G) {
     __shared__ LmShared<LM_TY> S;
-    __shared__ unsigned long long keys[LM_CAP];
+    // the tile's local maxima over the derivative planes (dead once the eigenvalues are formed): 4 workgroups per CU
+    static_assert(sizeof(S.d) >= LM_CAP * sizeof(unsigned long long) && offsetof(LmShared<LM_TY>, d) % 8 == 0, "keys in S.d");
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(&S.d[0][0][0]);
     __shared__ unsigned int s_cnt;
     __shared__ uint32_t red[4];
     const int tile = xcd_tile(blockIdx.x, G.tiles_x * G.tiles_y);
