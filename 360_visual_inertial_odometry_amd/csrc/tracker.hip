@@ -2368,8 +2368,13 @@ hipError_t launch_gftt_after_lmax(const GfArgs& g, void* sort_tmp, size_t sort_t
     return launch_select(g, (const unsigned long long*)g.topk_sorted, (const unsigned int*)g.n_top, g.topk_cap, 1, st);
 }
 hipError_t launch_gftt_presort(const GfArgs& g, hipStream_t st) {
-    hipLaunchKernelGGL(gftt_lm_hist_kernel, dim3(256), dim3(256), 0, st, g);
-    hipLaunchKernelGGL(gftt_lm_topk_kernel, dim3(256), dim3(256), 0, st, g);
+    // grid sizes (experiment overrides VIO_TRK_HIST_WGS / VIO_TRK_TOPK_WGS): the histogram on 128 workgroups -- half
+    // the workgroups' LDS-histogram flushes beside the RANSAC kernels: config-1 pipeline 0.166-0.169 -> 0.160-0.164
+    // ms (64: 0.165, 32: 0.179, 512: 0.179; profiles/r6l_ab_hist_grid.log); the gather stays at 256
+    static const int hw = [] { const char* v = std::getenv("VIO_TRK_HIST_WGS"); return v ? std::max(1, std::atoi(v)) : 128; }();
+    static const int tw = [] { const char* v = std::getenv("VIO_TRK_TOPK_WGS"); return v ? std::max(1, std::atoi(v)) : 256; }();
+    hipLaunchKernelGGL(gftt_lm_hist_kernel, dim3(hw), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gftt_lm_topk_kernel, dim3(tw), dim3(256), 0, st, g);
     hipLaunchKernelGGL(gftt_topk_sort_kernel<4>, dim3((g.topk_cap + 63) / 64), dim3(64 * 4), 0, st, g);
     return hipGetLastError();
 }
