@@ -2082,13 +2082,28 @@ __global__ void __launch_bounds__(256) gftt_lm_hist_kernel(GfArgs G) {
     const int n_tiles = G.tiles_x * G.tiles_y;
     unsigned int cnt = 0;
     uint32_t sm = 0;  // (the presort: the static region's maximum over the wave's tiles)
-    for (int tile = blockIdx.x * 4 + wid; tile < n_tiles; tile += gridDim.x * 4) {
+    // the tile's count and its first 64 key slots are requested together (the slots lie inside the tile's
+    // LM_CAP block; those at or past the count are read and ignored), the next tile's one step ahead
+    const int stride = gridDim.x * 4;
+    int tile = blockIdx.x * 4 + wid;
+    unsigned int nk_n = 0;
+    unsigned long long k_n = 0ull;
+    if (tile < n_tiles) {
+        nk_n = G.lmax_n[tile];
+        k_n = G.lmax[(size_t)tile * LM_CAP + lane];
+    }
+    for (; tile < n_tiles; tile += stride) {
+        const unsigned int nk = nk_n;
+        const unsigned long long k0 = k_n;
+        if (tile + stride < n_tiles) {
+            nk_n = G.lmax_n[tile + stride];
+            k_n = G.lmax[(size_t)(tile + stride) * LM_CAP + lane];
+        }
         if (G.smax) sm = max(sm, G.tile_max[tile]);
-        const unsigned int nk = G.lmax_n[tile];
         if (nk > LM_CAP && lane == 0) *G.lmax_over = 1;
         const unsigned long long* keys = G.lmax + (size_t)tile * LM_CAP;
         for (unsigned int i = lane; i < min(nk, (unsigned int)LM_CAP); i += 64) {
-            const unsigned long long k = keys[i];
+            const unsigned long long k = i < 64 ? k0 : keys[i];
             if (lm_survives(G, k, thr)) {
                 atomicAdd(&h[(unsigned int)(k >> 52)], 1u);
                 ++cnt;
