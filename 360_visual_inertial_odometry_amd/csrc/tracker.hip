@@ -2286,8 +2286,9 @@ static hipError_t launch_select(const GfArgs& g, const unsigned long long* keys,
 // waves counts over one sixteenth of the list, staged through LDS in 512-key chunks (coalesced 8-key-per-
 // lane loads of the next chunk in flight while the current one is compared; ds_read_b128 broadcasts,
 // two comparands per read); the partial counts are summed in LDS and the key written to its position.
-// TS_WAVES = 16 for the masked tail's top-K (~5 k keys); the presort's prefix (~2-4 k keys) uses 4-wave
-// workgroups (its 256-workgroup grid of 16-wave ones took 13 us, most of it launching idle workgroups)
+// TS_WAVES = 16 for the masked tail's top-K (~5 k keys); the presort's prefix (~2-4 k keys) uses 8-wave
+// workgroups: 17 -> 11.5 us against 4-wave ones beside the RANSAC kernels (config-1 pipeline 0.159-0.163 ->
+// 0.154-0.156 ms; 16 waves 0.158-0.160 ms: profiles/r6x_ab_presort_sort_waves.log)
 constexpr int TS_CHUNK = 512;
 template <int TS_WAVES>
 __global__ void __launch_bounds__(64 * TS_WAVES) gftt_topk_sort_kernel(GfArgs G) {
@@ -2390,7 +2391,7 @@ hipError_t launch_gftt_presort(const GfArgs& g, hipStream_t st) {
     static const int tw = [] { const char* v = std::getenv("VIO_TRK_TOPK_WGS"); return v ? std::max(1, std::atoi(v)) : 256; }();
     hipLaunchKernelGGL(gftt_lm_hist_kernel, dim3(hw), dim3(256), 0, st, g);
     hipLaunchKernelGGL(gftt_lm_topk_kernel, dim3(tw), dim3(256), 0, st, g);
-    hipLaunchKernelGGL(gftt_topk_sort_kernel<4>, dim3((g.topk_cap + 63) / 64), dim3(64 * 4), 0, st, g);
+    hipLaunchKernelGGL(gftt_topk_sort_kernel<8>, dim3((g.topk_cap + 63) / 64), dim3(64 * 8), 0, st, g);
     return hipGetLastError();
 }
 hipError_t launch_gftt_presel(const GfArgs& g, const unsigned long long* keys, const unsigned int* n_keys,
