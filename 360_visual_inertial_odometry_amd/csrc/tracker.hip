@@ -2128,6 +2128,20 @@ __global__ void __launch_bounds__(256) gftt_lm_topk_kernel(GfArgs G) {
     __shared__ unsigned int s_n, s_base;
     __shared__ CutShared cs;
     if (threadIdx.x == 0) s_n = 0;
+    // the first tile's bucket bound, count and first 64 key slots requested before the cut is formed (the slots
+    // lie inside the tile's LM_CAP block; those past the count are ignored), the next tile's one step ahead
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n_tiles = G.tiles_x * G.tiles_y;
+    const int stride = gridDim.x * 4;
+    int tile = blockIdx.x * 4 + wid;
+    uint32_t km_n = 0;
+    unsigned int nk_n = 0;
+    unsigned long long k_n = 0ull;
+    if (tile < n_tiles) {
+        km_n = G.tile_kmax[tile];
+        nk_n = G.lmax_n[tile];
+        k_n = G.lmax[(size_t)tile * LM_CAP + lane];
+    }
     unsigned int below_empty;
     const unsigned int cut = (unsigned int)gftt_cut_block(G, cs, below_empty);  // (its barriers order s_n = 0)
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the selection pass
@@ -2135,18 +2149,23 @@ __global__ void __launch_bounds__(256) gftt_lm_topk_kernel(GfArgs G) {
         G.cut[1] = (int)below_empty;
     }
     const float thr = lm_threshold(G);
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n_tiles = G.tiles_x * G.tiles_y;
-    for (int tile = blockIdx.x * 4 + wid; tile < n_tiles; tile += gridDim.x * 4) {
-        if (G.tile_kmax[tile] < cut) continue;  // no key of the tile reaches the cut bucket
-        const unsigned int nk = min(G.lmax_n[tile], (unsigned int)LM_CAP);
+    for (; tile < n_tiles; tile += stride) {
+        const uint32_t km = km_n;
+        const unsigned int nk = min(nk_n, (unsigned int)LM_CAP);
+        const unsigned long long k0 = k_n;
+        if (tile + stride < n_tiles) {
+            km_n = G.tile_kmax[tile + stride];
+            nk_n = G.lmax_n[tile + stride];
+            k_n = G.lmax[(size_t)(tile + stride) * LM_CAP + lane];
+        }
+        if (km < cut) continue;  // no key of the tile reaches the cut bucket
         const unsigned long long* keys = G.lmax + (size_t)tile * LM_CAP;
         for (unsigned int i0 = 0; i0 < nk; i0 += 64) {  // wave-uniform trip count
             const unsigned int i = i0 + lane;
             unsigned long long k = 0ull;
             bool take = false;
             if (i < nk) {
-                k = keys[i];
+                k = i0 == 0 ? k0 : keys[i];
                 take = (unsigned int)(k >> 52) >= cut && lm_survives(G, k, thr);
             }
             const unsigned long long bal = __ballot(take);
